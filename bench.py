@@ -1,0 +1,168 @@
+"""Benchmark: the Stage-4 uncertainty-guided training step on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
+
+Workload (BASELINE.json configs[1], weak-scaled for N > 1): per GPU a batch of
+16 synthetic 3x256x256 images ~N(0,1) with Bernoulli(0.5) masks; one step =
+UncertaintyGuidedProgressiveTrainer.train_step at stage 4 =
+PGUNet4 train forward + PGUNet3 eval forward at 128^2 for the uncertainty map +
+uncertainty-weighted BCE + backward + RCCL gradient all-reduce (N > 1) +
+RMSprop + Dice/accuracy, with one host synchronisation per step (as the
+trainer does).  Random-init weights of the reference architecture, fp32.
+
+Prints ONE JSON line (rank 0).  `roofline` is measured live: every launch of
+the conv kernels inside the timed region is bracketed by HIP events on the
+launching stream; achieved = algorithmic FLOPs / kernel time for the dominant
+kernel.  `cpu_baseline` times the CPU oracle (oracle/ref_cpu.py: the
+reference's torch CPU ops, same order) on a bounded sample on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path[:0] = [str(ROOT), str(ROOT / "ug-pg-unet_amd")]
+
+METRIC = "images/sec Stage-4 256×256 bs16 fwd+bwd at 1/2/4/8 MI355X; Dice vs ref"
+FP32_PEAK_TFLOPS = 157.3  # MI355X dense FP32 (matrix = vector rate), MI355X_MICROARCH.md
+UG_STEP_GFLOP = 225.2866  # per image, SURVEY.md §8d
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=16, help="images per GPU")
+    ap.add_argument("--res", type=int, default=256)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--no-roofline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(batch, res, steps, threads):
+    """Time the CPU oracle's UG step (bounded sample) on this host."""
+    import torch
+    from oracle import detgen as G
+    from oracle import ref_cpu as O
+    torch.set_num_threads(threads)
+    cur = G.make_state(O.state_spec(4, 3, 1), 0)
+    prev = G.make_state(O.state_spec(3, 3, 1), 1)
+    sq = {k: torch.zeros_like(v) for k, v in cur.items() if v.is_floating_point() and not O._is_buffer(k)}
+    x = G.randn(1, (batch, 3, res, res), "x")
+    t = G.bernoulli(2, (batch, 1, res, res), 0.5, "t")
+    O.ug_train_step(4, cur, prev, x, t, sq, 1e-4)  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        O.ug_train_step(4, cur, prev, x, t, sq, 1e-4)
+    dt = time.perf_counter() - t0
+    return {"value": round(batch * steps / dt, 4), "unit": "images/sec", "cores": threads,
+            "kind": "port",
+            "sample": f"{steps} oracle UG steps (bs{batch} {res}^2, S4 fwd+bwd + S3 U-map + RMSprop) "
+                      f"after 1 warm-up, torch CPU fp32, {threads} threads"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import ugpg
+    from ugpg import ops
+    from ugpg.dist import broadcast_parameters, init_from_env, max_over_ranks
+
+    rank, world = init_from_env("nccl")
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but world size {world}", file=sys.stderr)
+
+    torch.manual_seed(1234)
+    tr = ugpg.UncertaintyGuidedProgressiveTrainer(3, 1, device=dev, uncertainty_alpha=1.0)
+    tr.current_stage = 4
+    tr.current_model = tr.models[4]
+    tr.setup_optimizer(4)
+    for s in (3, 4):
+        broadcast_parameters(tr.models[s])
+    B, R = args.batch, args.res
+    g = torch.Generator().manual_seed(100 + rank)
+    x = torch.randn(B, 3, R, R, generator=g).to(dev)
+    t = (torch.rand(B, 1, R, R, generator=g) < 0.5).float().to(dev)
+    tr.current_model.train()
+    tr.models[3].eval()
+
+    def step():
+        mbuf = tr.train_step(x, t, 4)
+        return mbuf.tolist()
+
+    for _ in range(args.warmup):
+        last = step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    timer = None if args.no_roofline else ops.KernelTimer()
+    ops.TIMER = timer
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        last = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ops.TIMER = None
+    elapsed = max_over_ranks(elapsed, dev)
+    ms = 1000 * elapsed / args.steps
+    value = world * B * args.steps / elapsed
+
+    roof = None
+    kernels = None
+    if timer is not None:
+        summ = timer.summary()
+        kernels = {k: {"launches": v["launches"], "ms_per_step": round(v["ms"] / args.steps, 3),
+                       "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2)}
+                   for k, v in summ.items()}
+        dom = max(summ, key=lambda k: summ[k]["ms"])
+        d = summ[dom]
+        achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
+        roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2),
+                "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                "flops_per_launch": round(d["flops"] / d["launches"]),
+                "avg_launch_ms": round(d["ms"] / d["launches"], 4)}
+
+    result = {
+        "metric": METRIC, "value": round(value, 3), "unit": "images/sec", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (x~N(0,1), masks~Bernoulli(0.5); random-init weights)",
+        "config": {"workload": "Stage-4 uncertainty-guided train step: PGUNet4 fwd+bwd 256^2 + "
+                               "PGUNet3 eval fwd 128^2 (U-map) + weighted BCE + RMSprop",
+                   "per_gpu_batch": B, "global_batch": B * world, "resolution": R,
+                   "parallelism": f"dp{world}", "baseline_config": "BASELINE.json configs[1]"},
+        "step_roofline": {"gflop_per_image": UG_STEP_GFLOP,
+                          "achieved_tflops_per_gpu": round(value / world * UG_STEP_GFLOP / 1e3, 2),
+                          "frac_of_fp32_peak": round(value / world * UG_STEP_GFLOP / 1e3 / FP32_PEAK_TFLOPS, 4)},
+        "roofline": roof,
+        "kernels": kernels,
+        "last_step_metrics": {"loss": last[0], "base_loss": last[1], "dice": last[2],
+                              "unc_mean": last[5], "unc_std": last[6]},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+        result["cpu_baseline"] = cpu_baseline(B, R, args.cpu_steps, threads)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

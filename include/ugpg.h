@@ -1,0 +1,222 @@
+/*
+ * ugpg.h -- C-ABI of libugpg.so, the MI355X (gfx950) hot path of the
+ * Uncertainty-Guided Progressive U-Net (reference: tridang04022004/UG-PG-UNet).
+ *
+ * The reference has no FFI: all of its hot-path arithmetic is PyTorch ATen
+ * calls made from Python.  Each entry point below
+ * replaces one family of those calls; the reference call site it replaces is
+ * cited next to it.  The Python host layer (ug-pg-unet_amd/ugpg/_C.py) binds
+ * these with ctypes and keeps the reference's module/trainer API on top.
+ *
+ * Conventions
+ *  - Plain pointers + sizes only; no torch types cross this boundary.
+ *  - Activations are NHWC fp32 ([B][H][W][C], C fastest) unless an entry says NCHW.
+ *  - Every entry returns 0 on success or a negative UGPG_ERR_* code; the message is
+ *    in ugpg_last_error() (thread-local).  No C++ exception crosses the ABI.
+ *  - `stream` is a hipStream_t (torch.cuda.current_stream().cuda_stream).  All work
+ *    is stream-ordered; nothing allocates, frees or synchronises (graph-capturable).
+ *  - The caller owns every buffer, including workspaces sized by *_workspace().
+ */
+#ifndef UGPG_H_
+#define UGPG_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define UGPG_OK 0
+#define UGPG_ERR_INVALID (-1)     /* bad argument / unsupported shape */
+#define UGPG_ERR_LAUNCH (-2)      /* hipGetLastError after a launch */
+#define UGPG_ERR_WORKSPACE (-3)   /* workspace too small */
+
+const char* ugpg_version(void);
+const char* ugpg_last_error(void);
+
+/* A lazily-activated NHWC operand: value = relu(scale[c]*x + shift[c]) when
+ * scale != NULL (train/eval BatchNorm + ReLU folded into the consumer's load,
+ * UG_unet_parts.py:11-12,14-15), else x.  `C` is the channel count (stride). */
+typedef struct {
+    const float* data;
+    const float* scale;
+    const float* shift;
+    int C;
+} ugpg_src_t;
+
+/* ---- 3x3 convolution, padding 1, stride 1 (UG_unet_parts.py:10,13) ---------
+ * Implicit GEMM on v_mfma_f32_32x32x2_f32 with LDS-staged halo tiles.
+ * Input = channel-concat of src[0] and src[1] (src[1].data may be NULL):
+ * this is the concat-free `torch.cat([x2, x1], dim=1)` of Up (UG_unet_parts.py:80).
+ * Cin = src[0].C + src[1].C must be a multiple of 8 (pad the image to 8 channels).
+ * Output channels [0, out_split) go to out[0] (channel stride out_split) and
+ * [out_split, Cout) to out[1] (stride Cout - out_split); out_split == Cout for one
+ * output.  accumulate[i] != 0 adds into out[i].  When `stats` != NULL the kernel
+ * also writes per-tile BatchNorm partials [3][Cout][ntiles] = (count, sum, M2)
+ * for ugpg_bn_finalize. */
+typedef struct {
+    int B, H, W;
+    ugpg_src_t src[2];
+    const float* wpk;      /* packed by ugpg_pack_conv3x3 */
+    const float* bias;     /* [Cout] or NULL */
+    int Cout;
+    float* out[2];
+    int out_split;
+    int accumulate[2];
+    float* stats;
+} ugpg_conv_t;
+
+/* Replaces aten::convolution forward (cuDNN/oneDNN) for DoubleConv's 3x3 convs. */
+int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream);
+/* number of BatchNorm partial tiles the forward writes (size stats as 3*Cout*ntiles) */
+int ugpg_conv3x3_fwd_ntiles(int B, int H, int W, int Cin, int Cout);
+
+/* Weight repack from OIHW fp32 [Cout][Cin][3][3].
+ *  mode 0 (forward):  wpk[Cin_pad/8][9][Cout][8],    wpk = W[co][ci][t]
+ *  mode 1 (dgrad):    wpk[Cout/8][9][Cin_pad][8],    wpk = W[co][ci][8-t]
+ *    (the data-gradient of a 3x3/p1 conv is the forward conv of dY with the
+ *     180-degree-rotated, channel-transposed kernel; replaces aten
+ *     convolution_backward's grad_input) */
+int ugpg_pack_conv3x3(const float* w_oihw, float* wpk, int Cout, int Cin, int Cin_pad,
+                      int mode, void* stream);
+
+/* Weight gradient (aten convolution_backward grad_weight/grad_bias, K3):
+ *   dw[co][ci][ky][kx] (+)= sum_p dy[p][co] * act(x)[p + (ky-1,kx-1)][ci]
+ *   db[co] (+)= sum_p dy[p][co]
+ * Deterministic split-K over pixel tiles (no float atomics). dw is OIHW with
+ * Cin_real input channels (<= the padded Cin of src). */
+typedef struct {
+    int B, H, W;
+    ugpg_src_t src[2];
+    const float* dy;       /* NHWC [B][H][W][Cout] */
+    int Cout;
+    float* dw;
+    int Cin_real;
+    float* db;             /* [Cout] or NULL */
+    int accumulate;
+} ugpg_wgrad_t;
+size_t ugpg_conv3x3_wgrad_workspace(const ugpg_wgrad_t* p);
+int ugpg_conv3x3_wgrad(const ugpg_wgrad_t* p, void* ws, size_t ws_bytes, void* stream);
+
+/* ---- BatchNorm2d (eps, momentum) -------------------------------------------
+ * Train: combine the conv's tile partials (Chan merge in fp64), produce
+ * mean/invstd and the folded (scale, shift) = (g*invstd, b - mean*g*invstd),
+ * update running stats with the unbiased variance, num_batches_tracked += 1.
+ * Replaces aten::native_batch_norm (train) at UG_unet_parts.py:11,14 (K4). */
+int ugpg_bn_finalize(const float* stats, int ntiles, int C, const float* gamma,
+                     const float* beta, float* running_mean, float* running_var,
+                     int64_t* num_batches_tracked, float momentum, float eps,
+                     float* mean, float* invstd, float* scale, float* shift, void* stream);
+/* Eval: (scale, shift) from running stats (K5). */
+int ugpg_bn_eval_params(const float* gamma, const float* beta, const float* running_mean,
+                        const float* running_var, float eps, int C, float* scale,
+                        float* shift, void* stream);
+/* Backward of relu(bn(y)) given da = dL/d(relu output) (K6+K7):
+ *   g = da * [scale*y+shift > 0];  dgamma = sum g*xhat;  dbeta = sum g
+ *   dy = scale * (g - mean(g) - xhat*mean(g*xhat))
+ * dy may alias da.  dgamma/dbeta written (or accumulated). */
+size_t ugpg_bn_relu_bwd_workspace(int64_t npix, int C);
+int ugpg_bn_relu_bwd(const float* da, const float* y, int64_t npix, int C, const float* mean,
+                     const float* invstd, const float* scale, const float* shift,
+                     float* dy, float* dgamma, float* dbeta, int accumulate_params,
+                     void* ws, size_t ws_bytes, void* stream);
+/* Materialise relu(scale*y+shift) (used only for the standalone block API). */
+int ugpg_bn_relu_apply(ugpg_src_t src, int64_t npix, float* out, void* stream);
+
+/* ---- MaxPool2d(2) (UG_unet_parts.py:49, K8) on an activated source -------- */
+int ugpg_maxpool2_fwd(ugpg_src_t src, int B, int H, int W, float* out, uint8_t* argmax,
+                      void* stream);
+int ugpg_maxpool2_bwd(const float* dout, const uint8_t* argmax, int B, int H, int W, int C,
+                      float* din, int accumulate, void* stream);
+
+/* ---- align_corners=True bilinear resize, NHWC (UG_unet_parts.py:78, K9) ---- */
+int ugpg_bilinear_nhwc_fwd(ugpg_src_t src, int B, int Hi, int Wi, float* out, int Ho, int Wo,
+                           void* stream);
+int ugpg_bilinear_nhwc_bwd(const float* dout, int B, int Ho, int Wo, int C, float* din, int Hi,
+                           int Wi, int accumulate, void* stream);
+
+/* ---- NCHW resize (F.interpolate at uncertainty_guided_trainer.py:208-209,
+ * UG_unet.py:36-53, 419-424; K12/K13)
+ *  mode 0: bilinear align_corners;  mode 1: nearest;
+ *  mode 2: U = 1 - 2|bilinear(sigmoid(in)) - 0.5|  (uncertainty map, UG_unet.py:45-57) */
+int ugpg_resize_nchw(const float* in, int B, int C, int Hi, int Wi, float* out, int Ho, int Wo,
+                     int mode, void* stream);
+/* NCHW <-> NHWC (with zero channel padding to Cpad) */
+int ugpg_nchw_to_nhwc(const float* in, int B, int C, int H, int W, float* out, int Cpad,
+                      void* stream);
+int ugpg_nhwc_to_nchw(const float* in, int B, int C, int H, int W, int Cstride, float* out,
+                      int accumulate, void* stream);
+
+/* ---- deep-supervision heads: 1x1 OutConv + align_corners upsample + sum
+ * (UG_unet_parts.py:84-91, UG_unet.py:294-303; K11) */
+int ugpg_head_fwd(ugpg_src_t src, int64_t npix, const float* w, const float* b, int nc,
+                  float* h, void* stream);
+/* logits[b][k][y][x] (NCHW, HxW) = sum_i up_i(h_i) in order i = 0..n-1; h_i NHWC at
+ * (hres[i] x hres[i]) with nc channels; resolution HxW == finest. */
+int ugpg_heads_combine(const float* const* h, const int* hres, int n, int B, int H, int W,
+                       int nc, float* logits, void* stream);
+/* dh_i = upsample_i^T(dlogits) for every head (NHWC nc channels). */
+int ugpg_heads_split_bwd(const float* dlogits, int B, int H, int W, int nc, float* const* dh,
+                         const int* hres, int n, void* stream);
+size_t ugpg_head_bwd_workspace(int64_t npix, int C, int nc);
+int ugpg_head_bwd(ugpg_src_t src, int64_t npix, const float* w, int nc, const float* dh,
+                  float* dw, float* db, float* da, int accumulate_da, void* ws, size_t ws_bytes,
+                  void* stream);
+
+/* ---- uncertainty-weighted BCE-with-logits (UG_unet.py:61-94, K13) ---------
+ * pixel = (1-t)x + (1+(pw-1)t)*softplus(-x);  final = mean(pixel*(1+alpha*U))
+ * (U == NULL: final = mean(pixel));  out[0]=final, out[1]=mean(pixel).
+ * U is NCHW with Cu channels (1 or C; broadcast over C when Cu == 1). */
+size_t ugpg_ug_loss_workspace(int64_t n);
+int ugpg_ug_loss_fwd(const float* logits, const float* target, const float* umap, int B, int C,
+                     int HW, int Cu, const float* pos_weight, float alpha, float* out,
+                     void* ws, size_t ws_bytes, void* stream);
+/* dlogits = gout[0] * (1+alpha*U) * ((1-t) - (1+(pw-1)t)*sigmoid(-x)) / N */
+int ugpg_ug_loss_bwd(const float* logits, const float* target, const float* umap, int B, int C,
+                     int HW, int Cu, const float* pos_weight, float alpha, const float* gout,
+                     float* dlogits, void* stream);
+/* weighted mean of an arbitrary per-pixel loss (non-BCE criteria) */
+int ugpg_weighted_mean_fwd(const float* pixel_loss, const float* umap, int B, int C, int HW,
+                           int Cu, float alpha, float* out, void* ws, size_t ws_bytes,
+                           void* stream);
+int ugpg_weighted_mean_bwd(const float* umap, int B, int C, int HW, int Cu, float alpha,
+                           const float* gout, float* dpixel, void* stream);
+
+/* ---- trainer metrics (uncertainty_guided_trainer.py:90-123, K14) ----------
+ * pred = sigmoid(x) > 0.5 ; per-sample Dice (2I+1)/(P+T+1) averaged over B;
+ * accuracy = 1 - #(pred != trunc(t)) / (B*HW).  out = [dice, acc, wrong_count]. */
+size_t ugpg_seg_metrics_workspace(int B);
+int ugpg_seg_metrics(const float* logits, const float* target, int B, int HW, float* out,
+                     void* ws, size_t ws_bytes, void* stream);
+/* mean and unbiased std of n floats: out = [mean, std] (torch.mean/torch.std) */
+size_t ugpg_mean_std_workspace(int64_t n);
+int ugpg_mean_std(const float* x, int64_t n, float* out, void* ws, size_t ws_bytes,
+                  void* stream);
+
+/* ---- RMSprop (torch.optim.RMSprop rule, uncertainty_guided_trainer.py:84-88, K15)
+ * g = grad*grad_scale + wd*p;  v = alpha*v + (1-alpha)*g^2;  p -= lr*g/(sqrt(v)+eps) */
+int ugpg_rmsprop_step(float* param, const float* grad, float* square_avg, int64_t n, float lr,
+                      float alpha, float eps, float weight_decay, float grad_scale,
+                      void* stream);
+
+/* ---- Herlev classifier head (Herlev/train_herlev.py:66-77, K16) ----------- */
+/* global average pool of an activated NHWC source -> [B][C] */
+int ugpg_avgpool_fwd(ugpg_src_t src, int B, int HW, float* out, void* stream);
+int ugpg_avgpool_bwd(const float* dout, int B, int HW, int C, float* da, int accumulate,
+                     void* stream);
+/* y[m][n] = act(sum_k x[m][k]*w[n][k] + b[n]) (act: 0 none, 1 relu); x row-major [M][K] */
+int ugpg_linear_fwd(const float* x, const float* w, const float* b, int M, int N, int K,
+                    int relu, float* y, void* stream);
+/* given dy (already masked by relu if any): dx = dy*w, dw = dy^T x, db = sum dy */
+int ugpg_linear_bwd(const float* x, const float* w, const float* dy, int M, int N, int K,
+                    float* dx, float* dw, float* db, void* stream);
+/* in-place relu backward mask: dy *= (y > 0) */
+int ugpg_relu_bwd(const float* y, float* dy, int64_t n, void* stream);
+/* elementwise y = x * mask (dropout with a precomputed scaled mask) */
+int ugpg_mul(const float* x, const float* m, float* y, int64_t n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* UGPG_H_ */

@@ -1,0 +1,165 @@
+"""Network-level parity: PGUNet1-4 forward/backward, uncertainty map, weighted
+loss, RMSprop and the trainer step on the HIP path vs the CPU oracle
+(oracle/ref_cpu.py, itself pinned to the reference by tests/golden)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import detgen as G
+from oracle import ref_cpu as O
+from tests._parity import (det_state, grad_check, is_prebn_bias, noise_floor, oracle_run,
+                           param_keys)
+
+pytestmark = pytest.mark.gpu
+
+LOGIT_TOL = 1e-3  # BASELINE.json north_star: within 1e-3 fp32
+
+
+def build(stage, nc, state, dev):
+    import ugpg
+    m = getattr(ugpg, f"PGUNet{stage}")(3, nc)
+    m.load_state_dict(state)
+    return m.to(dev).train()
+
+
+@pytest.mark.parametrize("stage,B,res,nc", [(1, 4, 32, 2), (1, 4, 32, 1), (2, 2, 64, 1),
+                                            (3, 2, 64, 1), (4, 2, 64, 1), (4, 2, 256, 1)])
+def test_pgunet_train_step_parity(dev, stage, B, res, nc):
+    from ugpg.loss import UncertaintyGuidedLoss
+    import torch.nn as nn
+    state = det_state(stage, 3, nc)
+    x = G.randn(1, (B, 3, res, res), "x")
+    t = G.bernoulli(2, (B, nc, res, res), 0.5, "t")
+    logits32, final32, base32, g32, P32 = oracle_run(stage, state, x, t)
+    _, final64, _, g64, _ = oracle_run(stage, state, x, t, dtype=torch.float64)
+    floor = noise_floor(stage, state, x, t, g32, g64)
+
+    m = build(stage, nc, state, dev)
+    out = m(x.to(dev))
+    crit = nn.BCEWithLogitsLoss(pos_weight=torch.tensor([5.0], device=dev), reduction="none")
+    final, base = UncertaintyGuidedLoss(dev).apply_uncertainty_weighted_loss(crit, out, t.to(dev))
+    final.backward()
+    # forward logits and mask
+    lg = out.detach().cpu()
+    assert (lg - logits32).abs().max().item() <= LOGIT_TOL
+    sure = logits32.abs() >= 1e-4
+    assert torch.equal((torch.sigmoid(lg) > 0.5)[sure], (torch.sigmoid(logits32) > 0.5)[sure])
+    # losses
+    assert abs(final.item() - final64.item()) <= 1e-5 * abs(final64.item())
+    assert abs(base - base32) <= 1e-5 * abs(base32)
+    # gradients (SURVEY §8d rule)
+    bad = []
+    named = dict(m.named_parameters())
+    for k in param_keys(state):
+        ok, err, bound = grad_check(k, named[k].grad, g32[k], g64[k], floor[k])
+        if not ok:
+            bad.append(f"{k}: {err:.3e} > {bound:.3e}")
+    assert not bad, "gradient parity failures:\n" + "\n".join(bad[:20])
+    # BatchNorm running statistics after the train forward
+    sd = m.state_dict()
+    for k, v in P32.items():
+        if k.endswith(("running_mean", "running_var")):
+            assert (sd[k].cpu() - v).abs().max().item() <= 1e-5 * max(1.0, v.abs().max().item()), k
+        if k.endswith("num_batches_tracked"):
+            assert int(sd[k]) == int(v), k
+
+
+def test_grads_are_one_flat_buffer(dev):
+    state = det_state(1, 3, 1)
+    m = build(1, 1, state, dev)
+    out = m(G.randn(1, (2, 3, 32, 32), "x").to(dev))
+    out.sum().backward()
+    from ugpg.flat import contiguous_run
+    params = list(m.parameters())
+    assert contiguous_run(params) is not None, "parameters are not one flat buffer"
+    assert contiguous_run([p.grad for p in params]) is not None, "grads were copied by autograd"
+
+
+def test_eval_forward_and_uncertainty_map(dev):
+    from ugpg.loss import UncertaintyGuidedLoss
+    fx = np.load("tests/golden/g2_umap.npz")
+    for prev_stage, B, cur_res in ((1, 2, 64), (3, 2, 256)):
+        prev_res = O.STAGE_RES[prev_stage]
+        state = det_state(prev_stage, 3, 1, seed=10 + prev_stage)
+        x = G.randn(20 + prev_stage, (B, 3, cur_res, cur_res), "x")
+        m = build(prev_stage, 1, state, dev)
+        u = UncertaintyGuidedLoss(dev).generate_uncertainty_map(x.to(dev), m, prev_res, cur_res)
+        assert not m.training
+        gold = torch.from_numpy(fx[f"s{prev_stage}_u"])
+        assert (u.cpu() - gold).abs().max().item() <= 1e-3
+        # no BN statistics may change in eval mode
+        for k, v in m.state_dict().items():
+            if k.endswith("num_batches_tracked"):
+                assert int(v) == 0
+
+
+def test_ug_loss_alpha_sweep_golden(dev):
+    import torch.nn as nn
+    from ugpg.loss import UncertaintyGuidedLoss
+    rows = np.load("tests/golden/g3_loss.npz")["rows"]
+    out = G.randn(30, (2, 1, 64, 64), "logits").to(dev)
+    t = G.bernoulli(31, (2, 1, 64, 64), 0.3, "t").to(dev)
+    u = torch.from_numpy(G.uniform(32, 2 * 64 * 64, "u").reshape(2, 1, 64, 64)).float().to(dev)
+    L = UncertaintyGuidedLoss(dev)
+    for pw, alpha, fin, base in rows:
+        crit = nn.BCEWithLogitsLoss(pos_weight=None if pw == 0 else torch.tensor([pw], device=dev),
+                                    reduction="none")
+        f, b = L.apply_uncertainty_weighted_loss(crit, out, t, None if alpha < 0 else u,
+                                                 1.0 if alpha < 0 else alpha)
+        assert abs(f.item() - fin) <= 1e-5 * abs(fin) and abs(b - base) <= 1e-5 * abs(base)
+
+
+def test_trainer_epoch_golden(dev):
+    """trainer.train_epoch on a 1-batch loader == the reference's 6-tuple (G6)."""
+    import json
+    from torch.utils.data import DataLoader, TensorDataset
+    import ugpg
+    gold = json.load(open("tests/golden/g6_train_epoch.json"))
+    for stage in (1, 2):
+        tr = ugpg.UncertaintyGuidedProgressiveTrainer(3, 1, device=dev, uncertainty_alpha=1.0)
+        for s in (1, 2):
+            tr.models[s].load_state_dict(det_state(s, 3, 1, seed=60 + s))
+        tr.current_stage = stage
+        tr.current_model = tr.models[stage]
+        tr.setup_optimizer(stage)
+        res = O.STAGE_RES[stage]
+        x = G.randn(61, (4, 3, res, res), "x")
+        t = G.bernoulli(62, (4, 1, res, res), 0.5, "t")
+        tup = tr.train_epoch(DataLoader(TensorDataset(x, t), batch_size=4), stage)
+        ref = gold[f"stage{stage}"]
+        assert abs(tup[0] - ref[0]) <= 1e-5 * abs(ref[0])
+        assert abs(tup[1] - ref[1]) <= 1e-5 * abs(ref[1])
+        assert abs(tup[2] - ref[2]) <= 1e-3          # Dice within +-0.001
+        assert abs(tup[3] - ref[3]) <= 1e-3
+        assert abs(tup[4] - ref[4]) <= 1e-5 and abs(tup[5] - ref[5]) <= 1e-5
+
+
+def test_rmsprop_step_matches_oracle(dev):
+    """Two ugpg RMSprop steps (flat single-launch path) == the oracle's
+    torch.optim.RMSprop rule applied to the same (GPU-computed) gradients."""
+    import torch.nn as nn
+    import ugpg
+    from ugpg.flat import contiguous_run
+    state = det_state(1, 3, 1)
+    x = G.randn(1, (2, 3, 32, 32), "x")
+    t = G.bernoulli(2, (2, 1, 32, 32), 0.5, "t")
+    m = build(1, 1, state, dev)
+    opt = ugpg.RMSprop(m.parameters(), lr=3e-4, weight_decay=1e-4)
+    crit = nn.BCEWithLogitsLoss(pos_weight=torch.tensor([5.0], device=dev), reduction="none")
+    keys = [k for k, _ in m.named_parameters()]
+    P = {k: p.detach().cpu().clone() for k, p in m.named_parameters()}
+    sq = {k: torch.zeros_like(P[k]) for k in keys}
+    for _ in range(2):
+        opt.zero_grad()
+        f, _ = ugpg.UncertaintyGuidedLoss(dev).apply_uncertainty_weighted_loss(
+            crit, m(x.to(dev)), t.to(dev))
+        f.backward()
+        grads = {k: p.grad.detach().cpu().clone() for k, p in m.named_parameters()}
+        opt.step()
+        O.rmsprop_step(P, grads, sq, 3e-4)
+    assert contiguous_run([opt.state[p]["square_avg"] for p in m.parameters()]) is not None
+    named = dict(m.named_parameters())
+    for k in keys:
+        err = (named[k].detach().cpu() - P[k]).abs().max().item()
+        assert err <= 1e-6 * max(1.0, P[k].abs().max().item()), (k, err)
+        assert int(opt.state[named[k]]["step"]) == 2

@@ -1,0 +1,349 @@
+"""Kernel-level parity: every libugpg entry point vs the same op in PyTorch on the
+CPU (fp64 where it sharpens the reference).  Sizes cover every conv tile
+configuration, ragged (non tile-multiple) images, concat inputs and the
+fused BatchNorm-apply prologue."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import detgen as G
+
+pytestmark = pytest.mark.gpu
+
+
+def rnd(shape, seed, name="t", scale=1.0):
+    return G.randn(seed, shape, name) * scale
+
+
+def nhwc(t):  # NCHW cpu -> NHWC contiguous
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+def nchw(t):
+    return t.permute(0, 3, 1, 2).contiguous()
+
+
+def close(a, b, tol, what=""):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    err = (a - b).abs().max().item()
+    scale = max(b.abs().max().item(), 1e-30)
+    assert err <= tol * scale, f"{what}: max|diff| {err:.3e} > {tol:.1e} * {scale:.3e}"
+
+
+def act_ref(y, scale, shift):
+    if scale is None:
+        return y
+    return torch.relu(y * scale.view(1, -1, 1, 1) + shift.view(1, -1, 1, 1))
+
+
+CONV_CASES = [
+    # B, H, W, C0, C1, Cout, affine
+    (2, 16, 16, 64, 0, 64, False),
+    (2, 32, 32, 64, 0, 128, True),     # CFG_W candidate / CFG_S
+    (1, 24, 20, 8, 0, 64, False),      # ragged tiles, BKC 8
+    (2, 16, 16, 128, 128, 256, True),  # concat, CFG_S
+    (4, 64, 64, 64, 64, 64, True),     # concat, CFG_L
+    (16, 32, 32, 256, 0, 128, False),  # CFG_W
+    (1, 8, 8, 512, 512, 256, True),    # deep K, tiny image
+    (2, 256, 256, 64, 0, 64, True),    # CFG_L (16x16 tile), multi-tile wgrad splits
+    (4, 128, 128, 64, 0, 128, False),  # CFG_W (8x16 x 128)
+    (2, 256, 256, 64, 64, 64, True),   # Up4-shaped: concat dgrad must not straddle the split
+]
+BIG = {5, 6, 7}
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv3x3_fwd_stats(dev, case):
+    from ugpg import ops
+    B, H, W, C0, C1, Cout, affine = case
+    cin = C0 + C1
+    x0 = rnd((B, C0, H, W), 1, "x0")
+    x1 = rnd((B, C1, H, W), 2, "x1") if C1 else None
+    w = rnd((Cout, cin, 3, 3), 3, "w", 1.0 / (3 * cin ** 0.5))
+    b = rnd((Cout,), 4, "b", 0.1)
+    sc0 = sh0 = sc1 = sh1 = None
+    if affine:
+        sc0, sh0 = rnd((C0,), 5, "s0", 0.5) + 1, rnd((C0,), 6, "h0", 0.2)
+        if C1:
+            sc1, sh1 = rnd((C1,), 7, "s1", 0.5) + 1, rnd((C1,), 8, "h1", 0.2)
+    inp = act_ref(x0, sc0, sh0)
+    if C1:
+        inp = torch.cat([inp, act_ref(x1, sc1, sh1) if affine else x1], 1)
+    ref = F.conv2d(inp.double(), w.double(), b.double(), padding=1)
+
+    g = lambda t: None if t is None else t.to(dev)
+    srcs = [ops.Act(nhwc(x0).to(dev), g(sc0), g(sh0))]
+    if C1:
+        srcs.append(ops.Act(nhwc(x1).to(dev), g(sc1), g(sh1)))
+    wpk = ops.pack_conv3x3(w.to(dev), cin, 0)
+    out = torch.empty(B, H, W, Cout, device=dev)
+    nt = ops.conv_ntiles(B, H, W, cin, Cout)
+    stats = torch.empty(3 * Cout * nt, device=dev)
+    ops.conv3x3_fwd(srcs, wpk, b.to(dev), Cout, [out], stats=stats)
+    close(nchw(out.cpu()), ref, 2e-5, "conv fwd")
+    # BatchNorm finalize from the fused partials
+    gam, bet = rnd((Cout,), 9, "g", 0.3) + 1, rnd((Cout,), 10, "be", 0.1)
+    rm, rv = torch.zeros(Cout, device=dev), torch.ones(Cout, device=dev)
+    nbt = torch.zeros((), dtype=torch.int64, device=dev)
+    mean, invstd, scale, shift = ops.bn_finalize(stats, nt, gam.to(dev), bet.to(dev), rm, rv, nbt,
+                                                 0.1, 1e-5)
+    rmean = ref.mean(dim=(0, 2, 3))
+    rvar = ref.var(dim=(0, 2, 3), unbiased=False)
+    close(mean.cpu(), rmean, 1e-5, "bn mean")
+    close(invstd.cpu(), 1 / torch.sqrt(rvar + 1e-5), 1e-5, "bn invstd")
+    n = B * H * W
+    close(rv.cpu(), 0.9 + 0.1 * rvar * n / (n - 1), 1e-5, "running_var")
+    close(rm.cpu(), 0.1 * rmean, 1e-5, "running_mean")
+    assert int(nbt.item()) == 1
+
+
+@pytest.mark.parametrize("case", CONV_CASES[:5] + CONV_CASES[7:])
+def test_conv3x3_dgrad_wgrad(dev, case):
+    from ugpg import ops
+    B, H, W, C0, C1, Cout, affine = case
+    cin = C0 + C1
+    cin_real = 3 if cin == 8 else cin
+    x = rnd((B, cin, H, W), 11, "x")
+    if cin_real < cin:
+        x[:, cin_real:] = 0
+    sc = rnd((cin,), 12, "s", 0.5) + 1 if affine else None
+    sh = rnd((cin,), 13, "h", 0.2) if affine else None
+    w = rnd((Cout, cin_real, 3, 3), 14, "w", 0.05)
+    dy = rnd((B, Cout, H, W), 15, "dy")
+    xin = act_ref(x, sc, sh).double()[:, :cin_real].clone().requires_grad_(True)
+    wd = w.double().requires_grad_(True)
+    bd = torch.zeros(Cout, dtype=torch.float64, requires_grad=True)
+    y = F.conv2d(xin, wd, bd, padding=1)
+    y.backward(dy.double())
+    # dgrad (only for real input channels that are multiples of 64)
+    if cin_real % 64 == 0:
+        wpk = ops.pack_conv3x3(w.to(dev), cin_real, 1)
+        if C1:
+            d0 = torch.empty(B, H, W, C0, device=dev)
+            d1 = torch.full((B, H, W, C1), 0.5, device=dev)
+            ops.conv3x3_fwd([ops.Act(nhwc(dy).to(dev))], wpk, None, cin_real, [d0, d1], split=C0,
+                            accumulate=(0, 1))
+            close(nchw(d0.cpu()), xin.grad[:, :C0], 2e-5, "dgrad src0")
+            close(nchw(d1.cpu()) - 0.5, xin.grad[:, C0:], 2e-5, "dgrad src1 (accumulate)")
+        else:
+            dx = torch.empty(B, H, W, cin_real, device=dev)
+            ops.conv3x3_fwd([ops.Act(nhwc(dy).to(dev))], wpk, None, cin_real, [dx])
+            close(nchw(dx.cpu()), xin.grad, 2e-5, "dgrad")
+    # wgrad on the activated (lazy) source
+    g = lambda t: None if t is None else t.to(dev)
+    xs = nhwc(x).to(dev)
+    if C1:
+        srcs = [ops.Act(xs[..., :C0].contiguous(), g(sc[:C0] if affine else None), g(sh[:C0] if affine else None)),
+                ops.Act(xs[..., C0:].contiguous(), g(sc[C0:] if affine else None), g(sh[C0:] if affine else None))]
+    else:
+        srcs = [ops.Act(xs, g(sc), g(sh))]
+    dw = torch.empty(Cout, cin_real, 3, 3, device=dev)
+    db = torch.empty(Cout, device=dev)
+    ops.conv3x3_wgrad(srcs, nhwc(dy).to(dev), dw, db, cin_real)
+    close(dw.cpu(), wd.grad, 2e-5, "wgrad")
+    close(db.cpu(), bd.grad, 2e-5, "bias grad")
+
+
+@pytest.mark.parametrize("C,npix", [(64, 5000), (512, 300), (128, 70000)])
+def test_bn_relu_bwd(dev, C, npix):
+    from ugpg import ops
+    y = rnd((npix, C), 20, "y") * 2 + 0.3
+    gam = rnd((C,), 21, "g", 0.3) + 1
+    bet = rnd((C,), 22, "b", 0.3)
+    da = rnd((npix, C), 23, "da")
+    yd = y.double().requires_grad_(True)
+    gd = gam.double().requires_grad_(True)
+    bd = bet.double().requires_grad_(True)
+    a = torch.relu(F.batch_norm(yd.t().unsqueeze(0), None, None, gd, bd, True, 0.1, 1e-5))
+    a.backward(da.double().t().unsqueeze(0))
+    mean = y.double().mean(0)
+    var = y.double().var(0, unbiased=False)
+    invstd = 1 / torch.sqrt(var + 1e-5)
+    scale = (gam.double() * invstd)
+    shift = bet.double() - mean * scale
+    f = lambda t: t.float().to(dev)
+    dy = torch.empty(npix, C, device=dev)
+    dg, dbt = torch.empty(C, device=dev), torch.empty(C, device=dev)
+    ops.bn_relu_bwd(f(da), f(y), f(mean), f(invstd), f(scale), f(shift), dy, dg, dbt)
+    close(dy.cpu(), yd.grad, 1e-4, "bn bwd dx")
+    close(dg.cpu(), gd.grad, 1e-4, "dgamma")
+    close(dbt.cpu(), bd.grad, 1e-4, "dbeta")
+
+
+def test_maxpool(dev):
+    from ugpg import ops
+    B, H, W, C = 2, 18, 22, 64
+    y = rnd((B, C, H, W), 30, "y")
+    sc, sh = rnd((C,), 31, "s", 0.5) + 1, rnd((C,), 32, "h", 0.3)
+    a = act_ref(y, sc, sh).double().requires_grad_(True)
+    ref = F.max_pool2d(a, 2)
+    d = rnd(tuple(ref.shape), 33, "d")
+    ref.backward(d.double())
+    out, am = ops.maxpool2_fwd(ops.Act(nhwc(y).to(dev), sc.to(dev), sh.to(dev)))
+    close(nchw(out.cpu()), ref, 1e-6, "maxpool fwd")
+    din = torch.full((B, H, W, C), 1.0, device=dev)
+    ops.maxpool2_bwd(nhwc(d).to(dev), am, H, W, din, 1)
+    close(nchw(din.cpu()) - 1.0, a.grad, 1e-6, "maxpool bwd")
+
+
+@pytest.mark.parametrize("hi,wi,ho,wo", [(16, 16, 32, 32), (8, 8, 16, 16), (7, 5, 13, 11), (32, 32, 16, 16)])
+def test_bilinear_nhwc(dev, hi, wi, ho, wo):
+    from ugpg import ops
+    B, C = 2, 64
+    y = rnd((B, C, hi, wi), 40, "y")
+    sc, sh = rnd((C,), 41, "s", 0.5) + 1, rnd((C,), 42, "h", 0.3)
+    # fp32 reference: ATen derives the align_corners weights in fp32 (fp64 rounds differently)
+    a = act_ref(y, sc, sh).requires_grad_(True)
+    ref = F.interpolate(a, size=(ho, wo), mode="bilinear", align_corners=True)
+    d = rnd(tuple(ref.shape), 43, "d")
+    ref.backward(d)
+    out = ops.bilinear_nhwc_fwd(ops.Act(nhwc(y).to(dev), sc.to(dev), sh.to(dev)), ho, wo)
+    close(nchw(out.cpu()), ref, 2e-6, "bilinear fwd")
+    din = torch.empty(B, hi, wi, C, device=dev)
+    ops.bilinear_nhwc_bwd(nhwc(d).to(dev), hi, wi, din, 0)
+    close(nchw(din.cpu()), a.grad, 1e-5, "bilinear bwd")
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("hi,ho", [(256, 128), (128, 256), (64, 64), (30, 47)])
+def test_resize_nchw(dev, mode, hi, ho):
+    from ugpg import ops
+    x = rnd((2, 3, hi, hi), 50, "x")
+    if mode == 0:
+        ref = F.interpolate(x, size=(ho, ho), mode="bilinear", align_corners=True)
+    elif mode == 1:
+        ref = F.interpolate(x, size=(ho, ho), mode="nearest")
+    else:
+        p = F.interpolate(torch.sigmoid(x), size=(ho, ho), mode="bilinear", align_corners=True)
+        ref = 1.0 - 2.0 * torch.abs(p - 0.5)
+    out = ops.resize_nchw(x.to(dev), ho, ho, mode)
+    close(out.cpu(), ref, 2e-6, f"resize mode {mode}")
+    if mode == 1:
+        assert torch.equal(out.cpu(), ref)
+
+
+@pytest.mark.parametrize("nc", [1, 2])
+def test_heads(dev, nc):
+    from ugpg import ops
+    B = 2
+    specs = [(256, 8), (128, 16), (64, 32), (64, 64)]
+    ys, acts, ws, bs, refs, leaf = [], [], [], [], [], []
+    for i, (C, R) in enumerate(specs):
+        y = rnd((B, C, R, R), 60 + i, "y")
+        sc, sh = rnd((C,), 70 + i, "s", 0.5) + 1, rnd((C,), 80 + i, "h", 0.3)
+        a = act_ref(y, sc, sh).double().requires_grad_(True)
+        w = rnd((nc, C, 1, 1), 90 + i, "w", 0.1).double().requires_grad_(True)
+        b = rnd((nc,), 95 + i, "b", 0.1).double().requires_grad_(True)
+        h = F.conv2d(a, w, b)
+        if R != 64:
+            h = F.interpolate(h, scale_factor=64 // R, mode="bilinear", align_corners=True)
+        refs.append(h)
+        leaf.append((a, w, b))
+        acts.append(ops.Act(nhwc(y).to(dev), sc.to(dev), sh.to(dev)))
+        ws.append(w.detach().float().reshape(nc, C).contiguous().to(dev))
+        bs.append(b.detach().float().to(dev))
+    ref = refs[0] + refs[1] + refs[2] + refs[3]
+    dl = rnd(tuple(ref.shape), 99, "dl")
+    ref.backward(dl.double())
+    hs = [ops.head_fwd(a, w, b) for a, w, b in zip(acts, ws, bs)]
+    logits = ops.heads_combine(hs, B, 64, 64, nc)
+    close(logits.cpu(), ref, 1e-5, "heads fwd")
+    dhs = ops.heads_split_bwd(dl.to(dev), [R for _, R in specs])
+    for i, (a, w, b) in enumerate(leaf):
+        dw = torch.empty_like(ws[i])
+        db = torch.empty(nc, device=dev)
+        da = torch.empty_like(acts[i].y)
+        ops.head_bwd(acts[i], ws[i], dhs[i].contiguous(), dw, db, da, 0)
+        close(dw.cpu(), w.grad.reshape(nc, -1), 1e-5, f"head{i} dw")
+        # db is a heavily cancelling sum: bound it relative to sum|terms|
+        dh64 = dhs[i].double().cpu()
+        assert (db.cpu().double() - b.grad).abs().max() <= 1e-6 * dh64.abs().sum(), f"head{i} db"
+        close(nchw(da.cpu()), a.grad, 1e-5, f"head{i} da")
+
+
+@pytest.mark.parametrize("pw,with_u,cu", [(5.0, True, 1), (None, True, 1), (5.0, False, 1), (2.0, True, 2)])
+def test_ug_loss(dev, pw, with_u, cu):
+    from ugpg import ops
+    B, C, H = 3, 2 if cu == 2 else 1, 40
+    x = rnd((B, C, H, H), 100, "x", 3.0)
+    t = G.bernoulli(101, (B, C, H, H), 0.4, "t")
+    u = torch.from_numpy(G.uniform(102, B * cu * H * H, "u").reshape(B, cu, H, H)).float() if with_u else None
+    alpha = 1.5
+    xd = x.double().requires_grad_(True)
+    pwt = None if pw is None else torch.tensor([pw], dtype=torch.float64)
+    pl = F.binary_cross_entropy_with_logits(xd, t.double(), pos_weight=pwt, reduction="none")
+    final = (pl * (1 + alpha * u.double())).mean() if with_u else pl.mean()
+    final.backward()
+    g = lambda v: None if v is None else v.to(dev)
+    pw_dev = None if pw is None else torch.tensor([pw], device=dev)
+    out = ops.ug_loss_fwd(x.to(dev), t.to(dev), g(u), pw_dev, alpha if with_u else 0.0)
+    close(out[0:1].cpu(), final.reshape(1), 1e-6, "final")
+    close(out[1:2].cpu(), pl.mean().reshape(1), 1e-6, "base")
+    gout = torch.tensor([1.0], device=dev)
+    dx = ops.ug_loss_bwd(x.to(dev), t.to(dev), g(u), pw_dev, alpha if with_u else 0.0, gout)
+    close(dx.cpu(), xd.grad, 1e-5, "dlogits")
+
+
+def test_seg_metrics_and_mean_std(dev):
+    from ugpg import ops
+    B, H = 4, 64
+    x = rnd((B, 1, H, H), 110, "x", 2.0)
+    x[0, 0, 0, :4] = torch.tensor([1e-9, -1e-9, 0.0, 1e-3])  # around the 0.5 threshold
+    t = G.bernoulli(111, (B, 1, H, H), 0.3, "t")
+    pred = (torch.sigmoid(x) > 0.5).float().squeeze(1)
+    ts = t.squeeze(1)
+    inter = (pred * ts).view(B, -1).sum(1)
+    dice = ((2 * inter + 1) / (pred.view(B, -1).sum(1) + ts.view(B, -1).sum(1) + 1)).mean()
+    wrong = pred.ne(ts.long()).sum().item()
+    out = ops.seg_metrics(x.to(dev), t.to(dev)).cpu()
+    assert abs(out[0].item() - dice.item()) < 1e-6
+    assert int(out[2].item()) == wrong
+    u = torch.from_numpy(G.uniform(112, 3 * 100003, "u")).float()
+    ms = ops.mean_std(u.to(dev)).cpu()
+    close(ms[0:1], u.double().mean().reshape(1), 1e-6, "mean")
+    close(ms[1:2], u.double().std().reshape(1), 1e-6, "std")
+
+
+@pytest.mark.parametrize("n,off", [(4096, 0), (1001, 3)])
+def test_rmsprop(dev, n, off):
+    from ugpg import ops
+    p = rnd((n + off,), 120, "p")
+    g = rnd((n + off,), 121, "g", 0.1)
+    ref_p = p[off:].clone().requires_grad_(True)
+    ref_p.grad = g[off:].clone()
+    opt = torch.optim.RMSprop([ref_p], lr=1e-3, weight_decay=1e-4)
+    pd, gd = p.to(dev), g.to(dev)
+    v = torch.zeros(n + off, device=dev)
+    for _ in range(3):
+        opt.step()
+        ops.rmsprop_step(pd[off:], gd[off:], v[off:], 1e-3, 0.99, 1e-8, 1e-4)
+    close(pd[off:].cpu(), ref_p.detach(), 1e-6, "rmsprop params")
+
+
+def test_avgpool_linear(dev):
+    from ugpg import ops
+    B, C, H = 4, 512, 8
+    y = rnd((B, C, H, H), 130, "y")
+    sc, sh = rnd((C,), 131, "s", 0.5) + 1, rnd((C,), 132, "h", 0.3)
+    a = act_ref(y, sc, sh)
+    ref = F.adaptive_avg_pool2d(a, 1).flatten(1)
+    out = ops.avgpool_fwd(ops.Act(nhwc(y).to(dev), sc.to(dev), sh.to(dev)))
+    close(out.cpu(), ref, 1e-6, "avgpool")
+    w = rnd((256, C), 133, "w", 0.05).double().requires_grad_(True)
+    b = rnd((256,), 134, "b", 0.05).double().requires_grad_(True)
+    xin = ref.double().requires_grad_(True)
+    yr = torch.relu(F.linear(xin, w, b))
+    dy = rnd(tuple(yr.shape), 135, "dy")
+    yr.backward(dy.double())
+    yo = ops.linear_fwd(out, w.detach().float().to(dev), b.detach().float().to(dev), True)
+    close(yo.cpu(), yr, 1e-5, "linear fwd")
+    dyd = dy.to(dev).contiguous()
+    ops.relu_bwd_(yo, dyd)
+    dx = torch.empty(B, C, device=dev)
+    dw = torch.empty(256, C, device=dev)
+    db = torch.empty(256, device=dev)
+    ops.linear_bwd(out, w.detach().float().to(dev), dyd, dx, dw, db)
+    close(dx.cpu(), xin.grad, 1e-5, "linear dx")
+    close(dw.cpu(), w.grad, 1e-5, "linear dw")
+    close(db.cpu(), b.grad, 1e-5, "linear db")

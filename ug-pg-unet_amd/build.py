@@ -1,0 +1,88 @@
+"""Build libugpg.so (HIP, gfx950) in-tree: ug-pg-unet_amd/ugpg/libugpg.so.
+
+    python ug-pg-unet_amd/build.py [--force]
+
+Plain hipcc, one object per translation unit (compiled in parallel), no torch
+dependency in the library.  Incremental: a TU is rebuilt only when it or a header
+is newer than its object.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+CSRC = HERE / "csrc"
+INCLUDE = HERE.parent / "include"
+BUILD = HERE / "build"
+LIB = HERE / "ugpg" / "libugpg.so"
+ARCH = os.environ.get("UGPG_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
+         "-Wno-unused-variable", "-Wno-unused-but-set-variable"]
+
+
+def _hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and Path(c).exists():
+            return c
+    raise RuntimeError("hipcc not found: libugpg.so cannot be built")
+
+
+def _sources():
+    return sorted(CSRC.glob("*.hip"))
+
+
+def _newest_header() -> float:
+    hs = list(CSRC.glob("*.h")) + list(INCLUDE.glob("*.h"))
+    return max((h.stat().st_mtime for h in hs), default=0.0)
+
+
+# memory-bound kernels: no FMA contraction, so interpolation weights round exactly
+# like ATen's CPU kernels (align_corners source index = rounded(scale*o))
+PER_FILE = {"ops.hip": ["-ffp-contract=off"]}
+
+
+def _compile(src: Path, force: bool) -> Path:
+    obj = BUILD / (src.stem + ".o")
+    if not force and obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime, _newest_header()):
+        return obj
+    cmd = [_hipcc(), *FLAGS, *PER_FILE.get(src.name, []), "-c", str(src), "-o", str(obj)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr}")
+    return obj
+
+
+def build(force: bool = False, verbose: bool = True) -> Path:
+    BUILD.mkdir(exist_ok=True)
+    srcs = _sources()
+    jobs = min(len(srcs), int(os.environ.get("MAX_JOBS", "8")))
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        objs = list(ex.map(lambda s: _compile(s, force), srcs))
+    newest = max(o.stat().st_mtime for o in objs)
+    if force or not LIB.exists() or LIB.stat().st_mtime < newest:
+        tmp = LIB.with_suffix(".so.tmp")
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr}")
+        os.replace(tmp, LIB)
+    if verbose:
+        print(f"built {LIB} ({LIB.stat().st_size / 1e6:.1f} MB)")
+    return LIB
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    a = ap.parse_args()
+    try:
+        build(force=a.force)
+    except RuntimeError as e:
+        print(e, file=sys.stderr)
+        sys.exit(1)

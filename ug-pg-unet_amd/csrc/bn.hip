@@ -1,0 +1,274 @@
+// BatchNorm2d(train/eval) + ReLU for NHWC fp32 on gfx950.
+// Replaces aten::native_batch_norm / native_batch_norm_backward / threshold_backward
+// behind DoubleConv (reference UG_unet_parts.py:11-12,14-15).
+//
+// Forward statistics come from the producing conv's epilogue as per-tile
+// (count, sum, M2); ugpg_bn_finalize merges them in fp64 (Chan et al.), which is
+// the numerically stable two-pass result, deterministic for a fixed tiling.
+// The normalisation itself is never materialised: consumers apply
+// relu(scale*y + shift) while loading (ugpg_src_t).
+#include "common.h"
+
+namespace ugpg {
+
+__global__ void bn_finalize_kernel(const float* __restrict__ stats, int ntiles, int C,
+                                   const float* gamma, const float* beta, float* rmean,
+                                   float* rvar, int64_t* nbt, float momentum, float eps,
+                                   float* mean_o, float* invstd_o, float* scale_o,
+                                   float* shift_o) {
+    const int c = blockIdx.x;
+    __shared__ double sn[256], sm[256], sq[256];
+    const float* cnt = stats + (size_t)c * ntiles;
+    const float* sum = stats + ((size_t)C + c) * ntiles;
+    const float* m2 = stats + ((size_t)2 * C + c) * ntiles;
+    double n = 0, mu = 0, M = 0;
+    for (int t = threadIdx.x; t < ntiles; t += blockDim.x) {
+        const double nb = cnt[t];
+        if (nb <= 0) continue;
+        const double mb = (double)sum[t] / nb, Mb = m2[t];
+        const double nn = n + nb, d = mb - mu;
+        mu += d * nb / nn;
+        M += Mb + d * d * n * nb / nn;
+        n = nn;
+    }
+    sn[threadIdx.x] = n;
+    sm[threadIdx.x] = mu;
+    sq[threadIdx.x] = M;
+    __syncthreads();
+    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+        if (threadIdx.x < s) {
+            const double na = sn[threadIdx.x], nb = sn[threadIdx.x + s];
+            const double nn = na + nb;
+            if (nb > 0) {
+                const double d = sm[threadIdx.x + s] - sm[threadIdx.x];
+                sm[threadIdx.x] += d * nb / nn;
+                sq[threadIdx.x] += sq[threadIdx.x + s] + d * d * na * nb / nn;
+                sn[threadIdx.x] = nn;
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const double N = sn[0], m = sm[0];
+        const double var = sq[0] / N;
+        const float inv = (float)(1.0 / sqrt(var + (double)eps));
+        const float mf = (float)m;
+        const float sc = inv * gamma[c];
+        mean_o[c] = mf;
+        invstd_o[c] = inv;
+        scale_o[c] = sc;
+        shift_o[c] = beta[c] - mf * sc;
+        if (rmean) {
+            const double unbiased = N > 1 ? sq[0] / (N - 1) : sq[0];
+            rmean[c] = (float)(momentum * m + (1.0 - momentum) * (double)rmean[c]);
+            rvar[c] = (float)(momentum * unbiased + (1.0 - momentum) * (double)rvar[c]);
+        }
+        if (c == 0 && nbt) *nbt += 1;
+    }
+}
+
+__global__ void bn_eval_params_kernel(const float* gamma, const float* beta, const float* rm,
+                                      const float* rv, float eps, int C, float* scale,
+                                      float* shift) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const float inv = (float)(1.0 / sqrt((double)rv[c] + (double)eps));
+    const float sc = inv * gamma[c];
+    scale[c] = sc;
+    shift[c] = beta[c] - rm[c] * sc;
+}
+
+// Per-block partial sums of g and g*xhat over a contiguous pixel range.
+// Thread layout: C/4 threads per pixel (float4 channels), 256/(C/4) pixel slots.
+__global__ void __launch_bounds__(256)
+    bn_bwd_reduce_kernel(const float* __restrict__ da, const float* __restrict__ y, int64_t npix,
+                         int C, const float* mean, const float* invstd, const float* scale,
+                         const float* shift, int64_t ppb, float* part, int nblk) {
+    const int c4n = C / 4, slots = 256 / c4n;
+    const int tid = threadIdx.x, q = tid % c4n, slot = tid / c4n;
+    const int c = q * 4;
+    __shared__ f32x4 rs[256], rq[256];
+    f32x4 sg = {0, 0, 0, 0}, sgx = {0, 0, 0, 0};
+    if (slot < slots) {
+        const f32x4 mu = *reinterpret_cast<const f32x4*>(mean + c);
+        const f32x4 is = *reinterpret_cast<const f32x4*>(invstd + c);
+        const f32x4 sc = *reinterpret_cast<const f32x4*>(scale + c);
+        const f32x4 sh = *reinterpret_cast<const f32x4*>(shift + c);
+        const int64_t p0 = blockIdx.x * ppb, p1 = min(npix, p0 + ppb);
+        for (int64_t p = p0 + slot; p < p1; p += slots) {
+            const f32x4 d = *reinterpret_cast<const f32x4*>(da + p * C + c);
+            const f32x4 v = *reinterpret_cast<const f32x4*>(y + p * C + c);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float g = fmaf(v[k], sc[k], sh[k]) > 0.f ? d[k] : 0.f;
+                sg[k] += g;
+                sgx[k] = fmaf(g, (v[k] - mu[k]) * is[k], sgx[k]);
+            }
+        }
+    }
+    rs[tid] = sg;
+    rq[tid] = sgx;
+    __syncthreads();
+    if (slot == 0) {
+        for (int s = 1; s < slots; ++s) {
+            sg += rs[s * c4n + q];
+            sgx += rq[s * c4n + q];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            part[(size_t)(c + k) * nblk + blockIdx.x] = sg[k];
+            part[((size_t)C + c + k) * nblk + blockIdx.x] = sgx[k];
+        }
+    }
+}
+
+__global__ void bn_bwd_finalize_kernel(const float* part, int nblk, int C, int64_t npix,
+                                       float* dgamma, float* dbeta, int acc, float* coef) {
+    const int c = blockIdx.x;
+    __shared__ double s1[256], s2[256];
+    double a = 0, b = 0;
+    for (int i = threadIdx.x; i < nblk; i += blockDim.x) {
+        a += part[(size_t)c * nblk + i];
+        b += part[((size_t)C + c) * nblk + i];
+    }
+    s1[threadIdx.x] = a;
+    s2[threadIdx.x] = b;
+    __syncthreads();
+    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+        if (threadIdx.x < s) {
+            s1[threadIdx.x] += s1[threadIdx.x + s];
+            s2[threadIdx.x] += s2[threadIdx.x + s];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const float sg = (float)s1[0], sgx = (float)s2[0];
+        if (dgamma) dgamma[c] = acc ? dgamma[c] + sgx : sgx;
+        if (dbeta) dbeta[c] = acc ? dbeta[c] + sg : sg;
+        coef[c] = (float)(s1[0] / (double)npix);      // mean(g)
+        coef[C + c] = (float)(s2[0] / (double)npix);  // mean(g*xhat)
+    }
+}
+
+__global__ void bn_bwd_apply_kernel(const float* da, const float* __restrict__ y, int64_t npix,
+                                    int C, const float* mean, const float* invstd,
+                                    const float* scale, const float* shift, const float* coef,
+                                    float* dy) {
+    const int64_t n4 = npix * C / 4;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)((i * 4) % C);
+        const f32x4 d = reinterpret_cast<const f32x4*>(da)[i];
+        const f32x4 v = reinterpret_cast<const f32x4*>(y)[i];
+        f32x4 o;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int cc = c + k;
+            const float g = fmaf(v[k], scale[cc], shift[cc]) > 0.f ? d[k] : 0.f;
+            const float xh = (v[k] - mean[cc]) * invstd[cc];
+            o[k] = (g - coef[cc] - xh * coef[C + cc]) * scale[cc];
+        }
+        reinterpret_cast<f32x4*>(dy)[i] = o;
+    }
+}
+
+__global__ void bn_relu_apply_kernel(const float* x, const float* sc, const float* sh,
+                                     int64_t n4, int C, float* out) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)((i * 4) % C);
+        reinterpret_cast<f32x4*>(out)[i] =
+            act_apply4(reinterpret_cast<const f32x4*>(x)[i], sc, sh, c);
+    }
+}
+
+namespace {
+struct BwdPlan {
+    int nblk;
+    int64_t ppb;
+};
+BwdPlan bwd_plan(int64_t npix) {
+    BwdPlan p;
+    int64_t nb = cdiv(npix, 64);
+    if (nb > 1024) nb = 1024;
+    if (nb < 1) nb = 1;
+    p.ppb = cdiv(npix, nb);
+    p.nblk = (int)cdiv(npix, p.ppb);
+    return p;
+}
+}  // namespace
+}  // namespace ugpg
+
+using namespace ugpg;
+
+extern "C" int ugpg_bn_finalize(const float* stats, int ntiles, int C, const float* gamma,
+                                const float* beta, float* running_mean, float* running_var,
+                                int64_t* nbt, float momentum, float eps, float* mean,
+                                float* invstd, float* scale, float* shift, void* stream) {
+    if (!stats || !gamma || !beta || !mean || !invstd || !scale || !shift || C <= 0 ||
+        ntiles <= 0 || (!running_mean != !running_var)) {
+        set_error("bn_finalize: bad arguments");
+        return UGPG_ERR_INVALID;
+    }
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, as_stream(stream), stats,
+                       ntiles, C, gamma, beta, running_mean, running_var, nbt, momentum, eps,
+                       mean, invstd, scale, shift);
+    return check_launch("bn_finalize");
+}
+
+extern "C" int ugpg_bn_eval_params(const float* gamma, const float* beta, const float* rm,
+                                   const float* rv, float eps, int C, float* scale, float* shift,
+                                   void* stream) {
+    if (!gamma || !beta || !rm || !rv || !scale || !shift || C <= 0) {
+        set_error("bn_eval_params: bad arguments");
+        return UGPG_ERR_INVALID;
+    }
+    hipLaunchKernelGGL(bn_eval_params_kernel, dim3(cdiv(C, 256)), dim3(256), 0,
+                       as_stream(stream), gamma, beta, rm, rv, eps, C, scale, shift);
+    return check_launch("bn_eval_params");
+}
+
+extern "C" size_t ugpg_bn_relu_bwd_workspace(int64_t npix, int C) {
+    BwdPlan p = bwd_plan(npix);
+    return ((size_t)2 * C * p.nblk + (size_t)2 * C) * sizeof(float);
+}
+
+extern "C" int ugpg_bn_relu_bwd(const float* da, const float* y, int64_t npix, int C,
+                                const float* mean, const float* invstd, const float* scale,
+                                const float* shift, float* dy, float* dgamma, float* dbeta,
+                                int acc, void* ws, size_t ws_bytes, void* stream) {
+    if (!da || !y || !dy || !mean || !invstd || !scale || !shift || C % 4 || C > 1024 ||
+        npix <= 0) {
+        set_error("bn_relu_bwd: bad arguments (C=%d)", C);
+        return UGPG_ERR_INVALID;
+    }
+    const size_t need = ugpg_bn_relu_bwd_workspace(npix, C);
+    if (!ws || ws_bytes < need) {
+        set_error("bn_relu_bwd: workspace %zu < %zu", ws_bytes, need);
+        return UGPG_ERR_WORKSPACE;
+    }
+    BwdPlan p = bwd_plan(npix);
+    float* part = static_cast<float*>(ws);
+    float* coef = part + (size_t)2 * C * p.nblk;
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(p.nblk), dim3(256), 0, st, da, y, npix, C, mean,
+                       invstd, scale, shift, p.ppb, part, p.nblk);
+    if (int e = check_launch("bn_bwd_reduce")) return e;
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, part, p.nblk, C, npix,
+                       dgamma, dbeta, acc, coef);
+    if (int e = check_launch("bn_bwd_finalize")) return e;
+    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(stream_grid(npix * C / 4)), dim3(256), 0, st, da,
+                       y, npix, C, mean, invstd, scale, shift, coef, dy);
+    return check_launch("bn_bwd_apply");
+}
+
+extern "C" int ugpg_bn_relu_apply(ugpg_src_t src, int64_t npix, float* out, void* stream) {
+    if (!src.data || !out || src.C % 4) {
+        set_error("bn_relu_apply: bad arguments");
+        return UGPG_ERR_INVALID;
+    }
+    const int64_t n4 = npix * src.C / 4;
+    hipLaunchKernelGGL(bn_relu_apply_kernel, dim3(stream_grid(n4)), dim3(256), 0,
+                       as_stream(stream), src.data, src.scale, src.shift, n4, src.C, out);
+    return check_launch("bn_relu_apply");
+}

@@ -1,0 +1,682 @@
+// 3x3 / pad-1 convolution for gfx950: forward, data-gradient (same kernel with a
+// rotated/transposed weight pack) and weight-gradient, all NHWC fp32 on
+// v_mfma_f32_32x32x2_f32 (exact fp32 FMA chains, 157 TF/s peak).
+//
+// Replaces aten::convolution / convolution_backward behind DoubleConv
+// (reference UG_unet_parts.py:10,13).
+//
+// Forward tile: a TH x TW output-pixel rectangle x BN output channels.  Per input
+// channel chunk (BKC channels) the (TH+2)x(TW+2) halo and the 9 x BKC x BN weight
+// slab are staged in LDS once and reused by all 9 taps (9x reuse of every loaded
+// activation).  The consumer-side BatchNorm+ReLU of the producing layer is applied
+// while staging (lazy activation), so the normalised tensor never touches HBM, and
+// zero padding stays zero.  The epilogue adds the bias, stores, and emits per-tile
+// (count, sum, M2) BatchNorm partials (two-pass inside the tile, Chan-merged later).
+//
+// MFMA k-permutation: lane l (h = l>>5) feeds k-slot h of step s with input channel
+// 8g + 4h + s for both operands, so each lane's 4 consecutive channels come from one
+// 16-byte ds_read_b128 for A and one for B.
+#include "common.h"
+
+namespace ugpg {
+
+struct ConvFwdArgs {
+    const float* src0;
+    const float* sc0;
+    const float* sh0;
+    int C0;
+    const float* src1;
+    const float* sc1;
+    const float* sh1;
+    int C1;
+    const float* wpk;
+    const float* bias;
+    float* out0;
+    float* out1;
+    int split, acc0, acc1;
+    float* stats;
+    int B, H, W, Cin, Cout;
+    int tiles_x, tiles_y, ntiles;
+};
+
+template <int TH, int TW, int BN, int BKC, int WM, int WN>
+__global__ void __launch_bounds__(256) conv3x3_fwd_kernel(ConvFwdArgs a) {
+    constexpr int BM = TH * TW, HWD = TW + 2, NHALO = (TH + 2) * HWD;
+    constexpr int WTM = BM / WM, WTN = BN / WN, MT = WTM / 32, NT = WTN / 32;
+    constexpr int AP = BKC + 4;  // +16 B per halo pixel: spreads ds_read_b128 over banks
+    constexpr int G = BKC / 8;
+    constexpr int A_VEC = NHALO * BKC / 4, B_VEC = 9 * G * BN * 2;
+    constexpr int A_PER = (A_VEC + 255) / 256, B_PER = (B_VEC + 255) / 256;
+    static_assert(WM * WN == 4 && MT >= 1 && NT >= 1 && A_PER <= 32, "bad tile");
+    __shared__ __attribute__((aligned(16))) float smem[NHALO * AP + 9 * G * BN * 8];
+    float* As = smem;
+    float* Bs = smem + NHALO * AP;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int NB = a.Cout / BN;
+    const int nb = blockIdx.x % NB, tile = blockIdx.x / NB;
+    const int n0 = nb * BN;
+    const int tpi = a.tiles_x * a.tiles_y;
+    const int b = tile / tpi, trem = tile % tpi;
+    const int ty0 = (trem / a.tiles_x) * TH, tx0 = (trem % a.tiles_x) * TW;
+
+    f32x4 ra[A_PER];
+    f32x4 rb[B_PER];
+    unsigned avalid = 0;
+
+    auto gload = [&](int c) {
+        int cb = c * BKC;
+        const float* src = a.src0;
+        int Cs = a.C0;
+        if (cb >= a.C0) {
+            src = a.src1;
+            Cs = a.C1;
+            cb -= a.C0;
+        }
+        avalid = 0;
+#pragma unroll
+        for (int v = 0; v < A_PER; ++v) {
+            const int idx = tid + v * 256;
+            f32x4 val = {0.f, 0.f, 0.f, 0.f};
+            if (idx < A_VEC) {
+                const int hp = idx / (BKC / 4), q = idx % (BKC / 4);
+                const int gy = ty0 - 1 + hp / HWD, gx = tx0 - 1 + hp % HWD;
+                if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
+                    val = *reinterpret_cast<const f32x4*>(
+                        src + ((size_t)(b * a.H + gy) * a.W + gx) * Cs + cb + q * 4);
+                    avalid |= 1u << v;
+                }
+            }
+            ra[v] = val;
+        }
+        const float* wsrc = a.wpk + (size_t)c * G * 9 * a.Cout * 8;
+#pragma unroll
+        for (int v = 0; v < B_PER; ++v) {
+            const int idx = tid + v * 256;
+            if (idx < B_VEC) {
+                const int t = idx / (G * BN * 2), g = (idx / (BN * 2)) % G, r2 = idx % (BN * 2);
+                rb[v] = *reinterpret_cast<const f32x4*>(
+                    wsrc + ((size_t)(g * 9 + t) * a.Cout + n0) * 8 + r2 * 4);
+            }
+        }
+    };
+
+    auto lstore = [&](int c) {
+        int cb = c * BKC;
+        const float* sc = a.sc0;
+        const float* sh = a.sh0;
+        if (cb >= a.C0) {
+            sc = a.sc1;
+            sh = a.sh1;
+            cb -= a.C0;
+        }
+#pragma unroll
+        for (int v = 0; v < A_PER; ++v) {
+            const int idx = tid + v * 256;
+            if (idx < A_VEC) {
+                const int hp = idx / (BKC / 4), q = idx % (BKC / 4);
+                f32x4 val = ra[v];
+                if ((avalid >> v) & 1u) val = act_apply4(val, sc, sh, cb + q * 4);
+                *reinterpret_cast<f32x4*>(&As[hp * AP + q * 4]) = val;
+            }
+        }
+#pragma unroll
+        for (int v = 0; v < B_PER; ++v) {
+            const int idx = tid + v * 256;
+            if (idx < B_VEC) *reinterpret_cast<f32x4*>(&Bs[idx * 4]) = rb[v];
+        }
+    };
+
+    f32x16 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    int aoff[MT], boff[NT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        const int m = wm * WTM + mt * 32 + (lane & 31);
+        aoff[mt] = ((m / TW) * HWD + (m % TW)) * AP + 4 * (lane >> 5);
+    }
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) boff[nt] = (wn * WTN + nt * 32 + (lane & 31)) * 8 + 4 * (lane >> 5);
+
+    const int nchunk = a.Cin / BKC;
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    for (int c = 0; c < nchunk; ++c) {
+        if (c + 1 < nchunk) gload(c + 1);
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const int toff = ((t / 3) * HWD + (t % 3)) * AP;
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                f32x4 af[MT], bf[NT];
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+                    af[mt] = *reinterpret_cast<const f32x4*>(&As[aoff[mt] + toff + g * 8]);
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+                    bf[nt] = *reinterpret_cast<const f32x4*>(&Bs[(t * G + g) * BN * 8 + boff[nt]]);
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                        for (int nt = 0; nt < NT; ++nt)
+                            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[mt][s], bf[nt][s],
+                                                                               acc[mt][nt], 0, 0, 0);
+            }
+        }
+        __syncthreads();
+        if (c + 1 < nchunk) {
+            lstore(c + 1);
+            __syncthreads();
+        }
+    }
+
+    // ---- epilogue: bias, store, BatchNorm partials ----
+    const int vh = min(TH, a.H - ty0), vw = min(TW, a.W - tx0);
+    float* out;
+    int ostride, ocol0, oacc;
+    if (n0 < a.split) {
+        out = a.out0;
+        ostride = a.split;
+        ocol0 = n0;
+        oacc = a.acc0;
+    } else {
+        out = a.out1;
+        ostride = a.Cout - a.split;
+        ocol0 = n0 - a.split;
+        oacc = a.acc1;
+    }
+    float psum[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        const int nl = wn * WTN + nt * 32 + (lane & 31);
+        const float bv = a.bias ? a.bias[n0 + nl] : 0.f;
+        psum[nt] = 0.f;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = wm * WTM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                const int py = m / TW, px = m % TW;
+                const float v = acc[mt][nt][r] + bv;
+                acc[mt][nt][r] = v;
+                if (py < vh && px < vw) {
+                    const size_t o =
+                        ((size_t)(b * a.H + ty0 + py) * a.W + tx0 + px) * ostride + ocol0 + nl;
+                    out[o] = oacc ? out[o] + v : v;
+                    psum[nt] += v;
+                }
+            }
+    }
+    if (a.stats == nullptr) return;
+    float* red = smem;            // [WM][BN]
+    float* tot = smem + WM * BN;  // [BN]
+    const float cnt = (float)(vh * vw);
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        const float s = psum[nt] + __shfl_xor(psum[nt], 32, 64);
+        if (lane < 32) red[wm * BN + wn * WTN + nt * 32 + lane] = s;
+    }
+    __syncthreads();
+    if (tid < BN) {
+        float s = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) s += red[w * BN + tid];
+        tot[tid] = s;
+    }
+    __syncthreads();
+    float pq[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        const int nl = wn * WTN + nt * 32 + (lane & 31);
+        const float mu = tot[nl] / cnt;
+        float q = 0.f;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = wm * WTM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                if (m / TW < vh && m % TW < vw) {
+                    const float d = acc[mt][nt][r] - mu;
+                    q = fmaf(d, d, q);
+                }
+            }
+        pq[nt] = q + __shfl_xor(q, 32, 64);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+        if (lane < 32) red[wm * BN + wn * WTN + nt * 32 + lane] = pq[nt];
+    __syncthreads();
+    if (tid < BN) {
+        float q = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) q += red[w * BN + tid];
+        const size_t n = n0 + tid, T = a.ntiles;
+        a.stats[(0 * (size_t)a.Cout + n) * T + tile] = cnt;
+        a.stats[(1 * (size_t)a.Cout + n) * T + tile] = tot[tid];
+        a.stats[(2 * (size_t)a.Cout + n) * T + tile] = q;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Weight gradient: per block a 64 (co) x 64 (ci) x 9 (tap) output, 4 waves as
+// 2 (co) x 2 (ci) each owning nine 32x32 accumulators; reduction over the pixel
+// tiles of one split.  Operands from LDS: dy tile [P][64], activated input halo
+// [(TH+2)(TW+2)][64]; one MFMA k-step = 2 pixels.
+// ---------------------------------------------------------------------------
+struct WgradArgs {
+    const float* src0;
+    const float* sc0;
+    const float* sh0;
+    int C0;
+    const float* src1;
+    const float* sc1;
+    const float* sh1;
+    int C1;
+    const float* dy;
+    int Cout, Cin;
+    float* part;
+    float* dbpart;
+    int B, H, W;
+    int tiles_x, tiles_y, ntiles, nsplit, tps;
+};
+
+template <int TH, int TW>
+__global__ void __launch_bounds__(256) conv3x3_wgrad_kernel(WgradArgs a) {
+    constexpr int P = TH * TW, HWD = TW + 2, NHALO = (TH + 2) * HWD;
+    constexpr int DY_VEC = P * 16, X_VEC = NHALO * 16;
+    constexpr int DY_PER = (DY_VEC + 255) / 256, X_PER = (X_VEC + 255) / 256;
+    static_assert(X_PER <= 32, "halo too large");
+    __shared__ __attribute__((aligned(16))) float smem[(P + NHALO) * 64];
+    float* dys = smem;
+    float* xs = smem + P * 64;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int NCO = a.Cout / 64, NCI = (a.Cin + 63) / 64;
+    const int nb = blockIdx.x % NCO;
+    const int rest = blockIdx.x / NCO;
+    const int cb = rest % NCI, split = rest / NCI;
+    const int co0 = nb * 64, ci0 = cb * 64;
+    const int t_begin = split * a.tps, t_end = min(a.ntiles, t_begin + a.tps);
+
+    const float* xsrc = a.src0;
+    const float* xsc = a.sc0;
+    const float* xsh = a.sh0;
+    int Cs = a.C0, cbase = ci0;
+    if (ci0 >= a.C0) {
+        xsrc = a.src1;
+        xsc = a.sc1;
+        xsh = a.sh1;
+        Cs = a.C1;
+        cbase = ci0 - a.C0;
+    }
+    const int tpi = a.tiles_x * a.tiles_y;
+
+    f32x4 rdy[DY_PER], rx[X_PER];
+    unsigned xvalid = 0;
+    auto gload = [&](int tile) {
+        const int b = tile / tpi, trem = tile % tpi;
+        const int ty0 = (trem / a.tiles_x) * TH, tx0 = (trem % a.tiles_x) * TW;
+#pragma unroll
+        for (int v = 0; v < DY_PER; ++v) {
+            const int idx = tid + v * 256;
+            f32x4 val = {0.f, 0.f, 0.f, 0.f};
+            if (idx < DY_VEC) {
+                const int p = idx >> 4, q = idx & 15;
+                const int gy = ty0 + p / TW, gx = tx0 + p % TW;
+                if (gy < a.H && gx < a.W)
+                    val = *reinterpret_cast<const f32x4*>(
+                        a.dy + ((size_t)(b * a.H + gy) * a.W + gx) * a.Cout + co0 + q * 4);
+            }
+            rdy[v] = val;
+        }
+        xvalid = 0;
+#pragma unroll
+        for (int v = 0; v < X_PER; ++v) {
+            const int idx = tid + v * 256;
+            f32x4 val = {0.f, 0.f, 0.f, 0.f};
+            if (idx < X_VEC) {
+                const int hp = idx >> 4, q = idx & 15;
+                const int gy = ty0 - 1 + hp / HWD, gx = tx0 - 1 + hp % HWD;
+                if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W && cbase + q * 4 < Cs) {
+                    val = *reinterpret_cast<const f32x4*>(
+                        xsrc + ((size_t)(b * a.H + gy) * a.W + gx) * Cs + cbase + q * 4);
+                    xvalid |= 1u << v;
+                }
+            }
+            rx[v] = val;
+        }
+    };
+    auto lstore = [&]() {
+#pragma unroll
+        for (int v = 0; v < DY_PER; ++v) {
+            const int idx = tid + v * 256;
+            if (idx < DY_VEC) *reinterpret_cast<f32x4*>(&dys[idx * 4]) = rdy[v];
+        }
+#pragma unroll
+        for (int v = 0; v < X_PER; ++v) {
+            const int idx = tid + v * 256;
+            if (idx < X_VEC) {
+                f32x4 val = rx[v];
+                if ((xvalid >> v) & 1u) val = act_apply4(val, xsc, xsh, cbase + (idx & 15) * 4);
+                *reinterpret_cast<f32x4*>(&xs[idx * 4]) = val;
+            }
+        }
+    };
+
+    f32x16 acc[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+    float dbacc = 0.f;
+    const bool do_db = (a.dbpart != nullptr) && cb == 0 && tid < 64;
+
+    if (t_begin < t_end) gload(t_begin);
+    for (int tile = t_begin; tile < t_end; ++tile) {
+        __syncthreads();
+        lstore();
+        __syncthreads();
+        if (tile + 1 < t_end) gload(tile + 1);
+        const int arow = wm * 32 + (lane & 31), bcol = wn * 32 + (lane & 31);
+#pragma unroll 4
+        for (int ks = 0; ks < P / 2; ++ks) {
+            const int p = 2 * ks + (lane >> 5);
+            const float af = dys[p * 64 + arow];
+            const int hb = ((p / TW) * HWD + (p % TW)) * 64 + bcol;
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                const float bf = xs[hb + ((t / 3) * HWD + (t % 3)) * 64];
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(af, bf, acc[t], 0, 0, 0);
+            }
+        }
+        if (do_db) {
+            float s = 0.f;
+            for (int p = 0; p < P; ++p) s += dys[p * 64 + tid];
+            dbacc += s;
+        }
+    }
+
+    const int ci = ci0 + wn * 32 + (lane & 31);
+    if (ci < a.Cin) {
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int co = co0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                a.part[((size_t)(split * 9 + t) * a.Cout + co) * a.Cin + ci] = acc[t][r];
+            }
+    }
+    if (do_db) a.dbpart[(size_t)split * a.Cout + co0 + tid] = dbacc;
+}
+
+__global__ void wgrad_reduce_kernel(const float* part, const float* dbpart, int nsplit, int Cout,
+                                    int Cin, int Cin_real, float* dw, float* db, int accumulate) {
+    const int64_t total = (int64_t)9 * Cout * Cin_real;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        // e enumerates (t, co, ci) with ci fastest: coalesced partial reads
+        const int ci = (int)(e % Cin_real);
+        const int64_t r = e / Cin_real;
+        const int co = (int)(r % Cout), t = (int)(r / Cout);
+        float s = 0.f;
+        for (int k = 0; k < nsplit; ++k) s += part[((size_t)(k * 9 + t) * Cout + co) * Cin + ci];
+        const size_t o = ((size_t)co * Cin_real + ci) * 9 + t;
+        dw[o] = accumulate ? dw[o] + s : s;
+    }
+    if (db && blockIdx.x == 0) {
+        for (int co = threadIdx.x; co < Cout; co += blockDim.x) {
+            float s = 0.f;
+            for (int k = 0; k < nsplit; ++k) s += dbpart[(size_t)k * Cout + co];
+            db[co] = accumulate ? db[co] + s : s;
+        }
+    }
+}
+
+__global__ void pack_conv3x3_kernel(const float* w, float* wpk, int Cout, int Cin, int Cin_pad,
+                                    int mode) {
+    // mode 0: wpk[Cin_pad/8][9][Cout][8];  mode 1: wpk[Cout/8][9][Cin_pad][8] (rot180, transposed)
+    const int64_t total = (int64_t)Cin_pad * 9 * Cout;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int j = (int)(e & 7);
+        int64_t r = e >> 3;
+        if (mode == 0) {
+            const int co = (int)(r % Cout);
+            r /= Cout;
+            const int t = (int)(r % 9), cg = (int)(r / 9);
+            const int ci = cg * 8 + j;
+            wpk[e] = ci < Cin ? w[((size_t)co * Cin + ci) * 9 + t] : 0.f;
+        } else {
+            const int ci = (int)(r % Cin_pad);
+            r /= Cin_pad;
+            const int t = (int)(r % 9), cg = (int)(r / 9);
+            const int co = cg * 8 + j;
+            wpk[e] = ci < Cin ? w[((size_t)co * Cin + ci) * 9 + (8 - t)] : 0.f;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host-side configuration
+// ---------------------------------------------------------------------------
+namespace {
+
+enum FwdCfg { CFG_L = 0, CFG_W = 1, CFG_S = 2 };
+struct FwdShape {
+    int th, tw, bn;
+};
+const FwdShape kFwd[3] = {{16, 16, 64}, {8, 16, 128}, {8, 8, 64}};
+
+int64_t fwd_blocks(int cfg, int B, int H, int W, int Cout) {
+    const FwdShape& s = kFwd[cfg];
+    return (int64_t)B * cdiv(H, s.th) * cdiv(W, s.tw) * (Cout / s.bn);
+}
+
+int pick_fwd_cfg(int B, int H, int W, int Cout, int split) {
+    // prefer the larger tiles while they still give >= 2 blocks per CU; a block
+    // must not straddle the output split (its BN must divide `split`)
+    const int64_t want = 512;
+    if (Cout % 128 == 0 && split % 128 == 0 && fwd_blocks(CFG_W, B, H, W, Cout) >= want)
+        return CFG_W;
+    if (fwd_blocks(CFG_L, B, H, W, Cout) >= want) return CFG_L;
+    return CFG_S;
+}
+
+constexpr int WG_TH = 4, WG_TW = 16;
+
+struct WgradPlan {
+    int tiles_x, tiles_y, ntiles, nsplit, tps;
+};
+
+WgradPlan wgrad_plan(int B, int H, int W, int Cin, int Cout) {
+    WgradPlan p;
+    p.tiles_x = (int)cdiv(W, WG_TW);
+    p.tiles_y = (int)cdiv(H, WG_TH);
+    p.ntiles = B * p.tiles_x * p.tiles_y;
+    const int64_t base = (int64_t)(Cout / 64) * cdiv(Cin, 64);
+    int64_t ns = cdiv(1024, base);
+    // cap the fp32 partial slab at 64 MB
+    const int64_t per = (int64_t)9 * Cout * Cin * 4;
+    int64_t cap = (64ll << 20) / per;
+    if (cap < 1) cap = 1;
+    if (ns > cap) ns = cap;
+    if (ns > p.ntiles) ns = p.ntiles;
+    if (ns < 1) ns = 1;
+    p.tps = (int)cdiv(p.ntiles, ns);
+    p.nsplit = (int)cdiv(p.ntiles, p.tps);
+    return p;
+}
+
+template <int TH, int TW, int BN, int BKC, int WM, int WN>
+void launch_fwd(const ConvFwdArgs& a, hipStream_t st) {
+    const unsigned grid = (unsigned)((int64_t)a.ntiles * (a.Cout / BN));
+    hipLaunchKernelGGL((conv3x3_fwd_kernel<TH, TW, BN, BKC, WM, WN>), dim3(grid), dim3(256), 0, st,
+                       a);
+}
+
+}  // namespace
+}  // namespace ugpg
+
+using namespace ugpg;
+
+extern "C" int ugpg_conv3x3_fwd_ntiles(int B, int H, int W, int Cin, int Cout) {
+    (void)Cin;
+    const int cfg = pick_fwd_cfg(B, H, W, Cout, Cout);
+    return (int)(B * cdiv(H, kFwd[cfg].th) * cdiv(W, kFwd[cfg].tw));
+}
+
+extern "C" int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream) {
+    if (!p || !p->src[0].data || !p->wpk || !p->out[0]) {
+        set_error("conv3x3_fwd: null argument");
+        return UGPG_ERR_INVALID;
+    }
+    const int C0 = p->src[0].C, C1 = p->src[1].data ? p->src[1].C : 0;
+    const int Cin = C0 + C1;
+    if (Cin % 8 || C0 % 8 || p->Cout % 64 || p->B <= 0 || p->H <= 0 || p->W <= 0) {
+        set_error("conv3x3_fwd: unsupported shape Cin=%d (C0=%d) Cout=%d", Cin, C0, p->Cout);
+        return UGPG_ERR_INVALID;
+    }
+    if (p->out_split <= 0 || p->out_split > p->Cout || p->out_split % 64 ||
+        (p->out_split < p->Cout && !p->out[1])) {
+        set_error("conv3x3_fwd: bad out_split %d (Cout %d)", p->out_split, p->Cout);
+        return UGPG_ERR_INVALID;
+    }
+    ConvFwdArgs a;
+    a.src0 = p->src[0].data;
+    a.sc0 = p->src[0].scale;
+    a.sh0 = p->src[0].shift;
+    a.C0 = C0;
+    a.src1 = p->src[1].data;
+    a.sc1 = p->src[1].scale;
+    a.sh1 = p->src[1].shift;
+    a.C1 = C1;
+    a.wpk = p->wpk;
+    a.bias = p->bias;
+    a.out0 = p->out[0];
+    a.out1 = p->out[1];
+    a.split = p->out_split;
+    a.acc0 = p->accumulate[0];
+    a.acc1 = p->accumulate[1];
+    a.stats = p->stats;
+    a.B = p->B;
+    a.H = p->H;
+    a.W = p->W;
+    a.Cin = Cin;
+    a.Cout = p->Cout;
+    const int cfg = pick_fwd_cfg(p->B, p->H, p->W, p->Cout, p->out_split);
+    if (p->out_split % kFwd[cfg].bn) {
+        set_error("conv3x3_fwd: out_split %d not a multiple of the tile width %d", p->out_split,
+                  kFwd[cfg].bn);
+        return UGPG_ERR_INVALID;
+    }
+    const bool bk16 = (C0 % 16 == 0) && (C1 % 16 == 0);
+    const FwdShape& s = kFwd[cfg];
+    a.tiles_x = (int)cdiv(p->W, s.tw);
+    a.tiles_y = (int)cdiv(p->H, s.th);
+    a.ntiles = p->B * a.tiles_x * a.tiles_y;
+    hipStream_t st = as_stream(stream);
+    switch (cfg) {
+        case CFG_L:
+            if (bk16) launch_fwd<16, 16, 64, 16, 4, 1>(a, st);
+            else launch_fwd<16, 16, 64, 8, 4, 1>(a, st);
+            break;
+        case CFG_W:
+            launch_fwd<8, 16, 128, 8, 2, 2>(a, st);
+            break;
+        default:
+            if (bk16) launch_fwd<8, 8, 64, 16, 2, 2>(a, st);
+            else launch_fwd<8, 8, 64, 8, 2, 2>(a, st);
+            break;
+    }
+    return check_launch("conv3x3_fwd");
+}
+
+extern "C" int ugpg_pack_conv3x3(const float* w, float* wpk, int Cout, int Cin, int Cin_pad,
+                                 int mode, void* stream) {
+    if (!w || !wpk || Cin_pad < Cin || Cin_pad % 8 || (mode == 1 && Cout % 8) || mode < 0 ||
+        mode > 1) {
+        set_error("pack_conv3x3: bad arguments (Cout=%d Cin=%d Cin_pad=%d mode=%d)", Cout, Cin,
+                  Cin_pad, mode);
+        return UGPG_ERR_INVALID;
+    }
+    const int64_t total = (int64_t)Cin_pad * 9 * Cout;
+    hipLaunchKernelGGL(pack_conv3x3_kernel, dim3(stream_grid(total)), dim3(256), 0,
+                       as_stream(stream), w, wpk, Cout, Cin, Cin_pad, mode);
+    return check_launch("pack_conv3x3");
+}
+
+static int wgrad_check(const ugpg_wgrad_t* p) {
+    if (!p || !p->src[0].data || !p->dy || !p->dw) {
+        set_error("conv3x3_wgrad: null argument");
+        return UGPG_ERR_INVALID;
+    }
+    const int C0 = p->src[0].C, C1 = p->src[1].data ? p->src[1].C : 0;
+    if (p->Cout % 64 || C0 % 4 || (C1 && (C0 % 64 || C1 % 64)) || p->Cin_real > C0 + C1) {
+        set_error("conv3x3_wgrad: unsupported shape C0=%d C1=%d Cout=%d", C0, C1, p->Cout);
+        return UGPG_ERR_INVALID;
+    }
+    return UGPG_OK;
+}
+
+extern "C" size_t ugpg_conv3x3_wgrad_workspace(const ugpg_wgrad_t* p) {
+    if (wgrad_check(p)) return 0;
+    const int Cin = p->src[0].C + (p->src[1].data ? p->src[1].C : 0);
+    WgradPlan w = wgrad_plan(p->B, p->H, p->W, Cin, p->Cout);
+    return ((size_t)w.nsplit * 9 * p->Cout * Cin + (size_t)w.nsplit * p->Cout) * sizeof(float);
+}
+
+extern "C" int ugpg_conv3x3_wgrad(const ugpg_wgrad_t* p, void* ws, size_t ws_bytes,
+                                  void* stream) {
+    if (int e = wgrad_check(p)) return e;
+    const int C0 = p->src[0].C, C1 = p->src[1].data ? p->src[1].C : 0;
+    const int Cin = C0 + C1;
+    WgradPlan w = wgrad_plan(p->B, p->H, p->W, Cin, p->Cout);
+    const size_t need = ugpg_conv3x3_wgrad_workspace(p);
+    if (!ws || ws_bytes < need) {
+        set_error("conv3x3_wgrad: workspace %zu < %zu", ws_bytes, need);
+        return UGPG_ERR_WORKSPACE;
+    }
+    WgradArgs a;
+    a.src0 = p->src[0].data;
+    a.sc0 = p->src[0].scale;
+    a.sh0 = p->src[0].shift;
+    a.C0 = C0;
+    a.src1 = p->src[1].data;
+    a.sc1 = p->src[1].scale;
+    a.sh1 = p->src[1].shift;
+    a.C1 = C1;
+    a.dy = p->dy;
+    a.Cout = p->Cout;
+    a.Cin = Cin;
+    a.part = static_cast<float*>(ws);
+    a.dbpart = p->db ? a.part + (size_t)w.nsplit * 9 * p->Cout * Cin : nullptr;
+    a.B = p->B;
+    a.H = p->H;
+    a.W = p->W;
+    a.tiles_x = w.tiles_x;
+    a.tiles_y = w.tiles_y;
+    a.ntiles = w.ntiles;
+    a.nsplit = w.nsplit;
+    a.tps = w.tps;
+    hipStream_t st = as_stream(stream);
+    const unsigned grid = (unsigned)((p->Cout / 64) * cdiv(Cin, 64) * w.nsplit);
+    hipLaunchKernelGGL((conv3x3_wgrad_kernel<WG_TH, WG_TW>), dim3(grid), dim3(256), 0, st, a);
+    if (int e = check_launch("conv3x3_wgrad")) return e;
+    const int Cr = p->Cin_real > 0 ? p->Cin_real : Cin;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(stream_grid((int64_t)9 * p->Cout * Cr)),
+                       dim3(256), 0, st, a.part, a.dbpart, w.nsplit, p->Cout, Cin, Cr, p->dw,
+                       p->db, p->accumulate);
+    return check_launch("conv3x3_wgrad_reduce");
+}

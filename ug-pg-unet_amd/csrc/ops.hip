@@ -1,0 +1,1029 @@
+// Memory-bound kernels of the UG-PG-UNet hot path (gfx950, fp32):
+//   MaxPool2d(2)          UG_unet_parts.py:49                 (K8)
+//   bilinear x2 / resize  UG_unet_parts.py:78, UG_unet.py:36-53 (K9, K12)
+//   uncertainty map       UG_unet.py:45-57                      (K13)
+//   1x1 heads + sum       UG_unet_parts.py:84-91, UG_unet.py:294-303 (K11)
+//   weighted BCE          UG_unet.py:61-94, uncertainty_guided_trainer.py:64-65 (K13)
+//   Dice / accuracy       uncertainty_guided_trainer.py:90-123 (K14)
+//   RMSprop               uncertainty_guided_trainer.py:84-88  (K15)
+//   avgpool/Linear head   Herlev/train_herlev.py:66-77         (K16)
+// All reductions are deterministic (fixed-order block partials, fp64 merge).
+#include "common.h"
+
+namespace ugpg {
+
+// ---------------------------------------------------------------- max-pool
+__global__ void maxpool2_fwd_kernel(const float* x, const float* sc, const float* sh, int B, int H,
+                                    int W, int C, float* out, uint8_t* am) {
+    const int Ho = H / 2, Wo = W / 2, C4 = C / 4;
+    const int64_t total = (int64_t)B * Ho * Wo * C4;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(i % C4) * 4;
+        int64_t r = i / C4;
+        const int ox = (int)(r % Wo);
+        r /= Wo;
+        const int oy = (int)(r % Ho), b = (int)(r / Ho);
+        f32x4 best;
+        uint8_t idx[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int y = 2 * oy + (k >> 1), xx = 2 * ox + (k & 1);
+            f32x4 v = *reinterpret_cast<const f32x4*>(x + ((size_t)(b * H + y) * W + xx) * C + c);
+            v = act_apply4(v, sc, sh, c);
+            if (k == 0) {
+                best = v;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (v[j] > best[j] || isnan(v[j])) {
+                        best[j] = v[j];
+                        idx[j] = (uint8_t)k;
+                    }
+            }
+        }
+        *reinterpret_cast<f32x4*>(out + i * 4) = best;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) am[i * 4 + j] = idx[j];
+    }
+}
+
+__global__ void maxpool2_bwd_kernel(const float* dout, const uint8_t* am, int B, int H, int W,
+                                    int C, float* din, int acc) {
+    const int Ho = H / 2, Wo = W / 2, C4 = C / 4;
+    const int64_t total = (int64_t)B * H * W * C4;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(i % C4) * 4;
+        int64_t r = i / C4;
+        const int x = (int)(r % W);
+        r /= W;
+        const int y = (int)(r % H), b = (int)(r / H);
+        f32x4 g = {0.f, 0.f, 0.f, 0.f};
+        const int oy = y >> 1, ox = x >> 1;
+        if (oy < Ho && ox < Wo) {
+            const int k = (y & 1) * 2 + (x & 1);
+            const size_t o = ((size_t)(b * Ho + oy) * Wo + ox) * C + c;
+            const f32x4 d = *reinterpret_cast<const f32x4*>(dout + o);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) g[j] = am[o + j] == k ? d[j] : 0.f;
+        }
+        f32x4* dst = reinterpret_cast<f32x4*>(din + i * 4);
+        if (acc) g += *dst;
+        *dst = g;
+    }
+}
+
+// ------------------------------------------------- bilinear (align_corners)
+// gather-form backward: input index i collects from outputs o with i0(o)==i or i1(o)==i
+__device__ __forceinline__ void ac_range(int i, int in, int out, int& lo, int& hi) {
+    if (in == out) {
+        lo = hi = i;
+        return;
+    }
+    if (out == 1) {
+        lo = 0;
+        hi = 0;
+        return;
+    }
+    const float scale = (float)(in - 1) / (float)(out - 1);
+    if (scale <= 0.f) {
+        lo = 0;
+        hi = out - 1;
+        return;
+    }
+    lo = (int)floorf((float)(i - 1) / scale) - 1;
+    hi = (int)ceilf((float)(i + 1) / scale) + 1;
+    lo = lo < 0 ? 0 : lo;
+    hi = hi > out - 1 ? out - 1 : hi;
+}
+
+__device__ __forceinline__ float ac_weight(int o, int i, int in, int out) {
+    int i0, i1;
+    float l0, l1;
+    ac_index(o, in, out, i0, i1, l0, l1);
+    float w = 0.f;
+    if (i0 == i) w += l0;
+    if (i1 == i) w += l1;
+    return w;
+}
+
+__global__ void bilinear_nhwc_fwd_kernel(const float* x, const float* sc, const float* sh, int B,
+                                         int Hi, int Wi, int C, float* out, int Ho, int Wo) {
+    const int C4 = C / 4;
+    const int64_t total = (int64_t)B * Ho * Wo * C4;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(i % C4) * 4;
+        int64_t r = i / C4;
+        const int ox = (int)(r % Wo);
+        r /= Wo;
+        const int oy = (int)(r % Ho), b = (int)(r / Ho);
+        int y0, y1, x0, x1;
+        float ly0, ly1, lx0, lx1;
+        ac_index(oy, Hi, Ho, y0, y1, ly0, ly1);
+        ac_index(ox, Wi, Wo, x0, x1, lx0, lx1);
+        const float* base = x + (size_t)b * Hi * Wi * C + c;
+        const f32x4 a00 = act_apply4(*reinterpret_cast<const f32x4*>(base + ((size_t)y0 * Wi + x0) * C), sc, sh, c);
+        const f32x4 a01 = act_apply4(*reinterpret_cast<const f32x4*>(base + ((size_t)y0 * Wi + x1) * C), sc, sh, c);
+        const f32x4 a10 = act_apply4(*reinterpret_cast<const f32x4*>(base + ((size_t)y1 * Wi + x0) * C), sc, sh, c);
+        const f32x4 a11 = act_apply4(*reinterpret_cast<const f32x4*>(base + ((size_t)y1 * Wi + x1) * C), sc, sh, c);
+        const f32x4 v = ly0 * (lx0 * a00 + lx1 * a01) + ly1 * (lx0 * a10 + lx1 * a11);
+        *reinterpret_cast<f32x4*>(out + i * 4) = v;
+    }
+}
+
+__global__ void bilinear_nhwc_bwd_kernel(const float* dout, int B, int Ho, int Wo, int C,
+                                         float* din, int Hi, int Wi, int acc) {
+    const int C4 = C / 4;
+    const int64_t total = (int64_t)B * Hi * Wi * C4;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(i % C4) * 4;
+        int64_t r = i / C4;
+        const int ix = (int)(r % Wi);
+        r /= Wi;
+        const int iy = (int)(r % Hi), b = (int)(r / Hi);
+        int ylo, yhi, xlo, xhi;
+        ac_range(iy, Hi, Ho, ylo, yhi);
+        ac_range(ix, Wi, Wo, xlo, xhi);
+        f32x4 s = {0.f, 0.f, 0.f, 0.f};
+        for (int oy = ylo; oy <= yhi; ++oy) {
+            const float wy = ac_weight(oy, iy, Hi, Ho);
+            if (wy == 0.f) continue;
+            for (int ox = xlo; ox <= xhi; ++ox) {
+                const float wx = ac_weight(ox, ix, Wi, Wo);
+                if (wx == 0.f) continue;
+                const f32x4 d = *reinterpret_cast<const f32x4*>(
+                    dout + ((size_t)(b * Ho + oy) * Wo + ox) * C + c);
+                s += (wy * wx) * d;
+            }
+        }
+        f32x4* dst = reinterpret_cast<f32x4*>(din + i * 4);
+        if (acc) s += *dst;
+        *dst = s;
+    }
+}
+
+// ------------------------------------------------------------- NCHW resize
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+__device__ __forceinline__ int nearest_src(int o, int in, int out) {
+    if (in == out) return o;
+    if (out == 2 * in) return o >> 1;
+    const float scale = (float)in / (float)out;
+    const int s = (int)floorf((float)o * scale);
+    return s < in - 1 ? s : in - 1;
+}
+
+__global__ void resize_nchw_kernel(const float* in, int BC, int Hi, int Wi, float* out, int Ho,
+                                   int Wo, int mode) {
+    const int64_t total = (int64_t)BC * Ho * Wo;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int ox = (int)(i % Wo);
+        int64_t r = i / Wo;
+        const int oy = (int)(r % Ho);
+        const int64_t bc = r / Ho;
+        const float* src = in + bc * Hi * Wi;
+        float v;
+        if (mode == 1) {
+            v = src[(size_t)nearest_src(oy, Hi, Ho) * Wi + nearest_src(ox, Wi, Wo)];
+        } else {
+            int y0, y1, x0, x1;
+            float ly0, ly1, lx0, lx1;
+            ac_index(oy, Hi, Ho, y0, y1, ly0, ly1);
+            ac_index(ox, Wi, Wo, x0, x1, lx0, lx1);
+            float a00 = src[(size_t)y0 * Wi + x0], a01 = src[(size_t)y0 * Wi + x1];
+            float a10 = src[(size_t)y1 * Wi + x0], a11 = src[(size_t)y1 * Wi + x1];
+            if (mode == 2) {
+                a00 = sigmoidf_(a00);
+                a01 = sigmoidf_(a01);
+                a10 = sigmoidf_(a10);
+                a11 = sigmoidf_(a11);
+            }
+            v = ly0 * (lx0 * a00 + lx1 * a01) + ly1 * (lx0 * a10 + lx1 * a11);
+            if (mode == 2) v = 1.0f - 2.0f * fabsf(v - 0.5f);
+        }
+        out[i] = v;
+    }
+}
+
+__global__ void nchw_to_nhwc_kernel(const float* in, int B, int C, int HW, float* out, int Cp) {
+    const int64_t total = (int64_t)B * HW * Cp;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(i % Cp);
+        const int64_t r = i / Cp;
+        const int p = (int)(r % HW), b = (int)(r / HW);
+        out[i] = c < C ? in[((size_t)b * C + c) * HW + p] : 0.f;
+    }
+}
+
+__global__ void nhwc_to_nchw_kernel(const float* in, int B, int C, int HW, int Cs, float* out,
+                                    int acc) {
+    const int64_t total = (int64_t)B * C * HW;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int p = (int)(i % HW);
+        const int64_t r = i / HW;
+        const int c = (int)(r % C), b = (int)(r / C);
+        const float v = in[((size_t)b * HW + p) * Cs + c];
+        out[i] = acc ? out[i] + v : v;
+    }
+}
+
+// ------------------------------------------------------------------ heads
+// 16 lanes per pixel; lane16 owns channels {4*l16 + 64*j}.
+constexpr int HEAD_NC_MAX = 4, HEAD_CJ_MAX = 4;
+
+__global__ void __launch_bounds__(256) head_fwd_kernel(const float* x, const float* sc,
+                                                       const float* sh, int64_t npix, int C,
+                                                       const float* w, const float* bias, int nc,
+                                                       float* h) {
+    const int l16 = threadIdx.x & 15, CJ = C / 64;
+    for (int64_t p = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 4; p < npix;
+         p += ((int64_t)gridDim.x * blockDim.x) >> 4) {
+        float acc[HEAD_NC_MAX] = {0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < CJ; ++j) {
+            const int c = l16 * 4 + 64 * j;
+            const f32x4 v = act_apply4(*reinterpret_cast<const f32x4*>(x + p * C + c), sc, sh, c);
+            for (int k = 0; k < nc; ++k) {
+                const f32x4 wv = *reinterpret_cast<const f32x4*>(w + (size_t)k * C + c);
+                acc[k] += v.x * wv.x + v.y * wv.y + v.z * wv.z + v.w * wv.w;
+            }
+        }
+        for (int k = 0; k < nc; ++k) {
+            float s = acc[k];
+#pragma unroll
+            for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 16);
+            if (l16 == 0) h[p * nc + k] = s + bias[k];
+        }
+    }
+}
+
+struct HeadSet {
+    const float* h[4];
+    int res[4];
+    int n;
+};
+
+__global__ void heads_combine_kernel(HeadSet hs, int B, int H, int W, int nc, float* logits) {
+    const int64_t total = (int64_t)B * nc * H * W;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int x = (int)(i % W);
+        int64_t r = i / W;
+        const int y = (int)(r % H);
+        r /= H;
+        const int k = (int)(r % nc), b = (int)(r / nc);
+        float s = 0.f;
+        for (int j = 0; j < hs.n; ++j) {
+            const int R = hs.res[j];
+            const float* hp = hs.h[j] + (size_t)b * R * R * nc + k;
+            float v;
+            if (R == H) {
+                v = hp[((size_t)y * W + x) * nc];
+            } else {
+                int y0, y1, x0, x1;
+                float ly0, ly1, lx0, lx1;
+                ac_index(y, R, H, y0, y1, ly0, ly1);
+                ac_index(x, R, W, x0, x1, lx0, lx1);
+                v = ly0 * (lx0 * hp[((size_t)y0 * R + x0) * nc] + lx1 * hp[((size_t)y0 * R + x1) * nc]) +
+                    ly1 * (lx0 * hp[((size_t)y1 * R + x0) * nc] + lx1 * hp[((size_t)y1 * R + x1) * nc]);
+            }
+            s = (j == 0) ? v : s + v;
+        }
+        logits[i] = s;
+    }
+}
+
+// dh (NHWC, R x R, nc) from NCHW dlogits (H x W)
+__global__ void head_split_bwd_kernel(const float* dl, int B, int H, int W, int nc, float* dh,
+                                      int R) {
+    const int64_t total = (int64_t)B * R * R * nc;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int k = (int)(i % nc);
+        int64_t r = i / nc;
+        const int ix = (int)(r % R);
+        r /= R;
+        const int iy = (int)(r % R), b = (int)(r / R);
+        const float* src = dl + ((size_t)b * nc + k) * H * W;
+        float s;
+        if (R == H) {
+            s = src[(size_t)iy * W + ix];
+        } else {
+            int ylo, yhi, xlo, xhi;
+            ac_range(iy, R, H, ylo, yhi);
+            ac_range(ix, R, W, xlo, xhi);
+            s = 0.f;
+            for (int oy = ylo; oy <= yhi; ++oy) {
+                const float wy = ac_weight(oy, iy, R, H);
+                if (wy == 0.f) continue;
+                for (int ox = xlo; ox <= xhi; ++ox) {
+                    const float wx = ac_weight(ox, ix, R, W);
+                    if (wx == 0.f) continue;
+                    s += (wy * wx) * src[(size_t)oy * W + ox];
+                }
+            }
+        }
+        dh[i] = s;
+    }
+}
+
+// da (+)= dh @ w ; per-block partials of dW = dh^T act and db = sum dh
+__global__ void __launch_bounds__(256) head_bwd_kernel(const float* x, const float* sc,
+                                                       const float* sh, int64_t npix, int C,
+                                                       const float* w, int nc, const float* dh,
+                                                       float* da, int acc_da, int64_t ppb,
+                                                       float* part, int nblk) {
+    const int tid = threadIdx.x, l16 = tid & 15, slot = tid >> 4, CJ = C / 64;
+    f32x4 gw[HEAD_NC_MAX][HEAD_CJ_MAX];
+    float gb[HEAD_NC_MAX] = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < HEAD_NC_MAX; ++k)
+        for (int j = 0; j < HEAD_CJ_MAX; ++j) gw[k][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int64_t p0 = blockIdx.x * ppb, p1 = min(npix, p0 + ppb);
+    for (int64_t p = p0 + slot; p < p1; p += 16) {
+        float d[HEAD_NC_MAX];
+        for (int k = 0; k < nc; ++k) d[k] = dh[p * nc + k];
+        for (int j = 0; j < CJ; ++j) {
+            const int c = l16 * 4 + 64 * j;
+            const f32x4 v = act_apply4(*reinterpret_cast<const f32x4*>(x + p * C + c), sc, sh, c);
+            f32x4 g = {0.f, 0.f, 0.f, 0.f};
+            for (int k = 0; k < nc; ++k) {
+                g += d[k] * *reinterpret_cast<const f32x4*>(w + (size_t)k * C + c);
+                gw[k][j] += d[k] * v;
+            }
+            f32x4* dst = reinterpret_cast<f32x4*>(da + p * C + c);
+            if (acc_da) g += *dst;
+            *dst = g;
+        }
+        if (l16 == 0)
+            for (int k = 0; k < nc; ++k) gb[k] += d[k];
+    }
+    __shared__ f32x4 red[256];
+    __shared__ float redb[16];
+    for (int k = 0; k < nc; ++k) {
+        for (int j = 0; j < CJ; ++j) {
+            red[tid] = gw[k][j];
+            if (l16 == 0) redb[slot] = gb[k];
+            __syncthreads();
+            if (slot == 0) {
+                f32x4 s = red[l16];
+                for (int q = 1; q < 16; ++q) s += red[q * 16 + l16];
+                float* dst = part + ((size_t)blockIdx.x * nc + k) * (C + 1) + l16 * 4 + 64 * j;
+                dst[0] = s.x;
+                dst[1] = s.y;
+                dst[2] = s.z;
+                dst[3] = s.w;
+                if (l16 == 0 && j == 0) {
+                    float sb = 0.f;
+                    for (int q = 0; q < 16; ++q) sb += redb[q];
+                    part[((size_t)blockIdx.x * nc + k) * (C + 1) + C] = sb;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__global__ void head_bwd_finalize_kernel(const float* part, int nblk, int nc, int C, float* dw,
+                                         float* db) {
+    const int total = nc * (C + 1);
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+        double s = 0;
+        for (int i = 0; i < nblk; ++i) s += part[(size_t)i * total + e];
+        const int k = e / (C + 1), c = e % (C + 1);
+        if (c < C) dw[(size_t)k * C + c] = (float)s;
+        else if (db) db[k] = (float)s;
+    }
+}
+
+// ------------------------------------------------------------- UG loss
+__device__ __forceinline__ void block_sum2(double& a, double& b) {
+    __shared__ double sa[4], sb[4];
+    a = wave_sum_d(a);
+    b = wave_sum_d(b);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) {
+        sa[wave] = a;
+        sb[wave] = b;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        a = sa[0] + sa[1] + sa[2] + sa[3];
+        b = sb[0] + sb[1] + sb[2] + sb[3];
+    }
+}
+
+__device__ __forceinline__ float bce_pixel(float x, float t, float pw) {
+    const float lw = 1.0f + (pw - 1.0f) * t;
+    const float sp = log1pf(expf(-fabsf(x))) - fminf(x, 0.0f);  // softplus(-x) = -log_sigmoid(x)
+    return (1.0f - t) * x + lw * sp;
+}
+
+__device__ __forceinline__ float umap_at(const float* u, int64_t i, int C, int HW, int Cu) {
+    if (!u) return 0.f;
+    if (Cu == C) return u[i];
+    const int64_t p = i % HW, b = i / ((int64_t)C * HW);
+    return u[b * HW + p];
+}
+
+__global__ void __launch_bounds__(256) ug_loss_fwd_kernel(const float* x, const float* t,
+                                                          const float* u, int64_t n, int C, int HW,
+                                                          int Cu, const float* pwp, float alpha,
+                                                          const float* pixel_loss,
+                                                          double* part) {
+    const float pw = pwp ? pwp[0] : 1.0f;
+    double sp = 0, sw = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const float pl = pixel_loss ? pixel_loss[i] : bce_pixel(x[i], t[i], pw);
+        sp += pl;
+        sw += pl * (1.0f + alpha * umap_at(u, i, C, HW, Cu));
+    }
+    block_sum2(sp, sw);
+    if (threadIdx.x == 0) {
+        part[2 * blockIdx.x] = sp;
+        part[2 * blockIdx.x + 1] = sw;
+    }
+}
+
+__global__ void ug_loss_finalize_kernel(const double* part, int nblk, int64_t n, int has_u,
+                                        float* out) {
+    if (threadIdx.x != 0) return;
+    double sp = 0, sw = 0;
+    for (int i = 0; i < nblk; ++i) {
+        sp += part[2 * i];
+        sw += part[2 * i + 1];
+    }
+    out[0] = (float)((has_u ? sw : sp) / (double)n);
+    out[1] = (float)(sp / (double)n);
+}
+
+__global__ void ug_loss_bwd_kernel(const float* x, const float* t, const float* u, int64_t n,
+                                   int C, int HW, int Cu, const float* pwp, float alpha,
+                                   const float* gout, float* dx, int generic) {
+    const float pw = pwp ? pwp[0] : 1.0f;
+    const float g = gout[0] / (float)n;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const float w = 1.0f + alpha * umap_at(u, i, C, HW, Cu);
+        if (generic) {
+            dx[i] = g * w;
+        } else {
+            const float tt = t[i], xx = x[i];
+            const float lw = 1.0f + (pw - 1.0f) * tt;
+            const float sneg = 1.0f / (1.0f + expf(xx));  // sigmoid(-x)
+            dx[i] = g * w * ((1.0f - tt) - lw * sneg);
+        }
+    }
+}
+
+// ------------------------------------------------------------- metrics
+__global__ void __launch_bounds__(256) seg_metrics_kernel(const float* x, const float* t, int HW,
+                                                          int nbps, float* part) {
+    const int b = blockIdx.y;
+    float si = 0, sp = 0, st = 0, sw = 0;
+    const int per = (HW + nbps - 1) / nbps;
+    const int p0 = blockIdx.x * per, p1 = min(HW, p0 + per);
+    for (int p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
+        const size_t i = (size_t)b * HW + p;
+        const float pr = sigmoidf_(x[i]) > 0.5f ? 1.0f : 0.0f;
+        const float tv = t[i];
+        si += pr * tv;
+        sp += pr;
+        st += tv;
+        sw += (pr != truncf(tv)) ? 1.0f : 0.0f;
+    }
+    si = wave_sum(si);
+    sp = wave_sum(sp);
+    st = wave_sum(st);
+    sw = wave_sum(sw);
+    __shared__ float red[4][4];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) {
+        red[wave][0] = si;
+        red[wave][1] = sp;
+        red[wave][2] = st;
+        red[wave][3] = sw;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        const float s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+        part[((size_t)b * nbps + blockIdx.x) * 4 + threadIdx.x] = s;
+    }
+}
+
+__global__ void seg_metrics_finalize_kernel(const float* part, int B, int nbps, int64_t npix,
+                                            float* out) {
+    if (threadIdx.x != 0) return;
+    float dsum = 0.f;
+    double wrong = 0;
+    for (int b = 0; b < B; ++b) {
+        float s[4] = {0, 0, 0, 0};  // counts: exact in fp32
+        for (int k = 0; k < nbps; ++k)
+            for (int q = 0; q < 4; ++q) s[q] += part[((size_t)b * nbps + k) * 4 + q];
+        const float d = (2.0f * s[0] + 1.0f) / (s[1] + s[2] + 1.0f);
+        dsum += d;
+        wrong += s[3];
+    }
+    out[0] = dsum / (float)B;
+    out[1] = (float)(1.0 - wrong / (double)npix);
+    out[2] = (float)wrong;
+}
+
+__global__ void __launch_bounds__(256) mean_std_part_kernel(const float* x, int64_t n,
+                                                            int64_t per, double* part) {
+    const int64_t p0 = blockIdx.x * per, p1 = min(n, p0 + per);
+    double s = 0;
+    for (int64_t i = p0 + threadIdx.x; i < p1; i += blockDim.x) s += x[i];
+    double dummy = 0;
+    block_sum2(s, dummy);
+    __shared__ double mu_s;
+    if (threadIdx.x == 0) mu_s = s / (double)(p1 - p0);
+    __syncthreads();
+    const double mu = mu_s;
+    double q = 0;
+    for (int64_t i = p0 + threadIdx.x; i < p1; i += blockDim.x) {
+        const double d = x[i] - mu;
+        q += d * d;
+    }
+    dummy = 0;
+    __syncthreads();
+    block_sum2(q, dummy);
+    if (threadIdx.x == 0) {
+        part[3 * blockIdx.x] = (double)(p1 - p0);
+        part[3 * blockIdx.x + 1] = mu;
+        part[3 * blockIdx.x + 2] = q;
+    }
+}
+
+__global__ void mean_std_finalize_kernel(const double* part, int nblk, float* out) {
+    if (threadIdx.x != 0) return;
+    double n = 0, mu = 0, M = 0;
+    for (int i = 0; i < nblk; ++i) {
+        const double nb = part[3 * i];
+        if (nb <= 0) continue;
+        const double nn = n + nb, d = part[3 * i + 1] - mu;
+        mu += d * nb / nn;
+        M += part[3 * i + 2] + d * d * n * nb / nn;
+        n = nn;
+    }
+    out[0] = (float)mu;
+    out[1] = (float)(n > 1 ? sqrt(M / (n - 1)) : (double)NAN);
+}
+
+// ------------------------------------------------------------- RMSprop
+__global__ void rmsprop_kernel(float* p, const float* g, float* v, int64_t n, float lr, float alpha,
+                               float eps, float wd, float gs) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const float pv = p[i];
+        float gv = g[i];
+        if (gs != 1.0f) gv *= gs;
+        if (wd != 0.0f) gv = gv + wd * pv;
+        const float sa = v[i] * alpha + (1.0f - alpha) * (gv * gv);
+        v[i] = sa;
+        p[i] = pv + (-lr) * (gv / (sqrtf(sa) + eps));
+    }
+}
+
+__global__ void rmsprop4_kernel(f32x4* p, const f32x4* g, f32x4* v, int64_t n4, float lr,
+                                float alpha, float eps, float wd, float gs) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const f32x4 pv = p[i];
+        f32x4 gv = g[i], sv = v[i], out;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float gg = gv[k];
+            if (gs != 1.0f) gg *= gs;
+            if (wd != 0.0f) gg = gg + wd * pv[k];
+            const float sa = sv[k] * alpha + (1.0f - alpha) * (gg * gg);
+            sv[k] = sa;
+            out[k] = pv[k] + (-lr) * (gg / (sqrtf(sa) + eps));
+        }
+        v[i] = sv;
+        p[i] = out;
+    }
+}
+
+// ------------------------------------------------------------- Herlev head
+__global__ void avgpool_fwd_kernel(const float* x, const float* sc, const float* sh, int B, int HW,
+                                   int C, float* out) {
+    const int64_t total = (int64_t)B * C / 4;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(i % (C / 4)) * 4, b = (int)(i / (C / 4));
+        f32x4 s = {0.f, 0.f, 0.f, 0.f};
+        for (int p = 0; p < HW; ++p)
+            s += act_apply4(*reinterpret_cast<const f32x4*>(x + ((size_t)b * HW + p) * C + c), sc, sh, c);
+        *reinterpret_cast<f32x4*>(out + (size_t)b * C + c) = s / (float)HW;
+    }
+}
+
+__global__ void avgpool_bwd_kernel(const float* dout, int B, int HW, int C, float* da, int acc) {
+    const int64_t total = (int64_t)B * HW * C;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(i % C);
+        const int b = (int)(i / ((int64_t)HW * C));
+        const float v = dout[(size_t)b * C + c] / (float)HW;
+        da[i] = acc ? da[i] + v : v;
+    }
+}
+
+__global__ void linear_fwd_kernel(const float* x, const float* w, const float* b, int M, int N,
+                                  int K, int relu, float* y) {
+    // one wave per output element, lanes split K
+    const int lane = threadIdx.x & 63;
+    const int64_t total = (int64_t)M * N;
+    for (int64_t o = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; o < total;
+         o += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+        const int m = (int)(o / N), n = (int)(o % N);
+        float s = 0.f;
+        for (int k = lane; k < K; k += 64) s += x[(size_t)m * K + k] * w[(size_t)n * K + k];
+        s = wave_sum(s);
+        if (lane == 0) {
+            s += b ? b[n] : 0.f;
+            y[o] = relu ? fmaxf(s, 0.f) : s;
+        }
+    }
+}
+
+__global__ void linear_bwd_dx_kernel(const float* w, const float* dy, int M, int N, int K,
+                                     float* dx) {
+    const int64_t total = (int64_t)M * K;
+    for (int64_t o = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; o < total;
+         o += (int64_t)gridDim.x * blockDim.x) {
+        const int m = (int)(o / K), k = (int)(o % K);
+        float s = 0.f;
+        for (int n = 0; n < N; ++n) s += dy[(size_t)m * N + n] * w[(size_t)n * K + k];
+        dx[o] = s;
+    }
+}
+
+__global__ void linear_bwd_dw_kernel(const float* x, const float* dy, int M, int N, int K,
+                                     float* dw, float* db) {
+    const int64_t total = (int64_t)N * K;
+    for (int64_t o = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; o < total;
+         o += (int64_t)gridDim.x * blockDim.x) {
+        const int n = (int)(o / K), k = (int)(o % K);
+        float s = 0.f;
+        for (int m = 0; m < M; ++m) s += dy[(size_t)m * N + n] * x[(size_t)m * K + k];
+        dw[o] = s;
+        if (db && k == 0) {
+            float t = 0.f;
+            for (int m = 0; m < M; ++m) t += dy[(size_t)m * N + n];
+            db[n] = t;
+        }
+    }
+}
+
+__global__ void relu_bwd_kernel(const float* y, float* dy, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        if (!(y[i] > 0.f)) dy[i] = 0.f;
+}
+
+__global__ void mul_kernel(const float* x, const float* m, float* y, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        y[i] = x[i] * m[i];
+}
+
+namespace {
+int loss_nblk(int64_t n) {
+    int64_t b = cdiv(n, 256 * 16);
+    if (b > 1024) b = 1024;
+    return (int)(b < 1 ? 1 : b);
+}
+int head_nblk(int64_t npix, int64_t& ppb) {
+    int64_t b = cdiv(npix, 256);
+    if (b > 1024) b = 1024;
+    if (b < 1) b = 1;
+    ppb = cdiv(npix, b);
+    return (int)cdiv(npix, ppb);
+}
+int metrics_nbps(int HW) {
+    int n = (int)cdiv(HW, 4096);
+    return n < 1 ? 1 : (n > 64 ? 64 : n);
+}
+int ms_nblk(int64_t n, int64_t& per) {
+    int64_t b = cdiv(n, 4096);
+    if (b > 1024) b = 1024;
+    if (b < 1) b = 1;
+    per = cdiv(n, b);
+    return (int)cdiv(n, per);
+}
+}  // namespace
+}  // namespace ugpg
+
+using namespace ugpg;
+
+#define UGPG_REQUIRE(cond, name)                         \
+    do {                                                 \
+        if (!(cond)) {                                   \
+            set_error("%s: invalid argument (%s)", name, #cond); \
+            return UGPG_ERR_INVALID;                     \
+        }                                                \
+    } while (0)
+
+extern "C" int ugpg_maxpool2_fwd(ugpg_src_t s, int B, int H, int W, float* out, uint8_t* am,
+                                 void* stream) {
+    UGPG_REQUIRE(s.data && out && am && s.C % 4 == 0 && H >= 2 && W >= 2, "maxpool2_fwd");
+    const int64_t total = (int64_t)B * (H / 2) * (W / 2) * (s.C / 4);
+    hipLaunchKernelGGL(maxpool2_fwd_kernel, dim3(stream_grid(total)), dim3(256), 0,
+                       as_stream(stream), s.data, s.scale, s.shift, B, H, W, s.C, out, am);
+    return check_launch("maxpool2_fwd");
+}
+
+extern "C" int ugpg_maxpool2_bwd(const float* dout, const uint8_t* am, int B, int H, int W, int C,
+                                 float* din, int acc, void* stream) {
+    UGPG_REQUIRE(dout && am && din && C % 4 == 0, "maxpool2_bwd");
+    const int64_t total = (int64_t)B * H * W * (C / 4);
+    hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(stream_grid(total)), dim3(256), 0,
+                       as_stream(stream), dout, am, B, H, W, C, din, acc);
+    return check_launch("maxpool2_bwd");
+}
+
+extern "C" int ugpg_bilinear_nhwc_fwd(ugpg_src_t s, int B, int Hi, int Wi, float* out, int Ho,
+                                      int Wo, void* stream) {
+    UGPG_REQUIRE(s.data && out && s.C % 4 == 0 && Ho > 0 && Wo > 0, "bilinear_nhwc_fwd");
+    const int64_t total = (int64_t)B * Ho * Wo * (s.C / 4);
+    hipLaunchKernelGGL(bilinear_nhwc_fwd_kernel, dim3(stream_grid(total)), dim3(256), 0,
+                       as_stream(stream), s.data, s.scale, s.shift, B, Hi, Wi, s.C, out, Ho, Wo);
+    return check_launch("bilinear_nhwc_fwd");
+}
+
+extern "C" int ugpg_bilinear_nhwc_bwd(const float* dout, int B, int Ho, int Wo, int C, float* din,
+                                      int Hi, int Wi, int acc, void* stream) {
+    UGPG_REQUIRE(dout && din && C % 4 == 0, "bilinear_nhwc_bwd");
+    const int64_t total = (int64_t)B * Hi * Wi * (C / 4);
+    hipLaunchKernelGGL(bilinear_nhwc_bwd_kernel, dim3(stream_grid(total)), dim3(256), 0,
+                       as_stream(stream), dout, B, Ho, Wo, C, din, Hi, Wi, acc);
+    return check_launch("bilinear_nhwc_bwd");
+}
+
+extern "C" int ugpg_resize_nchw(const float* in, int B, int C, int Hi, int Wi, float* out, int Ho,
+                                int Wo, int mode, void* stream) {
+    UGPG_REQUIRE(in && out && mode >= 0 && mode <= 2 && Ho > 0 && Wo > 0, "resize_nchw");
+    const int64_t total = (int64_t)B * C * Ho * Wo;
+    hipLaunchKernelGGL(resize_nchw_kernel, dim3(stream_grid(total)), dim3(256), 0,
+                       as_stream(stream), in, B * C, Hi, Wi, out, Ho, Wo, mode);
+    return check_launch("resize_nchw");
+}
+
+extern "C" int ugpg_nchw_to_nhwc(const float* in, int B, int C, int H, int W, float* out, int Cp,
+                                 void* stream) {
+    UGPG_REQUIRE(in && out && Cp >= C, "nchw_to_nhwc");
+    const int64_t total = (int64_t)B * H * W * Cp;
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(stream_grid(total)), dim3(256), 0,
+                       as_stream(stream), in, B, C, H * W, out, Cp);
+    return check_launch("nchw_to_nhwc");
+}
+
+extern "C" int ugpg_nhwc_to_nchw(const float* in, int B, int C, int H, int W, int Cs, float* out,
+                                 int acc, void* stream) {
+    UGPG_REQUIRE(in && out && Cs >= C, "nhwc_to_nchw");
+    const int64_t total = (int64_t)B * H * W * C;
+    hipLaunchKernelGGL(nhwc_to_nchw_kernel, dim3(stream_grid(total)), dim3(256), 0,
+                       as_stream(stream), in, B, C, H * W, Cs, out, acc);
+    return check_launch("nhwc_to_nchw");
+}
+
+extern "C" int ugpg_head_fwd(ugpg_src_t s, int64_t npix, const float* w, const float* b, int nc,
+                             float* h, void* stream) {
+    UGPG_REQUIRE(s.data && w && b && h && s.C % 64 == 0 && s.C <= 64 * HEAD_CJ_MAX && nc >= 1 &&
+                     nc <= HEAD_NC_MAX,
+                 "head_fwd");
+    hipLaunchKernelGGL(head_fwd_kernel, dim3(stream_grid(npix * 16)), dim3(256), 0,
+                       as_stream(stream), s.data, s.scale, s.shift, npix, s.C, w, b, nc, h);
+    return check_launch("head_fwd");
+}
+
+extern "C" int ugpg_heads_combine(const float* const* h, const int* hres, int n, int B, int H,
+                                  int W, int nc, float* logits, void* stream) {
+    UGPG_REQUIRE(h && hres && n >= 1 && n <= 4 && logits && H == W, "heads_combine");
+    HeadSet hs;
+    hs.n = n;
+    for (int i = 0; i < 4; ++i) {
+        hs.h[i] = i < n ? h[i] : nullptr;
+        hs.res[i] = i < n ? hres[i] : 0;
+    }
+    const int64_t total = (int64_t)B * nc * H * W;
+    hipLaunchKernelGGL(heads_combine_kernel, dim3(stream_grid(total)), dim3(256), 0,
+                       as_stream(stream), hs, B, H, W, nc, logits);
+    return check_launch("heads_combine");
+}
+
+extern "C" int ugpg_heads_split_bwd(const float* dl, int B, int H, int W, int nc, float* const* dh,
+                                    const int* hres, int n, void* stream) {
+    UGPG_REQUIRE(dl && dh && hres && n >= 1 && H == W, "heads_split_bwd");
+    for (int i = 0; i < n; ++i) {
+        const int64_t total = (int64_t)B * hres[i] * hres[i] * nc;
+        hipLaunchKernelGGL(head_split_bwd_kernel, dim3(stream_grid(total)), dim3(256), 0,
+                           as_stream(stream), dl, B, H, W, nc, dh[i], hres[i]);
+        if (int e = check_launch("heads_split_bwd")) return e;
+    }
+    return UGPG_OK;
+}
+
+extern "C" size_t ugpg_head_bwd_workspace(int64_t npix, int C, int nc) {
+    int64_t ppb;
+    const int nblk = head_nblk(npix, ppb);
+    return (size_t)nblk * nc * (C + 1) * sizeof(float);
+}
+
+extern "C" int ugpg_head_bwd(ugpg_src_t s, int64_t npix, const float* w, int nc, const float* dh,
+                             float* dw, float* db, float* da, int acc_da, void* ws,
+                             size_t ws_bytes, void* stream) {
+    UGPG_REQUIRE(s.data && w && dh && dw && da && s.C % 64 == 0 && s.C <= 64 * HEAD_CJ_MAX &&
+                     nc >= 1 && nc <= HEAD_NC_MAX,
+                 "head_bwd");
+    const size_t need = ugpg_head_bwd_workspace(npix, s.C, nc);
+    if (!ws || ws_bytes < need) {
+        set_error("head_bwd: workspace %zu < %zu", ws_bytes, need);
+        return UGPG_ERR_WORKSPACE;
+    }
+    int64_t ppb;
+    const int nblk = head_nblk(npix, ppb);
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(head_bwd_kernel, dim3(nblk), dim3(256), 0, st, s.data, s.scale, s.shift,
+                       npix, s.C, w, nc, dh, da, acc_da, ppb, static_cast<float*>(ws), nblk);
+    if (int e = check_launch("head_bwd")) return e;
+    hipLaunchKernelGGL(head_bwd_finalize_kernel, dim3(cdiv(nc * (s.C + 1), 256)), dim3(256), 0,
+                       st, static_cast<const float*>(ws), nblk, nc, s.C, dw, db);
+    return check_launch("head_bwd_finalize");
+}
+
+extern "C" size_t ugpg_ug_loss_workspace(int64_t n) { return (size_t)loss_nblk(n) * 2 * sizeof(double); }
+
+static int loss_fwd_common(const float* x, const float* t, const float* u, int B, int C, int HW,
+                           int Cu, const float* pw, float alpha, const float* pl, float* out,
+                           void* ws, size_t ws_bytes, void* stream, const char* name) {
+    UGPG_REQUIRE(out && (pl || (x && t)) && (!u || Cu == 1 || Cu == C), name);
+    const int64_t n = (int64_t)B * C * HW;
+    const size_t need = ugpg_ug_loss_workspace(n);
+    if (!ws || ws_bytes < need) {
+        set_error("%s: workspace %zu < %zu", name, ws_bytes, need);
+        return UGPG_ERR_WORKSPACE;
+    }
+    const int nblk = loss_nblk(n);
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(ug_loss_fwd_kernel, dim3(nblk), dim3(256), 0, st, x, t, u, n, C, HW, Cu, pw,
+                       alpha, pl, static_cast<double*>(ws));
+    if (int e = check_launch(name)) return e;
+    hipLaunchKernelGGL(ug_loss_finalize_kernel, dim3(1), dim3(64), 0, st,
+                       static_cast<const double*>(ws), nblk, n, u ? 1 : 0, out);
+    return check_launch(name);
+}
+
+extern "C" int ugpg_ug_loss_fwd(const float* x, const float* t, const float* u, int B, int C,
+                                int HW, int Cu, const float* pw, float alpha, float* out,
+                                void* ws, size_t ws_bytes, void* stream) {
+    return loss_fwd_common(x, t, u, B, C, HW, Cu, pw, alpha, nullptr, out, ws, ws_bytes, stream,
+                           "ug_loss_fwd");
+}
+
+extern "C" int ugpg_ug_loss_bwd(const float* x, const float* t, const float* u, int B, int C,
+                                int HW, int Cu, const float* pw, float alpha, const float* gout,
+                                float* dx, void* stream) {
+    UGPG_REQUIRE(x && t && gout && dx && (!u || Cu == 1 || Cu == C), "ug_loss_bwd");
+    const int64_t n = (int64_t)B * C * HW;
+    hipLaunchKernelGGL(ug_loss_bwd_kernel, dim3(stream_grid(n)), dim3(256), 0, as_stream(stream),
+                       x, t, u, n, C, HW, Cu, pw, alpha, gout, dx, 0);
+    return check_launch("ug_loss_bwd");
+}
+
+extern "C" int ugpg_weighted_mean_fwd(const float* pl, const float* u, int B, int C, int HW,
+                                      int Cu, float alpha, float* out, void* ws, size_t ws_bytes,
+                                      void* stream) {
+    UGPG_REQUIRE(pl, "weighted_mean_fwd");
+    return loss_fwd_common(nullptr, nullptr, u, B, C, HW, Cu, nullptr, alpha, pl, out, ws,
+                           ws_bytes, stream, "weighted_mean_fwd");
+}
+
+extern "C" int ugpg_weighted_mean_bwd(const float* u, int B, int C, int HW, int Cu, float alpha,
+                                      const float* gout, float* dpl, void* stream) {
+    UGPG_REQUIRE(gout && dpl && (!u || Cu == 1 || Cu == C), "weighted_mean_bwd");
+    const int64_t n = (int64_t)B * C * HW;
+    hipLaunchKernelGGL(ug_loss_bwd_kernel, dim3(stream_grid(n)), dim3(256), 0, as_stream(stream),
+                       nullptr, nullptr, u, n, C, HW, Cu, nullptr, alpha, gout, dpl, 1);
+    return check_launch("weighted_mean_bwd");
+}
+
+extern "C" size_t ugpg_seg_metrics_workspace(int B) {
+    return (size_t)B * 64 * 4 * sizeof(float);
+}
+
+extern "C" int ugpg_seg_metrics(const float* x, const float* t, int B, int HW, float* out, void* ws,
+                                size_t ws_bytes, void* stream) {
+    UGPG_REQUIRE(x && t && out && B > 0 && HW > 0, "seg_metrics");
+    const int nbps = metrics_nbps(HW);
+    const size_t need = (size_t)B * nbps * 4 * sizeof(float);
+    if (!ws || ws_bytes < need) {
+        set_error("seg_metrics: workspace %zu < %zu", ws_bytes, need);
+        return UGPG_ERR_WORKSPACE;
+    }
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(seg_metrics_kernel, dim3(nbps, B), dim3(256), 0, st, x, t, HW, nbps,
+                       static_cast<float*>(ws));
+    if (int e = check_launch("seg_metrics")) return e;
+    hipLaunchKernelGGL(seg_metrics_finalize_kernel, dim3(1), dim3(64), 0, st,
+                       static_cast<const float*>(ws), B, nbps, (int64_t)B * HW, out);
+    return check_launch("seg_metrics_finalize");
+}
+
+extern "C" size_t ugpg_mean_std_workspace(int64_t n) {
+    int64_t per;
+    return (size_t)ms_nblk(n, per) * 3 * sizeof(double);
+}
+
+extern "C" int ugpg_mean_std(const float* x, int64_t n, float* out, void* ws, size_t ws_bytes,
+                             void* stream) {
+    UGPG_REQUIRE(x && out && n > 0, "mean_std");
+    int64_t per;
+    const int nblk = ms_nblk(n, per);
+    if (!ws || ws_bytes < (size_t)nblk * 3 * sizeof(double)) {
+        set_error("mean_std: workspace too small");
+        return UGPG_ERR_WORKSPACE;
+    }
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(mean_std_part_kernel, dim3(nblk), dim3(256), 0, st, x, n, per,
+                       static_cast<double*>(ws));
+    if (int e = check_launch("mean_std")) return e;
+    hipLaunchKernelGGL(mean_std_finalize_kernel, dim3(1), dim3(64), 0, st,
+                       static_cast<const double*>(ws), nblk, out);
+    return check_launch("mean_std_finalize");
+}
+
+extern "C" int ugpg_rmsprop_step(float* p, const float* g, float* v, int64_t n, float lr,
+                                 float alpha, float eps, float wd, float gs, void* stream) {
+    UGPG_REQUIRE(p && g && v && n >= 0, "rmsprop_step");
+    if (n == 0) return UGPG_OK;
+    hipStream_t st = as_stream(stream);
+    const bool al = ((uintptr_t)p % 16 == 0) && ((uintptr_t)g % 16 == 0) && ((uintptr_t)v % 16 == 0);
+    if (al && n % 4 == 0) {
+        hipLaunchKernelGGL(rmsprop4_kernel, dim3(stream_grid(n / 4)), dim3(256), 0, st,
+                           reinterpret_cast<f32x4*>(p), reinterpret_cast<const f32x4*>(g),
+                           reinterpret_cast<f32x4*>(v), n / 4, lr, alpha, eps, wd, gs);
+    } else {
+        hipLaunchKernelGGL(rmsprop_kernel, dim3(stream_grid(n)), dim3(256), 0, st, p, g, v, n, lr,
+                           alpha, eps, wd, gs);
+    }
+    return check_launch("rmsprop_step");
+}
+
+extern "C" int ugpg_avgpool_fwd(ugpg_src_t s, int B, int HW, float* out, void* stream) {
+    UGPG_REQUIRE(s.data && out && s.C % 4 == 0, "avgpool_fwd");
+    hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(stream_grid((int64_t)B * s.C / 4)), dim3(256), 0,
+                       as_stream(stream), s.data, s.scale, s.shift, B, HW, s.C, out);
+    return check_launch("avgpool_fwd");
+}
+
+extern "C" int ugpg_avgpool_bwd(const float* dout, int B, int HW, int C, float* da, int acc,
+                                void* stream) {
+    UGPG_REQUIRE(dout && da, "avgpool_bwd");
+    hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(stream_grid((int64_t)B * HW * C)), dim3(256), 0,
+                       as_stream(stream), dout, B, HW, C, da, acc);
+    return check_launch("avgpool_bwd");
+}
+
+extern "C" int ugpg_linear_fwd(const float* x, const float* w, const float* b, int M, int N, int K,
+                               int relu, float* y, void* stream) {
+    UGPG_REQUIRE(x && w && y && M > 0 && N > 0 && K > 0, "linear_fwd");
+    hipLaunchKernelGGL(linear_fwd_kernel, dim3(stream_grid((int64_t)M * N * 64)), dim3(256), 0,
+                       as_stream(stream), x, w, b, M, N, K, relu, y);
+    return check_launch("linear_fwd");
+}
+
+extern "C" int ugpg_linear_bwd(const float* x, const float* w, const float* dy, int M, int N,
+                               int K, float* dx, float* dw, float* db, void* stream) {
+    UGPG_REQUIRE(x && w && dy && dw, "linear_bwd");
+    hipStream_t st = as_stream(stream);
+    if (dx) {
+        hipLaunchKernelGGL(linear_bwd_dx_kernel, dim3(stream_grid((int64_t)M * K)), dim3(256), 0,
+                           st, w, dy, M, N, K, dx);
+        if (int e = check_launch("linear_bwd_dx")) return e;
+    }
+    hipLaunchKernelGGL(linear_bwd_dw_kernel, dim3(stream_grid((int64_t)N * K)), dim3(256), 0, st,
+                       x, dy, M, N, K, dw, db);
+    return check_launch("linear_bwd_dw");
+}
+
+extern "C" int ugpg_relu_bwd(const float* y, float* dy, int64_t n, void* stream) {
+    UGPG_REQUIRE(y && dy, "relu_bwd");
+    hipLaunchKernelGGL(relu_bwd_kernel, dim3(stream_grid(n)), dim3(256), 0, as_stream(stream), y,
+                       dy, n);
+    return check_launch("relu_bwd");
+}
+
+extern "C" int ugpg_mul(const float* x, const float* m, float* y, int64_t n, void* stream) {
+    UGPG_REQUIRE(x && m && y, "mul");
+    hipLaunchKernelGGL(mul_kernel, dim3(stream_grid(n)), dim3(256), 0, as_stream(stream), x, m, y,
+                       n);
+    return check_launch("mul");
+}

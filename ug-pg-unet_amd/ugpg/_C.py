@@ -1,0 +1,114 @@
+"""ctypes binding of libugpg.so (the C-ABI declared in include/ugpg.h).
+
+The library is built in-tree by ``ug-pg-unet_amd/build.py`` (or
+``__graft_entry__.build()``).  There is deliberately no fallback: if the shared
+library is missing every hot-path op raises immediately.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+LIB_PATH = Path(os.environ.get("UGPG_LIB", Path(__file__).resolve().parent / "libugpg.so"))
+
+c_float_p = C.c_void_p
+_i, _i64, _f, _p, _sz = C.c_int, C.c_int64, C.c_float, C.c_void_p, C.c_size_t
+
+
+class Src(C.Structure):
+    """ugpg_src_t: lazily-activated NHWC operand."""
+    _fields_ = [("data", _p), ("scale", _p), ("shift", _p), ("C", _i)]
+
+
+class ConvDesc(C.Structure):
+    """ugpg_conv_t."""
+    _fields_ = [("B", _i), ("H", _i), ("W", _i), ("src", Src * 2), ("wpk", _p), ("bias", _p),
+                ("Cout", _i), ("out", _p * 2), ("out_split", _i), ("accumulate", _i * 2),
+                ("stats", _p)]
+
+
+class WgradDesc(C.Structure):
+    """ugpg_wgrad_t."""
+    _fields_ = [("B", _i), ("H", _i), ("W", _i), ("src", Src * 2), ("dy", _p), ("Cout", _i),
+                ("dw", _p), ("Cin_real", _i), ("db", _p), ("accumulate", _i)]
+
+
+# name -> (restype, argtypes); must match include/ugpg.h exactly
+SIGNATURES = {
+    "ugpg_version": (C.c_char_p, []),
+    "ugpg_last_error": (C.c_char_p, []),
+    "ugpg_conv3x3_fwd": (_i, [C.POINTER(ConvDesc), _p]),
+    "ugpg_conv3x3_fwd_ntiles": (_i, [_i, _i, _i, _i, _i]),
+    "ugpg_pack_conv3x3": (_i, [_p, _p, _i, _i, _i, _i, _p]),
+    "ugpg_conv3x3_wgrad_workspace": (_sz, [C.POINTER(WgradDesc)]),
+    "ugpg_conv3x3_wgrad": (_i, [C.POINTER(WgradDesc), _p, _sz, _p]),
+    "ugpg_bn_finalize": (_i, [_p, _i, _i, _p, _p, _p, _p, _p, _f, _f, _p, _p, _p, _p, _p]),
+    "ugpg_bn_eval_params": (_i, [_p, _p, _p, _p, _f, _i, _p, _p, _p]),
+    "ugpg_bn_relu_bwd_workspace": (_sz, [_i64, _i]),
+    "ugpg_bn_relu_bwd": (_i, [_p, _p, _i64, _i, _p, _p, _p, _p, _p, _p, _p, _i, _p, _sz, _p]),
+    "ugpg_bn_relu_apply": (_i, [Src, _i64, _p, _p]),
+    "ugpg_maxpool2_fwd": (_i, [Src, _i, _i, _i, _p, _p, _p]),
+    "ugpg_maxpool2_bwd": (_i, [_p, _p, _i, _i, _i, _i, _p, _i, _p]),
+    "ugpg_bilinear_nhwc_fwd": (_i, [Src, _i, _i, _i, _p, _i, _i, _p]),
+    "ugpg_bilinear_nhwc_bwd": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _i, _p]),
+    "ugpg_resize_nchw": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _i, _p]),
+    "ugpg_nchw_to_nhwc": (_i, [_p, _i, _i, _i, _i, _p, _i, _p]),
+    "ugpg_nhwc_to_nchw": (_i, [_p, _i, _i, _i, _i, _i, _p, _i, _p]),
+    "ugpg_head_fwd": (_i, [Src, _i64, _p, _p, _i, _p, _p]),
+    "ugpg_heads_combine": (_i, [_p, _p, _i, _i, _i, _i, _i, _p, _p]),
+    "ugpg_heads_split_bwd": (_i, [_p, _i, _i, _i, _i, _p, _p, _i, _p]),
+    "ugpg_head_bwd_workspace": (_sz, [_i64, _i, _i]),
+    "ugpg_head_bwd": (_i, [Src, _i64, _p, _i, _p, _p, _p, _p, _i, _p, _sz, _p]),
+    "ugpg_ug_loss_workspace": (_sz, [_i64]),
+    "ugpg_ug_loss_fwd": (_i, [_p, _p, _p, _i, _i, _i, _i, _p, _f, _p, _p, _sz, _p]),
+    "ugpg_ug_loss_bwd": (_i, [_p, _p, _p, _i, _i, _i, _i, _p, _f, _p, _p, _p]),
+    "ugpg_weighted_mean_fwd": (_i, [_p, _p, _i, _i, _i, _i, _f, _p, _p, _sz, _p]),
+    "ugpg_weighted_mean_bwd": (_i, [_p, _i, _i, _i, _i, _f, _p, _p, _p]),
+    "ugpg_seg_metrics_workspace": (_sz, [_i]),
+    "ugpg_seg_metrics": (_i, [_p, _p, _i, _i, _p, _p, _sz, _p]),
+    "ugpg_mean_std_workspace": (_sz, [_i64]),
+    "ugpg_mean_std": (_i, [_p, _i64, _p, _p, _sz, _p]),
+    "ugpg_rmsprop_step": (_i, [_p, _p, _p, _i64, _f, _f, _f, _f, _f, _p]),
+    "ugpg_avgpool_fwd": (_i, [Src, _i, _i, _p, _p]),
+    "ugpg_avgpool_bwd": (_i, [_p, _i, _i, _i, _p, _i, _p]),
+    "ugpg_linear_fwd": (_i, [_p, _p, _p, _i, _i, _i, _i, _p, _p]),
+    "ugpg_linear_bwd": (_i, [_p, _p, _p, _i, _i, _i, _p, _p, _p, _p]),
+    "ugpg_relu_bwd": (_i, [_p, _p, _i64, _p]),
+    "ugpg_mul": (_i, [_p, _p, _p, _i64, _p]),
+}
+
+
+class _Lib:
+    def __init__(self):
+        self._lib = None
+
+    def load(self):
+        if self._lib is None:
+            if not LIB_PATH.exists():
+                raise ImportError(
+                    f"ugpg: native library {LIB_PATH} not found -- build it with "
+                    "`python ug-pg-unet_amd/build.py` (hipcc, gfx950). There is no CPU fallback.")
+            lib = C.CDLL(str(LIB_PATH))
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            self._lib = lib
+        return self._lib
+
+    def __getattr__(self, name):
+        return getattr(self.load(), name)
+
+
+lib = _Lib()
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib.ugpg_last_error().decode(errors="replace")
+        raise RuntimeError(f"ugpg {what} failed ({rc}): {msg}")
+
+
+def version() -> str:
+    return lib.ugpg_version().decode()

@@ -1,0 +1,270 @@
+"""Forward/backward executor for the Progressive U-Net graph on libugpg kernels.
+
+A network is a list of DoubleConv *blocks* (InConv / Down / Up, reference
+UG_unet_parts.py:5-81) plus optional 1x1 deep-supervision *heads*
+(UG_unet_parts.py:84-91, UG_unet.py:294-303).  Every block output is kept as a
+lazily-activated NHWC tensor ``Act(y, scale, shift)``: the second conv's raw
+output plus its folded BatchNorm affine; consumers (max-pool, bilinear x2, the
+next conv, the heads) apply ``relu(scale*y+shift)`` while loading.  The
+backward pass is an explicit schedule (heads -> decoder -> encoder -> inc) that
+writes parameter gradients straight into caller-provided tensors (views of one
+flat gradient buffer) and accumulates activation gradients in place, so no
+PyTorch arithmetic runs anywhere on the path.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import torch
+
+from . import ops
+from .ops import Act
+
+
+def ceil_to(v: int, m: int) -> int:
+    return (v + m - 1) // m * m
+
+
+@dataclass
+class Block:
+    """One DoubleConv application.  kind: 'inc' (image input), 'down' (maxpool of
+    inputs[0]) or 'up' (cat([inputs[0] (skip), up2x(inputs[1])]))."""
+    mod: torch.nn.Module
+    kind: str
+    inputs: tuple = ()
+
+
+@dataclass
+class Head:
+    mod: torch.nn.Module  # OutConv (holds .conv 1x1)
+    block: int
+
+
+@dataclass
+class BlockCtx:
+    srcs: list
+    y1: torch.Tensor = None
+    st1: tuple = None
+    y2: torch.Tensor = None
+    st2: tuple = None
+    extra: dict = field(default_factory=dict)
+
+
+def _conv_bn(seq):
+    return (seq[0], seq[1]), (seq[3], seq[4])
+
+
+def _bn_mode(bn):
+    return bn.training or not bn.track_running_stats
+
+
+def double_conv_forward(mod, srcs, ctx: BlockCtx, save: bool):
+    """conv3x3 -> BN -> ReLU, twice (UG_unet_parts.py:9-16) on Act inputs."""
+    B, H, W, _ = srcs[0].shape
+    cin = sum(s.C for s in srcs)
+    cur = srcs
+    for i, (conv, bn) in enumerate(_conv_bn(mod.conv_op)):
+        w = conv.weight
+        cout = w.shape[0]
+        if w.shape[1] > cin:
+            raise ValueError(f"conv expects {w.shape[1]} input channels, got {cin}")
+        wpk = ops.pack_conv3x3(w.detach(), cin, 0)
+        y = ops.empty(B, H, W, cout, like=srcs[0].y)
+        train = _bn_mode(bn)
+        stats = None
+        ntiles = 0
+        if train:
+            ntiles = ops.conv_ntiles(B, H, W, cin, cout)
+            stats = ops.empty(3 * cout * ntiles, like=y)
+        bias = conv.bias.detach() if conv.bias is not None else None
+        ops.conv3x3_fwd(cur, wpk, bias, cout, [y], stats=stats,
+                        flops=2.0 * B * H * W * cout * 9 * w.shape[1])
+        if train:
+            if bn.momentum is None:
+                raise NotImplementedError("BatchNorm2d(momentum=None) is not supported")
+            track = bn.track_running_stats and bn.running_mean is not None
+            mean, invstd, scale, shift = ops.bn_finalize(
+                stats, ntiles, bn.weight.detach(), bn.bias.detach(),
+                bn.running_mean if track else None, bn.running_var if track else None,
+                bn.num_batches_tracked if track else None, float(bn.momentum), float(bn.eps))
+            st = (mean, invstd, scale, shift)
+        else:
+            scale, shift = ops.bn_eval_params(bn.weight.detach(), bn.bias.detach(),
+                                              bn.running_mean, bn.running_var, float(bn.eps))
+            st = (None, None, scale, shift)
+        if save:
+            if i == 0:
+                ctx.y1, ctx.st1 = y, st
+            else:
+                ctx.y2, ctx.st2 = y, st
+        cur = [Act(y, scale, shift)]
+        cin = cout
+    return cur[0]
+
+
+def _bn_relu_wgrad(conv, bn, y, st, in_srcs, dy, grads):
+    """In place: dy <- dL/d(conv output) from dL/d(relu(bn(y))); then dW, db."""
+    mean, invstd, scale, shift = st
+    if mean is None:
+        raise RuntimeError("backward through an eval-mode BatchNorm is not supported")
+    ops.bn_relu_bwd(dy, y, mean, invstd, scale, shift, dy, grads.get(bn.weight),
+                    grads.get(bn.bias))
+    dw, db = grads.get(conv.weight), grads.get(conv.bias)
+    if dw is not None or db is not None:
+        if dw is None:
+            dw = torch.empty_like(conv.weight)
+        co, ci = conv.weight.shape[0], conv.weight.shape[1]
+        ops.conv3x3_wgrad(in_srcs, dy, dw, db, ci, flops=2.0 * dy.numel() / co * co * 9 * ci)
+
+
+def double_conv_backward(mod, ctx: BlockCtx, da2, targets, acc_flags, grads, pad_out=None):
+    """Backward of one DoubleConv given dL/d(block output) `da2` (overwritten).
+
+    targets: per input source, a tensor to receive dL/d(source activation) (or
+    None); acc_flags: accumulate into it.  grads: {param: destination or None}.
+    pad_out: padded channel count of a single dgrad target (the image input)."""
+    (c1, b1), (c2, b2) = _conv_bn(mod.conv_op)
+    B, H, W, cout = ctx.y2.shape
+    a1 = Act(ctx.y1, ctx.st1[2], ctx.st1[3])
+    # stage 2: BN2/ReLU backward, wgrad(conv2), dgrad(conv2) -> dL/d(a1)
+    _bn_relu_wgrad(c2, b2, ctx.y2, ctx.st2, [a1], da2, grads)
+    cmid = c2.weight.shape[1]
+    da1 = ops.empty(B, H, W, cmid, like=da2)
+    npix = B * H * W
+    ops.conv3x3_fwd([Act(da2)], ops.pack_conv3x3(c2.weight.detach(), cmid, 1), None, cmid, [da1],
+                    flops=2.0 * npix * cmid * 9 * cout)
+    # stage 1: BN1/ReLU backward, wgrad(conv1), dgrad(conv1) -> source targets
+    _bn_relu_wgrad(c1, b1, ctx.y1, ctx.st1, ctx.srcs, da1, grads)
+    if not any(t is not None for t in targets):
+        return
+    cin = c1.weight.shape[1]
+    fl = 2.0 * npix * cin * 9 * cmid
+    if pad_out is not None:
+        wpk = ops.pack_conv3x3(c1.weight.detach(), pad_out, 1)
+        ops.conv3x3_fwd([Act(da1)], wpk, None, pad_out, [targets[0]], accumulate=(acc_flags[0], 0),
+                        flops=fl)
+        return
+    wpk = ops.pack_conv3x3(c1.weight.detach(), cin, 1)
+    if len(targets) == 1:
+        ops.conv3x3_fwd([Act(da1)], wpk, None, cin, [targets[0]], accumulate=(acc_flags[0], 0),
+                        flops=fl)
+    else:
+        ops.conv3x3_fwd([Act(da1)], wpk, None, cin, [targets[0], targets[1]],
+                        split=ctx.srcs[0].C, accumulate=(acc_flags[0], acc_flags[1]), flops=fl)
+
+
+class UNetGraph:
+    """Executes blocks + heads.  `heads` empty -> the output is the last block's
+    activation (encoder-only graphs, e.g. the Herlev classifier)."""
+
+    def __init__(self, blocks, heads=()):
+        self.blocks = list(blocks)
+        self.heads = list(heads)
+
+    # -------------------------------------------------------------- forward
+    def forward(self, x, save: bool):
+        if x.dim() != 4:
+            raise ValueError(f"expected NCHW input, got shape {tuple(x.shape)}")
+        B, cx, H, W = x.shape
+        cpad = ceil_to(cx, 8)
+        x0 = ops.nchw_to_nhwc(x.detach().to(torch.float32), cpad)
+        outs, ctxs = [], []
+        for blk in self.blocks:
+            ctx = BlockCtx(srcs=[])
+            if blk.kind == "inc":
+                srcs = [Act(x0)]
+            elif blk.kind == "down":
+                a = outs[blk.inputs[0]]
+                p, am = ops.maxpool2_fwd(a)
+                ctx.extra["argmax"] = am
+                ctx.extra["in_hw"] = a.shape[1:3]
+                srcs = [Act(p)]
+            elif blk.kind == "up":
+                skip, low = outs[blk.inputs[0]], outs[blk.inputs[1]]
+                _, h, w, _ = low.shape
+                u = ops.bilinear_nhwc_fwd(low, 2 * h, 2 * w)
+                if u.shape[1:3] != skip.shape[1:3]:
+                    raise ValueError("Up: upsampled size does not match the skip connection")
+                ctx.extra["low_hw"] = (h, w)
+                srcs = [skip, Act(u)]
+            else:
+                raise ValueError(blk.kind)
+            ctx.srcs = srcs
+            outs.append(double_conv_forward(blk.mod, srcs, ctx, save))
+            ctxs.append(ctx if save else None)
+        state = dict(outs=outs, ctxs=ctxs, x_shape=(B, cx, H, W), cpad=cpad)
+        if not self.heads:
+            return outs[-1], state
+        hs = []
+        for hd in self.heads:
+            conv = hd.mod.conv
+            w = conv.weight.detach().reshape(conv.weight.shape[0], -1)
+            hs.append(ops.head_fwd(outs[hd.block], w.contiguous(), conv.bias.detach()))
+        fin = hs[-1]
+        nc = fin.shape[-1]
+        logits = ops.heads_combine(hs, B, fin.shape[1], fin.shape[2], nc)
+        state["hres"] = [h.shape[1] for h in hs]
+        return logits, state
+
+    # -------------------------------------------------------------- backward
+    def backward(self, state, grads, dlogits=None, dout_act=None, need_dx=False):
+        """dlogits: NCHW gradient of the combined head output, or dout_act: NHWC
+        gradient w.r.t. the last block's activation (encoder-only graphs).
+        grads: {param: destination tensor or None}.  Returns dx (NCHW) or None."""
+        outs, ctxs = state["outs"], state["ctxs"]
+        nb = len(self.blocks)
+        da = [None] * nb
+        if self.heads:
+            dhs = ops.heads_split_bwd(dlogits.contiguous(), state["hres"])
+            for hd, dh in zip(self.heads, dhs):
+                conv = hd.mod.conv
+                w = conv.weight.detach().reshape(conv.weight.shape[0], -1).contiguous()
+                a = outs[hd.block]
+                acc = da[hd.block] is not None
+                if not acc:
+                    da[hd.block] = torch.empty_like(a.y)
+                dw = grads.get(conv.weight)
+                dw_flat = dw.view(w.shape) if dw is not None else torch.empty_like(w)
+                db = grads.get(conv.bias)
+                ops.head_bwd(a, w, dh.contiguous(), dw_flat, db, da[hd.block], acc)
+        else:
+            da[nb - 1] = dout_act
+        dx0 = None
+        for bi in range(nb - 1, -1, -1):
+            blk, ctx, g = self.blocks[bi], ctxs[bi], da[bi]
+            if g is None:
+                raise RuntimeError(f"block {bi} output received no gradient")
+            if blk.kind == "inc":
+                if need_dx:
+                    B, cx, H, W = state["x_shape"]
+                    padc = ceil_to(state["cpad"], 64)
+                    dx0 = ops.empty(B, H, W, padc, like=g)
+                    double_conv_backward(blk.mod, ctx, g, [dx0], [0], grads, pad_out=padc)
+                else:
+                    double_conv_backward(blk.mod, ctx, g, [None], [0], grads)
+            elif blk.kind == "down":
+                src = blk.inputs[0]
+                dp = torch.empty_like(ctx.srcs[0].y)
+                double_conv_backward(blk.mod, ctx, g, [dp], [0], grads)
+                H, W = ctx.extra["in_hw"]
+                acc = da[src] is not None
+                if not acc:
+                    da[src] = torch.empty_like(outs[src].y)
+                ops.maxpool2_bwd(dp, ctx.extra["argmax"], H, W, da[src], acc)
+            else:
+                skip, low = blk.inputs
+                acc_s = da[skip] is not None
+                if not acc_s:
+                    da[skip] = torch.empty_like(outs[skip].y)
+                du = torch.empty_like(ctx.srcs[1].y)
+                double_conv_backward(blk.mod, ctx, g, [da[skip], du], [acc_s, 0], grads)
+                h, w = ctx.extra["low_hw"]
+                acc_l = da[low] is not None
+                if not acc_l:
+                    da[low] = torch.empty_like(outs[low].y)
+                ops.bilinear_nhwc_bwd(du, h, w, da[low], acc_l)
+            da[bi] = None
+            ctxs[bi] = None
+        if dx0 is not None:
+            return ops.nhwc_to_nchw(dx0, state["x_shape"][1])
+        return None

@@ -1,0 +1,107 @@
+"""Uncertainty-map fusion and uncertainty-weighted loss (drop-in for
+UncertaintyGuidedLoss, reference UG_unet.py:8-94).
+
+generate_uncertainty_map: resize input to the previous stage's resolution,
+run the previous model in eval mode, sigmoid, bilinear-resize the
+probabilities back, U = 1 - 2|P - 0.5| (the last three fused in one kernel).
+apply_uncertainty_weighted_loss: BCE-with-logits(pos_weight) per pixel,
+weighted by (1 + alpha*U), mean -- one fused reduction kernel forward and one
+elementwise kernel backward.  Criteria other than BCEWithLogitsLoss are
+evaluated by the criterion itself and only the weighting/mean runs in ugpg.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import ops
+
+
+def _pos_weight_tensor(loss_fn, like):
+    pw = getattr(loss_fn, "pos_weight", None)
+    if pw is None:
+        return None
+    if pw.numel() != 1:
+        raise NotImplementedError("ugpg: only a scalar pos_weight is supported")
+    if pw.device != like.device or pw.dtype != torch.float32:
+        pw = pw.to(device=like.device, dtype=torch.float32)
+    return pw.contiguous()
+
+
+class _UGBCEFn(torch.autograd.Function):
+    """(logits, target, umap, pos_weight) -> (final, base) with d final/d logits."""
+
+    @staticmethod
+    def forward(ctx, logits, target, umap, pos_weight, alpha, out):
+        logits, target = logits.contiguous(), target.contiguous().float()
+        out = ops.ug_loss_fwd(logits, target, umap, pos_weight, alpha, out)
+        ctx.save_for_backward(logits, target)
+        ctx.umap, ctx.pw, ctx.alpha = umap, pos_weight, alpha
+        final, base = out[0], out[1]
+        ctx.mark_non_differentiable(base)
+        return final, base
+
+    @staticmethod
+    def backward(ctx, gfinal, gbase):
+        logits, target = ctx.saved_tensors
+        g = gfinal.reshape(1).contiguous().float()
+        dx = ops.ug_loss_bwd(logits, target, ctx.umap, ctx.pw, ctx.alpha, g)
+        return dx, None, None, None, None, None
+
+
+class _WeightedMeanFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pixel_loss, umap, alpha):
+        pixel_loss = pixel_loss.contiguous().float()
+        out = ops.weighted_mean_fwd(pixel_loss, umap, alpha)
+        ctx.umap, ctx.alpha = umap, alpha
+        ctx.save_for_backward(pixel_loss)
+        ctx.mark_non_differentiable(out[1])
+        return out[0], out[1]
+
+    @staticmethod
+    def backward(ctx, gfinal, gbase):
+        (pl,) = ctx.saved_tensors
+        g = gfinal.reshape(1).contiguous().float()
+        return ops.weighted_mean_bwd(pl, ctx.umap, ctx.alpha, g), None, None
+
+
+def weighted_loss_tensors(loss_fn, output, target, uncertainty_map=None, alpha=1.0, out=None):
+    """Device-side (final_loss, base_loss) -- no host synchronisation.  `out`: optional
+    2-float device buffer receiving [final, base] (BCE path)."""
+    u = None
+    if uncertainty_map is not None:
+        u = uncertainty_map.detach().contiguous().float()
+        alpha_eff = float(alpha)
+    else:
+        alpha_eff = 0.0
+    if isinstance(loss_fn, nn.BCEWithLogitsLoss) and loss_fn.weight is None:
+        pw = _pos_weight_tensor(loss_fn, output)
+        return _UGBCEFn.apply(output, target, u, pw, alpha_eff, out)
+    pixel_loss = loss_fn(output, target)
+    return _WeightedMeanFn.apply(pixel_loss, u, alpha_eff)
+
+
+class UncertaintyGuidedLoss:
+    """Uncertainty map from the previous stage + uncertainty-weighted loss."""
+
+    def __init__(self, device="cuda"):
+        self.device = device
+
+    def generate_uncertainty_map(self, input_current, model_prev, prev_resolution,
+                                 current_resolution):
+        model_prev.eval()
+        with torch.no_grad():
+            x = input_current.detach().float().contiguous()
+            if x.shape[-2:] != (prev_resolution, prev_resolution):
+                x = ops.resize_nchw(x, prev_resolution, prev_resolution, ops.RESIZE_BILINEAR)
+            logits = model_prev(x)
+            u = ops.resize_nchw(logits.contiguous(), current_resolution, current_resolution,
+                                ops.RESIZE_UNCERTAINTY)
+        return u.detach()
+
+    def apply_uncertainty_weighted_loss(self, loss_fn, output_current, target_current,
+                                        uncertainty_map=None, alpha=1.0):
+        final, base = weighted_loss_tensors(loss_fn, output_current, target_current,
+                                            uncertainty_map, alpha)
+        return final, base.item()

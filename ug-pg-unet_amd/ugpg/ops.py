@@ -1,0 +1,404 @@
+"""Tensor-level wrappers over the libugpg C-ABI (one function per entry point).
+
+PyTorch is used only for device memory (the caching allocator) and the current
+HIP stream; every arithmetic op below runs in a hand-written gfx950 kernel.
+Activations are NHWC fp32 ``(B, H, W, C)`` tensors.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from ._C import ConvDesc, Src, WgradDesc, check, lib
+
+F32 = torch.float32
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError("ugpg: tensor is not on a ROCm/HIP device (no CPU fallback)")
+    if not t.is_contiguous():
+        raise RuntimeError("ugpg: tensor must be contiguous")
+    return t.data_ptr()
+
+
+def _f32(t):
+    if t.dtype != F32:
+        raise TypeError(f"ugpg: expected float32, got {t.dtype}")
+    return ptr(t)
+
+
+def empty(*shape, like=None, device=None, dtype=F32):
+    dev = device if device is not None else like.device
+    return torch.empty(*shape, dtype=dtype, device=dev)
+
+
+def workspace(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+
+
+class Act:
+    """A lazily-activated NHWC tensor: value = relu(scale*y + shift) when scale is set.
+
+    BatchNorm + ReLU of a DoubleConv (UG_unet_parts.py:11-12) is folded into the
+    consumer's load, so the normalised activation is never written to HBM.
+    """
+    __slots__ = ("y", "scale", "shift")
+
+    def __init__(self, y, scale=None, shift=None):
+        self.y, self.scale, self.shift = y, scale, shift
+
+    @property
+    def shape(self):
+        return tuple(self.y.shape)
+
+    @property
+    def C(self):
+        return self.y.shape[-1]
+
+    def src(self) -> Src:
+        return Src(ptr(self.y), ptr(self.scale), ptr(self.shift), self.C)
+
+    def materialize(self) -> torch.Tensor:
+        if self.scale is None:
+            return self.y
+        out = torch.empty_like(self.y)
+        check(lib.ugpg_bn_relu_apply(self.src(), self.y.numel() // self.C, ptr(out), stream()),
+              "bn_relu_apply")
+        return out
+
+
+NULL_SRC = Src(None, None, None, 0)
+
+
+# ------------------------------------------------------------------ conv
+def pack_conv3x3(w, cin_pad: int, mode: int) -> torch.Tensor:
+    cout, cin = w.shape[0], w.shape[1]
+    out = empty(cin_pad * 9 * cout, like=w)
+    check(lib.ugpg_pack_conv3x3(_f32(w.contiguous()), ptr(out), cout, cin, cin_pad, mode, stream()),
+          "pack_conv3x3")
+    return out
+
+
+def conv_ntiles(B, H, W, cin, cout) -> int:
+    return lib.ugpg_conv3x3_fwd_ntiles(B, H, W, cin, cout)
+
+
+class KernelTimer:
+    """Brackets selected launches with HIP events on the launching stream (used by
+    bench.py for the live per-kernel roofline).  Records (name, flops, ev0, ev1)."""
+
+    def __init__(self):
+        self.records = []
+
+    def wrap(self, name, flops, fn):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        self.records.append((name, flops, e0, e1))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for name, flops, e0, e1 in self.records:
+            d = out.setdefault(name, {"launches": 0, "flops": 0.0, "ms": 0.0})
+            d["launches"] += 1
+            d["flops"] += flops
+            d["ms"] += e0.elapsed_time(e1)
+        return out
+
+
+TIMER = None  # set to a KernelTimer to time conv launches
+
+
+def _timed(name, flops, fn):
+    if TIMER is None or flops is None:
+        fn()
+    else:
+        TIMER.wrap(name, flops, fn)
+
+
+def conv3x3_fwd(srcs, wpk, bias, cout, outs, split=None, accumulate=(0, 0), stats=None,
+                flops=None):
+    """srcs: 1-2 Act; outs: 1-2 NHWC tensors (channel split at `split`).
+    flops: algorithmic FLOPs of this call (for the optional KernelTimer)."""
+    B, H, W, _ = srcs[0].shape
+    d = ConvDesc()
+    d.B, d.H, d.W = B, H, W
+    d.src[0] = srcs[0].src()
+    d.src[1] = srcs[1].src() if len(srcs) > 1 else NULL_SRC
+    d.wpk, d.bias, d.Cout = ptr(wpk), ptr(bias), cout
+    d.out[0] = ptr(outs[0])
+    d.out[1] = ptr(outs[1]) if len(outs) > 1 else None
+    d.out_split = cout if split is None else split
+    d.accumulate[0], d.accumulate[1] = int(accumulate[0]), int(accumulate[1])
+    d.stats = ptr(stats)
+    _timed("conv3x3_fwd", flops,
+           lambda: check(lib.ugpg_conv3x3_fwd(C.byref(d), stream()), "conv3x3_fwd"))
+
+
+def conv3x3_wgrad(srcs, dy, dw, db, cin_real, accumulate=0, flops=None):
+    B, H, W, _ = srcs[0].shape
+    d = WgradDesc()
+    d.B, d.H, d.W = B, H, W
+    d.src[0] = srcs[0].src()
+    d.src[1] = srcs[1].src() if len(srcs) > 1 else NULL_SRC
+    d.dy, d.Cout = ptr(dy), dy.shape[-1]
+    d.dw, d.Cin_real, d.db, d.accumulate = ptr(dw), cin_real, ptr(db), int(accumulate)
+    nbytes = lib.ugpg_conv3x3_wgrad_workspace(C.byref(d))
+    if nbytes == 0:
+        check(-1, "conv3x3_wgrad_workspace")
+    ws = workspace(nbytes, dy.device)
+    _timed("conv3x3_wgrad", flops,
+           lambda: check(lib.ugpg_conv3x3_wgrad(C.byref(d), ptr(ws), ws.numel(), stream()),
+                         "conv3x3_wgrad"))
+
+
+# ------------------------------------------------------------------ BN
+def bn_finalize(stats, ntiles, gamma, beta, rm, rv, nbt, momentum, eps):
+    c = gamma.numel()
+    mean, invstd, scale, shift = (empty(c, like=gamma) for _ in range(4))
+    check(lib.ugpg_bn_finalize(ptr(stats), ntiles, c, _f32(gamma), _f32(beta), ptr(rm), ptr(rv),
+                               ptr(nbt), momentum, eps, ptr(mean), ptr(invstd), ptr(scale),
+                               ptr(shift), stream()), "bn_finalize")
+    return mean, invstd, scale, shift
+
+
+def bn_eval_params(gamma, beta, rm, rv, eps):
+    c = gamma.numel()
+    scale, shift = empty(c, like=gamma), empty(c, like=gamma)
+    check(lib.ugpg_bn_eval_params(_f32(gamma), _f32(beta), _f32(rm), _f32(rv), eps, c,
+                                  ptr(scale), ptr(shift), stream()), "bn_eval_params")
+    return scale, shift
+
+
+def bn_relu_bwd(da, y, mean, invstd, scale, shift, dy, dgamma, dbeta, accumulate=0):
+    c = y.shape[-1]
+    npix = y.numel() // c
+    ws = workspace(lib.ugpg_bn_relu_bwd_workspace(npix, c), y.device)
+    check(lib.ugpg_bn_relu_bwd(ptr(da), ptr(y), npix, c, ptr(mean), ptr(invstd), ptr(scale),
+                               ptr(shift), ptr(dy), ptr(dgamma), ptr(dbeta), int(accumulate),
+                               ptr(ws), ws.numel(), stream()), "bn_relu_bwd")
+
+
+# ------------------------------------------------------------------ pool / resize
+def maxpool2_fwd(a: Act):
+    B, H, W, c = a.shape
+    out = empty(B, H // 2, W // 2, c, like=a.y)
+    am = empty(B, H // 2, W // 2, c, like=a.y, dtype=torch.uint8)
+    check(lib.ugpg_maxpool2_fwd(a.src(), B, H, W, ptr(out), ptr(am), stream()), "maxpool2_fwd")
+    return out, am
+
+
+def maxpool2_bwd(dout, am, H, W, din, accumulate):
+    B, _, _, c = dout.shape
+    check(lib.ugpg_maxpool2_bwd(ptr(dout), ptr(am), B, H, W, c, ptr(din), int(accumulate),
+                                stream()), "maxpool2_bwd")
+
+
+def bilinear_nhwc_fwd(a: Act, Ho, Wo):
+    B, Hi, Wi, c = a.shape
+    out = empty(B, Ho, Wo, c, like=a.y)
+    check(lib.ugpg_bilinear_nhwc_fwd(a.src(), B, Hi, Wi, ptr(out), Ho, Wo, stream()),
+          "bilinear_nhwc_fwd")
+    return out
+
+
+def bilinear_nhwc_bwd(dout, Hi, Wi, din, accumulate):
+    B, Ho, Wo, c = dout.shape
+    check(lib.ugpg_bilinear_nhwc_bwd(ptr(dout), B, Ho, Wo, c, ptr(din), Hi, Wi, int(accumulate),
+                                     stream()), "bilinear_nhwc_bwd")
+
+
+RESIZE_BILINEAR, RESIZE_NEAREST, RESIZE_UNCERTAINTY = 0, 1, 2
+
+
+def resize_nchw(x, Ho, Wo, mode):
+    x = x.contiguous()
+    B, c, Hi, Wi = x.shape
+    out = empty(B, c, Ho, Wo, like=x)
+    check(lib.ugpg_resize_nchw(_f32(x), B, c, Hi, Wi, ptr(out), Ho, Wo, mode, stream()),
+          "resize_nchw")
+    return out
+
+
+def nchw_to_nhwc(x, cpad):
+    x = x.contiguous()
+    B, c, H, W = x.shape
+    out = empty(B, H, W, cpad, like=x)
+    check(lib.ugpg_nchw_to_nhwc(_f32(x), B, c, H, W, ptr(out), cpad, stream()), "nchw_to_nhwc")
+    return out
+
+
+def nhwc_to_nchw(y, c, out=None, accumulate=0):
+    B, H, W, cs = y.shape
+    if out is None:
+        out = empty(B, c, H, W, like=y)
+    check(lib.ugpg_nhwc_to_nchw(ptr(y), B, c, H, W, cs, ptr(out), int(accumulate), stream()),
+          "nhwc_to_nchw")
+    return out
+
+
+# ------------------------------------------------------------------ heads
+def head_fwd(a: Act, w, b):
+    B, H, W, c = a.shape
+    nc = w.shape[0]
+    h = empty(B, H, W, nc, like=a.y)
+    check(lib.ugpg_head_fwd(a.src(), B * H * W, _f32(w), _f32(b), nc, ptr(h), stream()),
+          "head_fwd")
+    return h
+
+
+def heads_combine(hs, B, H, W, nc):
+    n = len(hs)
+    arr = (C.c_void_p * n)(*[ptr(h) for h in hs])
+    res = (C.c_int * n)(*[h.shape[1] for h in hs])
+    out = empty(B, nc, H, W, like=hs[0])
+    check(lib.ugpg_heads_combine(arr, res, n, B, H, W, nc, ptr(out), stream()), "heads_combine")
+    return out
+
+
+def heads_split_bwd(dlogits, hres):
+    B, nc, H, W = dlogits.shape
+    dhs = [empty(B, r, r, nc, like=dlogits) for r in hres]
+    n = len(hres)
+    arr = (C.c_void_p * n)(*[ptr(d) for d in dhs])
+    res = (C.c_int * n)(*hres)
+    check(lib.ugpg_heads_split_bwd(ptr(dlogits), B, H, W, nc, arr, res, n, stream()),
+          "heads_split_bwd")
+    return dhs
+
+
+def head_bwd(a: Act, w, dh, dw, db, da, accumulate):
+    B, H, W, c = a.shape
+    nc = w.shape[0]
+    npix = B * H * W
+    ws = workspace(lib.ugpg_head_bwd_workspace(npix, c, nc), dh.device)
+    check(lib.ugpg_head_bwd(a.src(), npix, _f32(w), nc, ptr(dh), ptr(dw), ptr(db), ptr(da),
+                            int(accumulate), ptr(ws), ws.numel(), stream()), "head_bwd")
+
+
+# ------------------------------------------------------------------ loss / metrics
+def _umap_args(umap, logits):
+    if umap is None:
+        return None, 1
+    if umap.shape[0] != logits.shape[0] or umap.shape[2:] != logits.shape[2:]:
+        raise ValueError(f"uncertainty map shape {tuple(umap.shape)} vs output {tuple(logits.shape)}")
+    return umap.contiguous(), umap.shape[1]
+
+
+def ug_loss_fwd(logits, target, umap, pos_weight, alpha, out=None):
+    B, c = logits.shape[:2]
+    hw = logits.numel() // (B * c)
+    u, cu = _umap_args(umap, logits)
+    out = empty(2, like=logits) if out is None else out
+    ws = workspace(lib.ugpg_ug_loss_workspace(logits.numel()), logits.device)
+    check(lib.ugpg_ug_loss_fwd(_f32(logits), _f32(target), ptr(u), B, c, hw, cu, ptr(pos_weight),
+                               float(alpha), ptr(out), ptr(ws), ws.numel(), stream()), "ug_loss_fwd")
+    return out
+
+
+def ug_loss_bwd(logits, target, umap, pos_weight, alpha, gout):
+    B, c = logits.shape[:2]
+    hw = logits.numel() // (B * c)
+    u, cu = _umap_args(umap, logits)
+    dx = torch.empty_like(logits)
+    check(lib.ugpg_ug_loss_bwd(ptr(logits), ptr(target), ptr(u), B, c, hw, cu, ptr(pos_weight),
+                               float(alpha), ptr(gout), ptr(dx), stream()), "ug_loss_bwd")
+    return dx
+
+
+def weighted_mean_fwd(pixel_loss, umap, alpha):
+    B, c = pixel_loss.shape[:2]
+    hw = pixel_loss.numel() // (B * c)
+    u, cu = _umap_args(umap, pixel_loss)
+    out = empty(2, like=pixel_loss)
+    ws = workspace(lib.ugpg_ug_loss_workspace(pixel_loss.numel()), pixel_loss.device)
+    check(lib.ugpg_weighted_mean_fwd(_f32(pixel_loss), ptr(u), B, c, hw, cu, float(alpha), ptr(out),
+                                     ptr(ws), ws.numel(), stream()), "weighted_mean_fwd")
+    return out
+
+
+def weighted_mean_bwd(pixel_loss, umap, alpha, gout):
+    B, c = pixel_loss.shape[:2]
+    hw = pixel_loss.numel() // (B * c)
+    u, cu = _umap_args(umap, pixel_loss)
+    d = torch.empty_like(pixel_loss)
+    check(lib.ugpg_weighted_mean_bwd(ptr(u), B, c, hw, cu, float(alpha), ptr(gout), ptr(d),
+                                     stream()), "weighted_mean_bwd")
+    return d
+
+
+def seg_metrics(logits, target, out=None):
+    """-> device tensor [dice, acc, wrong_count] (single-channel segmentation)."""
+    B = logits.shape[0]
+    hw = logits.numel() // B
+    out = empty(3, like=logits) if out is None else out
+    ws = workspace(lib.ugpg_seg_metrics_workspace(B), logits.device)
+    check(lib.ugpg_seg_metrics(_f32(logits.contiguous()), _f32(target.contiguous()), B, hw,
+                               ptr(out), ptr(ws), ws.numel(), stream()), "seg_metrics")
+    return out
+
+
+def mean_std(x, out=None):
+    x = x.contiguous()
+    out = empty(2, like=x) if out is None else out
+    ws = workspace(lib.ugpg_mean_std_workspace(x.numel()), x.device)
+    check(lib.ugpg_mean_std(_f32(x), x.numel(), ptr(out), ptr(ws), ws.numel(), stream()),
+          "mean_std")
+    return out
+
+
+def rmsprop_step(p, g, v, lr, alpha, eps, weight_decay, grad_scale=1.0):
+    check(lib.ugpg_rmsprop_step(_f32(p), _f32(g), _f32(v), p.numel(), float(lr), float(alpha),
+                                float(eps), float(weight_decay), float(grad_scale), stream()),
+          "rmsprop_step")
+
+
+# ------------------------------------------------------------------ Herlev head
+def avgpool_fwd(a: Act):
+    B, H, W, c = a.shape
+    out = empty(B, c, like=a.y)
+    check(lib.ugpg_avgpool_fwd(a.src(), B, H * W, ptr(out), stream()), "avgpool_fwd")
+    return out
+
+
+def avgpool_bwd(dout, H, W, da, accumulate=0):
+    B, c = dout.shape
+    check(lib.ugpg_avgpool_bwd(ptr(dout), B, H * W, c, ptr(da), int(accumulate), stream()),
+          "avgpool_bwd")
+
+
+def linear_fwd(x, w, b, relu):
+    M, K = x.shape
+    N = w.shape[0]
+    y = empty(M, N, like=x)
+    check(lib.ugpg_linear_fwd(_f32(x.contiguous()), _f32(w), ptr(b), M, N, K, int(relu), ptr(y),
+                              stream()), "linear_fwd")
+    return y
+
+
+def linear_bwd(x, w, dy, dx, dw, db):
+    M, K = x.shape
+    N = w.shape[0]
+    check(lib.ugpg_linear_bwd(ptr(x), ptr(w), ptr(dy), M, N, K, ptr(dx), ptr(dw), ptr(db),
+                              stream()), "linear_bwd")
+
+
+def relu_bwd_(y, dy):
+    check(lib.ugpg_relu_bwd(ptr(y), ptr(dy), y.numel(), stream()), "relu_bwd")
+
+
+def mul(x, m):
+    y = torch.empty_like(x)
+    check(lib.ugpg_mul(ptr(x), ptr(m), ptr(y), x.numel(), stream()), "mul")
+    return y

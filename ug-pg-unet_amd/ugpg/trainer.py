@@ -1,0 +1,286 @@
+"""UncertaintyGuidedProgressiveTrainer on libugpg (drop-in for
+uncertainty_guided_trainer.py:25-525).
+
+Public attributes and methods are the reference's, because subclasses such as
+AugMoNuSegTrainer (MoNuSegImprove/train_aug_monuseg.py:36-121) override
+``__init__`` and replace ``base_criterion``.  The per-batch hot path
+(``train_epoch``: resize, forward, uncertainty map, weighted loss, backward,
+RMSprop, Dice/accuracy) runs entirely in ugpg kernels and synchronises with the
+host once per batch instead of the reference's six ``.item()``/``.cpu()`` calls.
+"""
+from __future__ import annotations
+
+import json
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import ops
+from .dist import allreduce_gradients, world
+from .loss import UncertaintyGuidedLoss, weighted_loss_tensors
+from .optim import RMSprop
+from .unet import PGUNet1, PGUNet2, PGUNet3, PGUNet4, transfer_state
+
+try:  # plotting is optional, as in the reference
+    import matplotlib
+    matplotlib.use("Agg")
+    import matplotlib.pyplot as plt
+    MATPLOTLIB_AVAILABLE = True
+except Exception:  # pragma: no cover
+    MATPLOTLIB_AVAILABLE = False
+
+
+class UncertaintyGuidedProgressiveTrainer:
+    def __init__(self, in_channels=3, num_classes=1, device="cuda", uncertainty_alpha=1.0):
+        self.device = device
+        self.in_channels = in_channels
+        self.num_classes = num_classes
+        self.uncertainty_alpha = uncertainty_alpha
+        self.stage_configs = {
+            1: {"resolution": 32, "epochs_per_stage": 40, "lr": 3e-4},
+            2: {"resolution": 64, "epochs_per_stage": 40, "lr": 1e-4},
+            3: {"resolution": 128, "epochs_per_stage": 40, "lr": 1e-4},
+            4: {"resolution": 256, "epochs_per_stage": 40, "lr": 1e-4},
+        }
+        self.models = {s: cls(in_channels, num_classes).to(device)
+                       for s, cls in ((1, PGUNet1), (2, PGUNet2), (3, PGUNet3), (4, PGUNet4))}
+        self.current_stage = 1
+        self.current_model = self.models[1]
+        self.uncertainty_loss = UncertaintyGuidedLoss(device)
+        self.base_criterion = nn.BCEWithLogitsLoss(
+            pos_weight=torch.tensor([5.0]).to(device), reduction="none")
+        self.optimizer = None
+        self.setup_optimizer(1)
+        self.history = {k: [] for k in ("train_loss", "val_loss", "train_dice", "val_dice",
+                                        "uncertainty_weights_mean", "uncertainty_weights_std",
+                                        "base_loss", "stage_transitions")}
+
+    # ------------------------------------------------------------ components
+    def setup_optimizer(self, stage):
+        self.optimizer = RMSprop(self.current_model.parameters(),
+                                 lr=self.stage_configs[stage]["lr"], weight_decay=1e-4)
+
+    def dice_coefficient(self, pred, target, smooth=1):
+        """Mean per-sample Dice (uncertainty_guided_trainer.py:90-107).  Host-side helper
+        kept for API parity; the training loop uses the fused seg_metrics kernel."""
+        p = pred.to(target.device).contiguous().float().view(pred.size(0), -1)
+        t = target.to(p.device).contiguous().float().view(target.size(0), -1)
+        inter = (p * t).sum(dim=1)
+        return ((2.0 * inter + smooth) / (p.sum(dim=1) + t.sum(dim=1) + smooth)).mean()
+
+    def get_predictions(self, output_batch):
+        return (torch.sigmoid(output_batch) > 0.5).float().squeeze(1)
+
+    def calculate_accuracy(self, pred, target):
+        pred = pred.to(target.device)
+        assert pred.size() == target.size()
+        bs, h, w = pred.size()
+        incorrect = pred.ne(target).cpu().sum().numpy()
+        return 1 - incorrect / (bs * h * w)
+
+    def transfer_weights(self, prev_stage, new_stage):
+        print(f"Transferring weights from stage {prev_stage} to stage {new_stage}")
+        prev_dict = self.models[prev_stage].state_dict()
+        new_dict = self.models[new_stage].state_dict()
+        new_state, copied = transfer_state(prev_dict, new_dict)
+        print(f"transfer_weights(stage={new_stage}): copied {len(copied)} keys "
+              f"(examples: {copied[:5]})")
+        self.models[new_stage].load_state_dict(new_state)
+        print(f"Weight transfer completed for stage {new_stage}")
+
+    # ------------------------------------------------------------ hot path
+    def _forward_device(self, data, target, stage, mbuf):
+        """Forward + uncertainty map + weighted loss; results stay on the device.
+        mbuf: 8-float device buffer [final, base, dice, acc, wrong, u_mean, u_std, 0]."""
+        output = self.current_model(data)
+        umap = None
+        if stage > 1:
+            umap = self.uncertainty_loss.generate_uncertainty_map(
+                data, self.models[stage - 1], self.stage_configs[stage - 1]["resolution"],
+                self.stage_configs[stage]["resolution"])
+        final, base = weighted_loss_tensors(self.base_criterion, output, target, umap,
+                                            self.uncertainty_alpha,
+                                            out=mbuf[0:2] if mbuf is not None else None)
+        return output, umap, final, base
+
+    def _resize_batch(self, data, target, res):
+        data = data.to(self.device, non_blocking=True).float()
+        target = target.to(self.device, non_blocking=True).float()
+        if data.shape[-2:] != (res, res):
+            data = ops.resize_nchw(data, res, res, ops.RESIZE_BILINEAR)
+        if target.shape[-2:] != (res, res):
+            target = ops.resize_nchw(target, res, res, ops.RESIZE_NEAREST)
+        return data.contiguous(), target.contiguous()
+
+    def _metrics_device(self, output, target, umap, mbuf):
+        if output.shape[1] != 1:
+            # the reference's calculate_accuracy unpacks a 3-D prediction
+            raise ValueError("too many values to unpack (expected 3)")
+        ops.seg_metrics(output, target, out=mbuf[2:5])
+        if umap is not None:
+            ops.mean_std(umap, out=mbuf[5:7])
+
+    def train_step(self, data, target, stage):
+        """One uncertainty-guided training step on device tensors already at the
+        stage resolution.  Returns the 8-float device metrics buffer (unsynced)."""
+        mbuf = torch.zeros(8, dtype=torch.float32, device=data.device)
+        self.optimizer.zero_grad()
+        output, umap, final, _ = self._forward_device(data, target, stage, mbuf)
+        final.backward()
+        self.optimizer.grad_scale = allreduce_gradients(
+            [p for g in self.optimizer.param_groups for p in g["params"]])
+        self.optimizer.step()
+        self._metrics_device(output, target, umap, mbuf)
+        return mbuf
+
+    def uncertainty_guided_forward_pass(self, data, target, stage):
+        mbuf = torch.zeros(8, dtype=torch.float32, device=data.device)
+        output, umap, final, _ = self._forward_device(data, target, stage, mbuf)
+        if umap is not None:
+            ops.mean_std(umap, out=mbuf[5:7])
+        v = mbuf.tolist()
+        metrics = {"final_loss": v[0], "base_loss": v[1], "output": output,
+                   "uncertainty_weight_mean": v[5] if umap is not None else 0.0,
+                   "uncertainty_weight_std": v[6] if umap is not None else 0.0}
+        return final, metrics
+
+    def _epoch(self, dataloader, stage, train):
+        model = self.current_model
+        model.train(train)
+        if stage > 1:
+            self.models[stage - 1].eval()
+        tot = np.zeros(6)
+        res = self.stage_configs[stage]["resolution"]
+        nb = 0
+        for batch_idx, (data, target) in enumerate(dataloader):
+            data, target = self._resize_batch(data, target, res)
+            if train:
+                mbuf = self.train_step(data, target, stage)
+            else:
+                mbuf = torch.zeros(8, dtype=torch.float32, device=data.device)
+                with torch.no_grad():
+                    output, umap, _, _ = self._forward_device(data, target, stage, mbuf)
+                    self._metrics_device(output, target, umap, mbuf)
+            v = mbuf.tolist()  # the one host synchronisation of the batch
+            npx = data.shape[0] * res * res
+            acc = 1 - v[4] / npx
+            um, us = (v[5], v[6]) if stage > 1 else (0.0, 0.0)
+            tot += (v[0], v[1], v[2], acc, um, us)
+            nb += 1
+            if train and batch_idx % 10 == 0:
+                extra = f", Unc_mean: {um:.4f}" if stage > 1 else ""
+                print(f"Stage {stage}, Batch {batch_idx}, Loss: {v[0]:.4f}, Base_Loss: {v[1]:.4f}, "
+                      f"Dice: {v[2]:.4f}, Acc: {acc:.4f}{extra}")
+        num = len(dataloader)
+        avg = tot / num
+        kind = "training" if train else "validation"
+        print(f"Stage {stage} {kind} epoch completed. Batches processed: {num}")
+        return tuple(float(a) for a in avg)
+
+    def train_epoch(self, dataloader, stage):
+        return self._epoch(dataloader, stage, True)
+
+    def validate_epoch(self, dataloader, stage):
+        return self._epoch(dataloader, stage, False)
+
+    # ------------------------------------------------------------ driver
+    def train_progressive(self, train_loader, val_loader, max_stages=4,
+                          save_dir="./uncertainty_guided_weights"):
+        save_path = Path(save_dir)
+        save_path.mkdir(exist_ok=True)
+        rank, _ = world()
+        print("Starting Uncertainty-Guided Progressive Growing U-Net Training")
+        for stage in range(1, max_stages + 1):
+            print(f"\nStarting Stage {stage}")
+            if stage > 1:
+                self.transfer_weights(stage - 1, stage)
+            self.current_stage = stage
+            self.current_model = self.models[stage]
+            self.setup_optimizer(stage)
+            self.history["stage_transitions"].append(len(self.history["train_loss"]))
+            best = 0
+            epochs = self.stage_configs[stage]["epochs_per_stage"]
+            for epoch in range(epochs):
+                t0 = time.time()
+                tr = self.train_epoch(train_loader, stage)
+                va = self.validate_epoch(val_loader, stage)
+                self.history["train_loss"].append(tr[0])
+                self.history["val_loss"].append(va[0])
+                self.history["train_dice"].append(tr[2])
+                self.history["val_dice"].append(va[2])
+                self.history["uncertainty_weights_mean"].append(va[4])
+                self.history["uncertainty_weights_std"].append(va[5])
+                self.history["base_loss"].append(va[1])
+                print(f"Stage {stage}, Epoch {epoch + 1}/{epochs} ({time.time() - t0:.2f}s)")
+                print(f"Train - Loss: {tr[0]:.4f}, Base: {tr[1]:.4f}, Dice: {tr[2]:.4f}, Acc: {tr[3]:.4f}")
+                print(f"Val   - Loss: {va[0]:.4f}, Base: {va[1]:.4f}, Dice: {va[2]:.4f}, Acc: {va[3]:.4f}")
+                if va[2] > best:
+                    best = va[2]
+                    if rank == 0:
+                        torch.save({"stage": stage, "epoch": epoch,
+                                    "model_state_dict": self.current_model.state_dict(),
+                                    "optimizer_state_dict": self.optimizer.state_dict(),
+                                    "val_dice": va[2], "train_dice": tr[2],
+                                    "uncertainty_alpha": self.uncertainty_alpha,
+                                    "history": self.history},
+                                   save_path / f"ug_pgunet_stage{stage}_best.pth")
+        print("Uncertainty-guided progressive training completed!")
+        if rank == 0:
+            self.save_training_plots(save_path)
+
+    def save_training_plots(self, save_path):
+        if not MATPLOTLIB_AVAILABLE:
+            print("Warning: matplotlib not available. Skipping plot generation.")
+            return
+        h = self.history
+        ep = range(len(h["train_loss"]))
+        fig, axs = plt.subplots(2, 2, figsize=(16, 12))
+        axs[0, 0].plot(ep, h["train_loss"], label="Train Loss (Weighted)")
+        axs[0, 0].plot(ep, h["val_loss"], label="Val Loss (Weighted)")
+        axs[0, 0].plot(ep, h["base_loss"], "--", label="Base Loss (Unweighted)")
+        axs[0, 1].plot(ep, h["train_dice"], label="Train Dice")
+        axs[0, 1].plot(ep, h["val_dice"], label="Val Dice")
+        m, s = np.array(h["uncertainty_weights_mean"]), np.array(h["uncertainty_weights_std"])
+        axs[1, 0].plot(ep, m, label="Mean Uncertainty Weight")
+        axs[1, 0].fill_between(ep, m - s, m + s, alpha=0.3, label="±1 Std")
+        axs[1, 1].plot(ep, np.array(h["val_loss"]) - np.array(h["base_loss"]),
+                       label="Loss Difference (Weighted - Base)")
+        for ax in axs.flat:
+            for t in h["stage_transitions"]:
+                ax.axvline(x=t, color="red", linestyle="--", alpha=0.5)
+            ax.legend()
+        plt.tight_layout()
+        plt.savefig(Path(save_path) / "uncertainty_guided_training_plots.png", dpi=100)
+        plt.close(fig)
+
+    def load_stage_weights(self, stage, checkpoint_path):
+        ck = torch.load(checkpoint_path, map_location=self.device, weights_only=True)
+        self.models[stage].load_state_dict(ck["model_state_dict"] if "model_state_dict" in ck else ck)
+        print(f"Loaded weights for stage {stage} from {checkpoint_path}")
+
+    def save_uncertainty_analysis(self, data_loader, stage, save_path):
+        if stage == 1:
+            print("No uncertainty analysis for stage 1 (base stage)")
+            return
+        self.current_model.eval()
+        self.models[stage - 1].eval()
+        res = self.stage_configs[stage]["resolution"]
+        prev_res = self.stage_configs[stage - 1]["resolution"]
+        stats = []
+        with torch.no_grad():
+            for batch_idx, (data, target) in enumerate(data_loader):
+                if batch_idx >= 10:
+                    break
+                data, _ = self._resize_batch(data, target, res)
+                u = self.uncertainty_loss.generate_uncertainty_map(
+                    data, self.models[stage - 1], prev_res, res)
+                ms = ops.mean_std(u).tolist()
+                stats.append({"batch_idx": batch_idx, "uncertainty_mean": ms[0],
+                              "uncertainty_std": ms[1], "uncertainty_min": float(u.min()),
+                              "uncertainty_max": float(u.max())})
+        with open(Path(save_path) / f"uncertainty_stats_stage{stage}.json", "w") as f:
+            json.dump(stats, f, indent=2)
+        print(f"Uncertainty analysis saved for stage {stage}")
