@@ -341,9 +341,26 @@ def g7(RU):
     save_npz("g7_herlev.npz", **fx)
 
 
+def g0(RU):
+    """state_dict keys/shapes/dtypes of every reference model (checkpoint format)."""
+    out = {}
+    for stage in (1, 2, 3, 4):
+        for nc in (1, 2):
+            m = getattr(RU, f"PGUNet{stage}")(3, nc)
+            out[f"PGUNet{stage}_nc{nc}"] = [[k, list(v.shape), str(v.dtype)]
+                                           for k, v in m.state_dict().items()]
+    pu = RU.ProgressiveUNet(3, 1)
+    out["ProgressiveUNet"] = [[k, list(v.shape), str(v.dtype)] for k, v in pu.state_dict().items()]
+    out["param_counts"] = {f"PGUNet{s}": sum(p.numel() for p in getattr(RU, f"PGUNet{s}")(3, 1).parameters())
+                           for s in (1, 2, 3, 4)}
+    (OUT / "g0_state_spec.json").write_text(json.dumps(out))
+    print("wrote g0_state_spec.json", out["param_counts"])
+
+
 def main():
     torch.set_num_threads(8)
     RU = _ref()
+    g0(RU)
     g1(RU, 1)
     g1(RU, 2)
     g2(RU)

@@ -1,0 +1,90 @@
+"""Data-parallel path on CPU with the gloo backend, world_size 2.
+
+Each rank computes the oracle's local-BatchNorm gradients on its contiguous
+shard, places them in ugpg's flat gradient layout and calls
+ugpg.dist.allreduce_gradients (the exact function the trainer and bench.py use
+with RCCL).  The result must equal the mean of the per-shard gradients computed
+in one process, on every rank, for both the flat (single all-reduce) and the
+per-tensor fallback layout."""
+import os
+import socket
+import tempfile
+
+import torch
+import torch.multiprocessing as mp
+import torch.nn as nn
+
+WORLD = 2
+B_PER = 2
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _shards():
+    from oracle import detgen as G
+    x = G.randn(1, (B_PER * WORLD, 3, 32, 32), "x")
+    t = G.bernoulli(2, (B_PER * WORLD, 1, 32, 32), 0.5, "t")
+    return x, t
+
+
+def _grads_for(rank):
+    from tests._parity import det_state, oracle_run, param_keys
+    from ugpg.dist import shard
+    torch.set_num_threads(2)
+    state = det_state(1, 3, 1)
+    x, t = _shards()
+    _, _, _, g, _ = oracle_run(1, state, shard(x, rank, WORLD), shard(t, rank, WORLD))
+    return [g[k] for k in param_keys(state)]
+
+
+def _worker(rank, port, outdir, flat):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "ug-pg-unet_amd")]
+    import torch.distributed as dist
+    from ugpg.dist import allreduce_gradients, world
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    assert world() == (rank, WORLD)
+    grads = _grads_for(rank)
+    params = [nn.Parameter(torch.zeros_like(g)) for g in grads]
+    if flat:
+        buf = torch.cat([g.reshape(-1) for g in grads])
+        off = 0
+        for p, g in zip(params, grads):
+            p.grad = buf[off:off + g.numel()].view_as(g)
+            off += g.numel()
+    else:
+        for p, g in zip(params, grads):
+            p.grad = g.clone()
+    scale = allreduce_gradients(params, bucket_bytes=1 << 20)
+    out = [p.grad * scale for p in params]
+    torch.save(out, os.path.join(outdir, f"rank{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def _run(flat):
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(_free_port(), d, flat), nprocs=WORLD, join=True)
+        res = [torch.load(os.path.join(d, f"rank{r}.pt"), weights_only=True) for r in range(WORLD)]
+    per = [_grads_for(r) for r in range(WORLD)]
+    mean = [(a + b) / WORLD for a, b in zip(*per)]
+    for r in range(WORLD):
+        for got, want in zip(res[r], mean):
+            assert torch.allclose(got, want, rtol=1e-6, atol=1e-9)
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b), "replicas diverged"
+
+
+def test_dp_allreduce_flat_buffer():
+    _run(flat=True)
+
+
+def test_dp_allreduce_per_tensor_fallback():
+    _run(flat=False)

@@ -1,0 +1,137 @@
+"""Host-side logic and API surface of ugpg (CPU only, no kernel launches):
+checkpoint format, progressive weight transfer, ProgressiveUNet / trainer /
+optimizer API, data-parallel sharding helpers."""
+import json
+
+import pytest
+import torch
+import torch.nn as nn
+
+import ugpg
+from oracle import detgen as G
+from oracle import ref_cpu as O
+
+GOLD = "tests/golden/"
+
+
+@pytest.fixture(scope="module")
+def spec():
+    return json.load(open(GOLD + "g0_state_spec.json"))
+
+
+@pytest.mark.parametrize("stage", [1, 2, 3, 4])
+@pytest.mark.parametrize("nc", [1, 2])
+def test_state_dict_matches_reference_checkpoint_format(spec, stage, nc):
+    m = getattr(ugpg, f"PGUNet{stage}")(3, nc)
+    got = [[k, list(v.shape), str(v.dtype)] for k, v in m.state_dict().items()]
+    assert got == spec[f"PGUNet{stage}_nc{nc}"]
+    assert sum(p.numel() for p in m.parameters()) == spec["param_counts"][f"PGUNet{stage}"] or nc != 1
+
+
+def test_progressive_unet_format_and_api(spec):
+    pu = ugpg.ProgressiveUNet(3, 1)
+    got = [[k, list(v.shape), str(v.dtype)] for k, v in pu.state_dict().items()]
+    assert got == spec["ProgressiveUNet"]
+    assert pu.current_stage == 1 and pu.get_current_resolution() == 32
+    pu.set_stage(3)
+    assert pu.get_current_resolution() == 128
+    with pytest.raises(ValueError):
+        pu.set_stage(5)
+    assert pu.stages[4] is pu.stage4
+    # README spelling (README.md:46-52) is accepted as an alias
+    alias = ugpg.ProgressiveUNet(in_channels=3, out_channels=2, stage=1)
+    assert alias.num_classes == 2 and alias.current_stage == 1
+
+
+def test_reference_checkpoint_loads():
+    """A state_dict produced by the reference module layout loads strictly."""
+    for stage in (1, 4):
+        state = G.make_state(O.state_spec(stage, 3, 1), 5)
+        m = getattr(ugpg, f"PGUNet{stage}")(3, 1)
+        m.load_state_dict(state, strict=True)
+        for k, v in m.state_dict().items():
+            assert torch.equal(v, state[k])
+
+
+def test_transfer_state_matches_reference_golden():
+    gold = json.load(open(GOLD + "g5_transfer.json"))
+    states = {s: G.make_state(O.state_spec(s, 3, 1), 50 + s) for s in range(1, 5)}
+    for s in (2, 3, 4):
+        new, copied = ugpg.transfer_state(states[s - 1], states[s])
+        g = gold[f"{s - 1}->{s}"]
+        assert copied == g["copied"]
+        for k in copied:
+            assert abs(float(new[k].double().sum()) - g["checksums"][k]) <= 1e-9 * max(1, abs(g["checksums"][k]))
+        assert list(new.keys()) == list(states[s].keys())
+
+
+def test_progressive_transfer_weights_prints_and_returns(capsys):
+    pu = ugpg.ProgressiveUNet(3, 1)
+    new = pu.transfer_weights(pu.stage1.state_dict(), pu.stage2.state_dict(), 2)
+    assert "copied 42 keys" in capsys.readouterr().out
+    pu.stage2.load_state_dict(new)
+
+
+def test_trainer_public_surface_on_cpu():
+    tr = ugpg.UncertaintyGuidedProgressiveTrainer(3, 1, device="cpu", uncertainty_alpha=0.5)
+    assert set(tr.stage_configs) == {1, 2, 3, 4}
+    assert [tr.stage_configs[s]["resolution"] for s in (1, 2, 3, 4)] == [32, 64, 128, 256]
+    assert [tr.stage_configs[s]["lr"] for s in (1, 2, 3, 4)] == [3e-4, 1e-4, 1e-4, 1e-4]
+    assert set(tr.models) == {1, 2, 3, 4} and tr.current_model is tr.models[1]
+    assert isinstance(tr.base_criterion, nn.BCEWithLogitsLoss)
+    assert tr.base_criterion.pos_weight.item() == 5.0 and tr.base_criterion.reduction == "none"
+    assert isinstance(tr.optimizer, ugpg.RMSprop)
+    assert tr.optimizer.param_groups[0]["weight_decay"] == 1e-4
+    assert set(tr.history) == {"train_loss", "val_loss", "train_dice", "val_dice",
+                               "uncertainty_weights_mean", "uncertainty_weights_std",
+                               "base_loss", "stage_transitions"}
+    for name in ("setup_optimizer", "dice_coefficient", "get_predictions", "calculate_accuracy",
+                 "transfer_weights", "uncertainty_guided_forward_pass", "train_epoch",
+                 "validate_epoch", "train_progressive", "save_training_plots",
+                 "load_stage_weights", "save_uncertainty_analysis"):
+        assert callable(getattr(tr, name))
+    # host-side metric helpers keep the reference semantics
+    pred = torch.tensor([[[1.0, 0.0], [1.0, 1.0]]])
+    tgt = torch.tensor([[[1.0, 0.0], [0.0, 1.0]]])
+    assert abs(tr.dice_coefficient(pred, tgt).item() - (2 * 2 + 1) / (3 + 2 + 1)) < 1e-7
+    assert tr.calculate_accuracy(pred, tgt.long()) == 0.75
+    # subclass contract (train_aug_monuseg.py:42-121): replace criterion and epochs
+    tr.base_criterion = nn.BCEWithLogitsLoss(pos_weight=torch.tensor([3.2]), reduction="none")
+    for s in tr.stage_configs:
+        tr.stage_configs[s]["epochs_per_stage"] = 2
+    tr.transfer_weights(1, 2)
+
+
+def test_v1_helper_and_aliases():
+    from ugpg import UG_unet, UG_unet_parts, uncertainty_guided_trainer
+    h = UG_unet.UncertaintyGuidedProgressiveTrainer(device="cpu")
+    assert h.stage_resolutions == {1: 32, 2: 64, 3: 128, 4: 256}
+    fn = h.create_uncertainty_weighted_loss_fn(nn.BCEWithLogitsLoss(pos_weight=torch.tensor([2.0])))
+    assert fn.reduction == "none" and fn.pos_weight.item() == 2.0
+    assert UG_unet_parts.Up is ugpg.Up and uncertainty_guided_trainer.UncertaintyGuidedProgressiveTrainer \
+        is ugpg.UncertaintyGuidedProgressiveTrainer
+
+
+def test_rmsprop_rejects_unsupported_configs():
+    p = [nn.Parameter(torch.zeros(3))]
+    with pytest.raises(NotImplementedError):
+        ugpg.RMSprop(p, lr=1e-3, momentum=0.9)
+    with pytest.raises(NotImplementedError):
+        ugpg.RMSprop(p, lr=1e-3, centered=True)
+    opt = ugpg.RMSprop(p, lr=1e-3, weight_decay=1e-4)
+    assert opt.state_dict()["param_groups"][0]["alpha"] == 0.99
+
+
+def test_models_refuse_cpu_execution():
+    m = ugpg.PGUNet1(3, 1)
+    with pytest.raises(RuntimeError, match="ROCm"):
+        m(torch.zeros(1, 3, 32, 32))
+
+
+def test_shard_helper():
+    from ugpg.dist import shard
+    x = torch.arange(16).view(16, 1)
+    parts = [shard(x, r, 4) for r in range(4)]
+    assert torch.equal(torch.cat(parts), x)
+    with pytest.raises(ValueError):
+        shard(x, 0, 3)
