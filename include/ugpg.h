@@ -115,12 +115,15 @@ int ugpg_bn_eval_params(const float* gamma, const float* beta, const float* runn
 /* Backward of relu(bn(y)) given da = dL/d(relu output) (K6+K7):
  *   g = da * [scale*y+shift > 0];  dgamma = sum g*xhat;  dbeta = sum g
  *   dy = scale * (g - mean(g) - xhat*mean(g*xhat))
- * dy may alias da.  dgamma/dbeta written (or accumulated). */
+ * dy may alias da.  dgamma/dbeta written (or accumulated).  dconv_bias (nullable)
+ * receives sum_p dy = -scale*mean(g*xhat)*sum(xhat), evaluated in fp64: the bias
+ * gradient of the conv that produced y (the reference's aten value is the same
+ * sum in fp32; both are ~0 because train-mode BN cancels a preceding bias). */
 size_t ugpg_bn_relu_bwd_workspace(int64_t npix, int C);
 int ugpg_bn_relu_bwd(const float* da, const float* y, int64_t npix, int C, const float* mean,
                      const float* invstd, const float* scale, const float* shift,
-                     float* dy, float* dgamma, float* dbeta, int accumulate_params,
-                     void* ws, size_t ws_bytes, void* stream);
+                     float* dy, float* dgamma, float* dbeta, float* dconv_bias,
+                     int accumulate_params, void* ws, size_t ws_bytes, void* stream);
 /* Materialise relu(scale*y+shift) (used only for the standalone block API). */
 int ugpg_bn_relu_apply(ugpg_src_t src, int64_t npix, float* out, void* stream);
 

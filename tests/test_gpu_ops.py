@@ -165,8 +165,11 @@ def test_bn_relu_bwd(dev, C, npix):
     f = lambda t: t.float().to(dev)
     dy = torch.empty(npix, C, device=dev)
     dg, dbt = torch.empty(C, device=dev), torch.empty(C, device=dev)
-    ops.bn_relu_bwd(f(da), f(y), f(mean), f(invstd), f(scale), f(shift), dy, dg, dbt)
+    dcb = torch.empty(C, device=dev)
+    ops.bn_relu_bwd(f(da), f(y), f(mean), f(invstd), f(scale), f(shift), dy, dg, dbt, dcb)
     close(dy.cpu(), yd.grad, 1e-4, "bn bwd dx")
+    # bias grad of the producing conv = sum_p dy (true value ~0)
+    assert (dcb.cpu().double() - yd.grad.sum(0)).abs().max() <= 1e-6 * yd.grad.abs().sum(0).max()
     close(dg.cpu(), gd.grad, 1e-4, "dgamma")
     close(dbt.cpu(), bd.grad, 1e-4, "dbeta")
 

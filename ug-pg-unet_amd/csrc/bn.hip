@@ -87,8 +87,8 @@ __global__ void __launch_bounds__(256)
     const int c4n = C / 4, slots = 256 / c4n;
     const int tid = threadIdx.x, q = tid % c4n, slot = tid / c4n;
     const int c = q * 4;
-    __shared__ f32x4 rs[256], rq[256];
-    f32x4 sg = {0, 0, 0, 0}, sgx = {0, 0, 0, 0};
+    __shared__ f32x4 rs[256], rq[256], rx[256];
+    f32x4 sg = {0, 0, 0, 0}, sgx = {0, 0, 0, 0}, sx = {0, 0, 0, 0};
     if (slot < slots) {
         const f32x4 mu = *reinterpret_cast<const f32x4*>(mean + c);
         const f32x4 is = *reinterpret_cast<const f32x4*>(invstd + c);
@@ -101,43 +101,52 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const float g = fmaf(v[k], sc[k], sh[k]) > 0.f ? d[k] : 0.f;
+                const float xh = (v[k] - mu[k]) * is[k];
                 sg[k] += g;
-                sgx[k] = fmaf(g, (v[k] - mu[k]) * is[k], sgx[k]);
+                sgx[k] = fmaf(g, xh, sgx[k]);
+                sx[k] += xh;
             }
         }
     }
     rs[tid] = sg;
     rq[tid] = sgx;
+    rx[tid] = sx;
     __syncthreads();
     if (slot == 0) {
         for (int s = 1; s < slots; ++s) {
             sg += rs[s * c4n + q];
             sgx += rq[s * c4n + q];
+            sx += rx[s * c4n + q];
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             part[(size_t)(c + k) * nblk + blockIdx.x] = sg[k];
             part[((size_t)C + c + k) * nblk + blockIdx.x] = sgx[k];
+            part[((size_t)2 * C + c + k) * nblk + blockIdx.x] = sx[k];
         }
     }
 }
 
 __global__ void bn_bwd_finalize_kernel(const float* part, int nblk, int C, int64_t npix,
-                                       float* dgamma, float* dbeta, int acc, float* coef) {
+                                       const float* scale, float* dgamma, float* dbeta,
+                                       float* dbias, int acc, float* coef) {
     const int c = blockIdx.x;
-    __shared__ double s1[256], s2[256];
-    double a = 0, b = 0;
+    __shared__ double s1[256], s2[256], s3[256];
+    double a = 0, b = 0, x = 0;
     for (int i = threadIdx.x; i < nblk; i += blockDim.x) {
         a += part[(size_t)c * nblk + i];
         b += part[((size_t)C + c) * nblk + i];
+        x += part[((size_t)2 * C + c) * nblk + i];
     }
     s1[threadIdx.x] = a;
     s2[threadIdx.x] = b;
+    s3[threadIdx.x] = x;
     __syncthreads();
     for (int s = blockDim.x / 2; s > 0; s >>= 1) {
         if (threadIdx.x < s) {
             s1[threadIdx.x] += s1[threadIdx.x + s];
             s2[threadIdx.x] += s2[threadIdx.x + s];
+            s3[threadIdx.x] += s3[threadIdx.x + s];
         }
         __syncthreads();
     }
@@ -145,8 +154,14 @@ __global__ void bn_bwd_finalize_kernel(const float* part, int nblk, int C, int64
         const float sg = (float)s1[0], sgx = (float)s2[0];
         if (dgamma) dgamma[c] = acc ? dgamma[c] + sgx : sgx;
         if (dbeta) dbeta[c] = acc ? dbeta[c] + sg : sg;
-        coef[c] = (float)(s1[0] / (double)npix);      // mean(g)
-        coef[C + c] = (float)(s2[0] / (double)npix);  // mean(g*xhat)
+        const double mg = s1[0] / (double)npix, mgx = s2[0] / (double)npix;
+        coef[c] = (float)mg;         // mean(g)
+        coef[C + c] = (float)mgx;    // mean(g*xhat)
+        if (dbias) {
+            // sum_p dy_p = scale*(sum g - N*mean(g) - mean(g*xhat)*sum xhat)
+            const float db = (float)((double)scale[c] * (s1[0] - (double)npix * mg - mgx * s3[0]));
+            dbias[c] = acc ? dbias[c] + db : db;
+        }
     }
 }
 
@@ -230,13 +245,13 @@ extern "C" int ugpg_bn_eval_params(const float* gamma, const float* beta, const 
 
 extern "C" size_t ugpg_bn_relu_bwd_workspace(int64_t npix, int C) {
     BwdPlan p = bwd_plan(npix);
-    return ((size_t)2 * C * p.nblk + (size_t)2 * C) * sizeof(float);
+    return ((size_t)3 * C * p.nblk + (size_t)2 * C) * sizeof(float);
 }
 
 extern "C" int ugpg_bn_relu_bwd(const float* da, const float* y, int64_t npix, int C,
                                 const float* mean, const float* invstd, const float* scale,
                                 const float* shift, float* dy, float* dgamma, float* dbeta,
-                                int acc, void* ws, size_t ws_bytes, void* stream) {
+                                float* dbias, int acc, void* ws, size_t ws_bytes, void* stream) {
     if (!da || !y || !dy || !mean || !invstd || !scale || !shift || C % 4 || C > 1024 ||
         npix <= 0) {
         set_error("bn_relu_bwd: bad arguments (C=%d)", C);
@@ -249,13 +264,13 @@ extern "C" int ugpg_bn_relu_bwd(const float* da, const float* y, int64_t npix, i
     }
     BwdPlan p = bwd_plan(npix);
     float* part = static_cast<float*>(ws);
-    float* coef = part + (size_t)2 * C * p.nblk;
+    float* coef = part + (size_t)3 * C * p.nblk;
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(p.nblk), dim3(256), 0, st, da, y, npix, C, mean,
                        invstd, scale, shift, p.ppb, part, p.nblk);
     if (int e = check_launch("bn_bwd_reduce")) return e;
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, part, p.nblk, C, npix,
-                       dgamma, dbeta, acc, coef);
+                       scale, dgamma, dbeta, dbias, acc, coef);
     if (int e = check_launch("bn_bwd_finalize")) return e;
     hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(stream_grid(npix * C / 4)), dim3(256), 0, st, da,
                        y, npix, C, mean, invstd, scale, shift, coef, dy);

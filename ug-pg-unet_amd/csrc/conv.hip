@@ -145,33 +145,39 @@ __global__ void __launch_bounds__(256) conv3x3_fwd_kernel(ConvFwdArgs a) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) boff[nt] = (wn * WTN + nt * 32 + (lane & 31)) * 8 + 4 * (lane >> 5);
 
+    // fragment loads of step i (= tap t, channel group g): A from the halo, B from the slab
+    constexpr int NSTEP = 9 * G;
+    auto ldfrag = [&](int i, f32x4* af, f32x4* bf) {
+        const int t = i / G, g = i % G;
+        const int toff = ((t / 3) * HWD + (t % 3)) * AP + g * 8;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+            af[mt] = *reinterpret_cast<const f32x4*>(&As[aoff[mt] + toff]);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+            bf[nt] = *reinterpret_cast<const f32x4*>(&Bs[i * BN * 8 + boff[nt]]);
+    };
+
     const int nchunk = a.Cin / BKC;
     gload(0);
     lstore(0);
     __syncthreads();
     for (int c = 0; c < nchunk; ++c) {
         if (c + 1 < nchunk) gload(c + 1);
+        // software-pipelined: step i+1's ds_reads are in flight under step i's MFMAs
+        f32x4 fa[2][MT], fb[2][NT];
+        ldfrag(0, fa[0], fb[0]);
 #pragma unroll
-        for (int t = 0; t < 9; ++t) {
-            const int toff = ((t / 3) * HWD + (t % 3)) * AP;
+        for (int i = 0; i < NSTEP; ++i) {
+            if (i + 1 < NSTEP) ldfrag(i + 1, fa[(i + 1) & 1], fb[(i + 1) & 1]);
 #pragma unroll
-            for (int g = 0; g < G; ++g) {
-                f32x4 af[MT], bf[NT];
+            for (int s = 0; s < 4; ++s)
 #pragma unroll
                 for (int mt = 0; mt < MT; ++mt)
-                    af[mt] = *reinterpret_cast<const f32x4*>(&As[aoff[mt] + toff + g * 8]);
 #pragma unroll
-                for (int nt = 0; nt < NT; ++nt)
-                    bf[nt] = *reinterpret_cast<const f32x4*>(&Bs[(t * G + g) * BN * 8 + boff[nt]]);
-#pragma unroll
-                for (int s = 0; s < 4; ++s)
-#pragma unroll
-                    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-                        for (int nt = 0; nt < NT; ++nt)
-                            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[mt][s], bf[nt][s],
-                                                                               acc[mt][nt], 0, 0, 0);
-            }
+                    for (int nt = 0; nt < NT; ++nt)
+                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+                            fa[i & 1][mt][s], fb[i & 1][nt][s], acc[mt][nt], 0, 0, 0);
         }
         __syncthreads();
         if (c + 1 < nchunk) {
@@ -390,16 +396,27 @@ __global__ void __launch_bounds__(256) conv3x3_wgrad_kernel(WgradArgs a) {
         __syncthreads();
         if (tile + 1 < t_end) gload(tile + 1);
         const int arow = wm * 32 + (lane & 31), bcol = wn * 32 + (lane & 31);
-#pragma unroll 4
-        for (int ks = 0; ks < P / 2; ++ks) {
+        // k-step ks = pixels 2ks, 2ks+1; fragments of step ks+1 prefetched under step ks
+        auto ldk = [&](int ks, float& af, float* bf) {
             const int p = 2 * ks + (lane >> 5);
-            const float af = dys[p * 64 + arow];
+            af = dys[p * 64 + arow];
             const int hb = ((p / TW) * HWD + (p % TW)) * 64 + bcol;
 #pragma unroll
-            for (int t = 0; t < 9; ++t) {
-                const float bf = xs[hb + ((t / 3) * HWD + (t % 3)) * 64];
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(af, bf, acc[t], 0, 0, 0);
-            }
+            for (int t = 0; t < 9; ++t) bf[t] = xs[hb + ((t / 3) * HWD + (t % 3)) * 64];
+        };
+        static_assert((P / 2) % 2 == 0, "two-step body needs an even k-step count");
+        float a0, a1, b0[9], b1[9];
+        ldk(0, a0, b0);
+#pragma unroll 1
+        for (int ks = 0; ks < P / 2; ks += 2) {
+            ldk(ks + 1, a1, b1);
+#pragma unroll
+            for (int t = 0; t < 9; ++t)
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0[t], acc[t], 0, 0, 0);
+            if (ks + 2 < P / 2) ldk(ks + 2, a0, b0);
+#pragma unroll
+            for (int t = 0; t < 9; ++t)
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1[t], acc[t], 0, 0, 0);
         }
         if (do_db) {
             float s = 0.f;
@@ -421,19 +438,33 @@ __global__ void __launch_bounds__(256) conv3x3_wgrad_kernel(WgradArgs a) {
     if (do_db) a.dbpart[(size_t)split * a.Cout + co0 + tid] = dbacc;
 }
 
-__global__ void wgrad_reduce_kernel(const float* part, const float* dbpart, int nsplit, int Cout,
-                                    int Cin, int Cin_real, float* dw, float* db, int accumulate) {
-    const int64_t total = (int64_t)9 * Cout * Cin_real;
-    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
-         e += (int64_t)gridDim.x * blockDim.x) {
-        // e enumerates (t, co, ci) with ci fastest: coalesced partial reads
-        const int ci = (int)(e % Cin_real);
-        const int64_t r = e / Cin_real;
+// Fixed-order split-K reduction.  Block = 64 consecutive ci of one (t, co) row
+// x 4 split-groups; each thread sums every 4th split, then a 4-way LDS combine
+// (deterministic: the summation tree depends only on nsplit).
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* part, const float* dbpart,
+                                                           int nsplit, int Cout, int Cin,
+                                                           int Cin_real, float* dw, float* db,
+                                                           int accumulate) {
+    __shared__ float red[4][64];
+    const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+    const int ncb = (Cin_real + 63) / 64;
+    const int64_t rows = (int64_t)9 * Cout;
+    for (int64_t bi = blockIdx.x; bi < rows * ncb; bi += gridDim.x) {
+        const int64_t r = bi / ncb;  // (t, co)
+        const int ci = (int)(bi % ncb) * 64 + lane;
         const int co = (int)(r % Cout), t = (int)(r / Cout);
         float s = 0.f;
-        for (int k = 0; k < nsplit; ++k) s += part[((size_t)(k * 9 + t) * Cout + co) * Cin + ci];
-        const size_t o = ((size_t)co * Cin_real + ci) * 9 + t;
-        dw[o] = accumulate ? dw[o] + s : s;
+        if (ci < Cin_real)
+            for (int k = grp; k < nsplit; k += 4)
+                s += part[((size_t)(k * 9 + t) * Cout + co) * Cin + ci];
+        red[grp][lane] = s;
+        __syncthreads();
+        if (grp == 0 && ci < Cin_real) {
+            s = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+            const size_t o = ((size_t)co * Cin_real + ci) * 9 + t;
+            dw[o] = accumulate ? dw[o] + s : s;
+        }
+        __syncthreads();
     }
     if (db && blockIdx.x == 0) {
         for (int co = threadIdx.x; co < Cout; co += blockDim.x) {
@@ -506,10 +537,12 @@ WgradPlan wgrad_plan(int B, int H, int W, int Cin, int Cout) {
     p.tiles_y = (int)cdiv(H, WG_TH);
     p.ntiles = B * p.tiles_x * p.tiles_y;
     const int64_t base = (int64_t)(Cout / 64) * cdiv(Cin, 64);
-    int64_t ns = cdiv(1024, base);
-    // cap the fp32 partial slab at 64 MB
+    // 2 co-resident blocks per CU (232 VGPR+AGPR, 44 KB LDS): aim for a multiple of 512
+    int64_t ns = cdiv(512, base);
+    if (ns * base < 512) ns = cdiv(1024, base);
+    // cap the fp32 partial slab at 192 MB
     const int64_t per = (int64_t)9 * Cout * Cin * 4;
-    int64_t cap = (64ll << 20) / per;
+    int64_t cap = (192ll << 20) / per;
     if (cap < 1) cap = 1;
     if (ns > cap) ns = cap;
     if (ns > p.ntiles) ns = p.ntiles;
@@ -675,8 +708,9 @@ extern "C" int ugpg_conv3x3_wgrad(const ugpg_wgrad_t* p, void* ws, size_t ws_byt
     hipLaunchKernelGGL((conv3x3_wgrad_kernel<WG_TH, WG_TW>), dim3(grid), dim3(256), 0, st, a);
     if (int e = check_launch("conv3x3_wgrad")) return e;
     const int Cr = p->Cin_real > 0 ? p->Cin_real : Cin;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(stream_grid((int64_t)9 * p->Cout * Cr)),
-                       dim3(256), 0, st, a.part, a.dbpart, w.nsplit, p->Cout, Cin, Cr, p->dw,
-                       p->db, p->accumulate);
+    int64_t rblocks = (int64_t)9 * p->Cout * cdiv(Cr, 64);
+    if (rblocks > 4096) rblocks = 4096;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)rblocks), dim3(256), 0, st, a.part,
+                       a.dbpart, w.nsplit, p->Cout, Cin, Cr, p->dw, p->db, p->accumulate);
     return check_launch("conv3x3_wgrad_reduce");
 }

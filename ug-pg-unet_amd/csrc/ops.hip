@@ -388,12 +388,29 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(const float* x, const flo
     }
 }
 
-__global__ void head_bwd_finalize_kernel(const float* part, int nblk, int nc, int C, float* dw,
-                                         float* db) {
+// fixed-order block tree: thread i sums i, i+256, ... then an LDS tree
+__device__ __forceinline__ double block_tree_sum(double v) {
+    __shared__ double t[256];
+    t[threadIdx.x] = v;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s) t[threadIdx.x] += t[threadIdx.x + s];
+        __syncthreads();
+    }
+    const double r = t[0];
+    __syncthreads();
+    return r;
+}
+
+// one block per output element (nc*(C+1) of them)
+__global__ void __launch_bounds__(256) head_bwd_finalize_kernel(const float* part, int nblk, int nc,
+                                                                int C, float* dw, float* db) {
     const int total = nc * (C + 1);
-    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
-        double s = 0;
-        for (int i = 0; i < nblk; ++i) s += part[(size_t)i * total + e];
+    const int e = blockIdx.x;
+    double s = 0;
+    for (int i = threadIdx.x; i < nblk; i += 256) s += part[(size_t)i * total + e];
+    s = block_tree_sum(s);
+    if (threadIdx.x == 0) {
         const int k = e / (C + 1), c = e % (C + 1);
         if (c < C) dw[(size_t)k * C + c] = (float)s;
         else if (db) db[k] = (float)s;
@@ -450,16 +467,19 @@ __global__ void __launch_bounds__(256) ug_loss_fwd_kernel(const float* x, const 
     }
 }
 
-__global__ void ug_loss_finalize_kernel(const double* part, int nblk, int64_t n, int has_u,
-                                        float* out) {
-    if (threadIdx.x != 0) return;
+__global__ void __launch_bounds__(256) ug_loss_finalize_kernel(const double* part, int nblk,
+                                                               int64_t n, int has_u, float* out) {
     double sp = 0, sw = 0;
-    for (int i = 0; i < nblk; ++i) {
+    for (int i = threadIdx.x; i < nblk; i += 256) {
         sp += part[2 * i];
         sw += part[2 * i + 1];
     }
-    out[0] = (float)((has_u ? sw : sp) / (double)n);
-    out[1] = (float)(sp / (double)n);
+    sp = block_tree_sum(sp);
+    sw = block_tree_sum(sw);
+    if (threadIdx.x == 0) {
+        out[0] = (float)((has_u ? sw : sp) / (double)n);
+        out[1] = (float)(sp / (double)n);
+    }
 }
 
 __global__ void ug_loss_bwd_kernel(const float* x, const float* t, const float* u, int64_t n,
@@ -516,22 +536,29 @@ __global__ void __launch_bounds__(256) seg_metrics_kernel(const float* x, const 
     }
 }
 
-__global__ void seg_metrics_finalize_kernel(const float* part, int B, int nbps, int64_t npix,
-                                            float* out) {
-    if (threadIdx.x != 0) return;
-    float dsum = 0.f;
-    double wrong = 0;
-    for (int b = 0; b < B; ++b) {
-        float s[4] = {0, 0, 0, 0};  // counts: exact in fp32
-        for (int k = 0; k < nbps; ++k)
-            for (int q = 0; q < 4; ++q) s[q] += part[((size_t)b * nbps + k) * 4 + q];
-        const float d = (2.0f * s[0] + 1.0f) / (s[1] + s[2] + 1.0f);
-        dsum += d;
-        wrong += s[3];
+__global__ void __launch_bounds__(256) seg_metrics_finalize_kernel(const float* part, int B,
+                                                                   int nbps, int64_t npix,
+                                                                   float* out) {
+    // per-sample counts (exact in fp32), one thread per (sample, quantity)
+    __shared__ float cnt[1024];
+    for (int e = threadIdx.x; e < B * 4; e += 256) {
+        const int b = e >> 2, q = e & 3;
+        float s = 0.f;
+        for (int k = 0; k < nbps; ++k) s += part[((size_t)b * nbps + k) * 4 + q];
+        cnt[e] = s;
     }
-    out[0] = dsum / (float)B;
-    out[1] = (float)(1.0 - wrong / (double)npix);
-    out[2] = (float)wrong;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float dsum = 0.f;
+        double wrong = 0;
+        for (int b = 0; b < B; ++b) {
+            dsum += (2.0f * cnt[4 * b] + 1.0f) / (cnt[4 * b + 1] + cnt[4 * b + 2] + 1.0f);
+            wrong += cnt[4 * b + 3];
+        }
+        out[0] = dsum / (float)B;
+        out[1] = (float)(1.0 - wrong / (double)npix);
+        out[2] = (float)wrong;
+    }
 }
 
 __global__ void __launch_bounds__(256) mean_std_part_kernel(const float* x, int64_t n,
@@ -560,10 +587,12 @@ __global__ void __launch_bounds__(256) mean_std_part_kernel(const float* x, int6
     }
 }
 
-__global__ void mean_std_finalize_kernel(const double* part, int nblk, float* out) {
-    if (threadIdx.x != 0) return;
+__global__ void __launch_bounds__(256) mean_std_finalize_kernel(const double* part, int nblk,
+                                                                float* out) {
+    // Chan merge: strided per thread, then a fixed LDS tree
+    __shared__ double sn[256], sm[256], sq[256];
     double n = 0, mu = 0, M = 0;
-    for (int i = 0; i < nblk; ++i) {
+    for (int i = threadIdx.x; i < nblk; i += 256) {
         const double nb = part[3 * i];
         if (nb <= 0) continue;
         const double nn = n + nb, d = part[3 * i + 1] - mu;
@@ -571,8 +600,26 @@ __global__ void mean_std_finalize_kernel(const double* part, int nblk, float* ou
         M += part[3 * i + 2] + d * d * n * nb / nn;
         n = nn;
     }
-    out[0] = (float)mu;
-    out[1] = (float)(n > 1 ? sqrt(M / (n - 1)) : (double)NAN);
+    sn[threadIdx.x] = n;
+    sm[threadIdx.x] = mu;
+    sq[threadIdx.x] = M;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s) {
+            const double na = sn[threadIdx.x], nb = sn[threadIdx.x + s];
+            if (nb > 0) {
+                const double nn = na + nb, d = sm[threadIdx.x + s] - sm[threadIdx.x];
+                sm[threadIdx.x] += d * nb / nn;
+                sq[threadIdx.x] += sq[threadIdx.x + s] + d * d * na * nb / nn;
+                sn[threadIdx.x] = nn;
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        out[0] = (float)sm[0];
+        out[1] = (float)(sn[0] > 1 ? sqrt(sq[0] / (sn[0] - 1)) : (double)NAN);
+    }
 }
 
 // ------------------------------------------------------------- RMSprop
@@ -854,7 +901,7 @@ extern "C" int ugpg_head_bwd(ugpg_src_t s, int64_t npix, const float* w, int nc,
     hipLaunchKernelGGL(head_bwd_kernel, dim3(nblk), dim3(256), 0, st, s.data, s.scale, s.shift,
                        npix, s.C, w, nc, dh, da, acc_da, ppb, static_cast<float*>(ws), nblk);
     if (int e = check_launch("head_bwd")) return e;
-    hipLaunchKernelGGL(head_bwd_finalize_kernel, dim3(cdiv(nc * (s.C + 1), 256)), dim3(256), 0,
+    hipLaunchKernelGGL(head_bwd_finalize_kernel, dim3(nc * (s.C + 1)), dim3(256), 0,
                        st, static_cast<const float*>(ws), nblk, nc, s.C, dw, db);
     return check_launch("head_bwd_finalize");
 }
@@ -876,7 +923,7 @@ static int loss_fwd_common(const float* x, const float* t, const float* u, int B
     hipLaunchKernelGGL(ug_loss_fwd_kernel, dim3(nblk), dim3(256), 0, st, x, t, u, n, C, HW, Cu, pw,
                        alpha, pl, static_cast<double*>(ws));
     if (int e = check_launch(name)) return e;
-    hipLaunchKernelGGL(ug_loss_finalize_kernel, dim3(1), dim3(64), 0, st,
+    hipLaunchKernelGGL(ug_loss_finalize_kernel, dim3(1), dim3(256), 0, st,
                        static_cast<const double*>(ws), nblk, n, u ? 1 : 0, out);
     return check_launch(name);
 }
@@ -932,7 +979,7 @@ extern "C" int ugpg_seg_metrics(const float* x, const float* t, int B, int HW, f
     hipLaunchKernelGGL(seg_metrics_kernel, dim3(nbps, B), dim3(256), 0, st, x, t, HW, nbps,
                        static_cast<float*>(ws));
     if (int e = check_launch("seg_metrics")) return e;
-    hipLaunchKernelGGL(seg_metrics_finalize_kernel, dim3(1), dim3(64), 0, st,
+    hipLaunchKernelGGL(seg_metrics_finalize_kernel, dim3(1), dim3(256), 0, st,
                        static_cast<const float*>(ws), B, nbps, (int64_t)B * HW, out);
     return check_launch("seg_metrics_finalize");
 }
@@ -955,7 +1002,7 @@ extern "C" int ugpg_mean_std(const float* x, int64_t n, float* out, void* ws, si
     hipLaunchKernelGGL(mean_std_part_kernel, dim3(nblk), dim3(256), 0, st, x, n, per,
                        static_cast<double*>(ws));
     if (int e = check_launch("mean_std")) return e;
-    hipLaunchKernelGGL(mean_std_finalize_kernel, dim3(1), dim3(64), 0, st,
+    hipLaunchKernelGGL(mean_std_finalize_kernel, dim3(1), dim3(256), 0, st,
                        static_cast<const double*>(ws), nblk, out);
     return check_launch("mean_std_finalize");
 }

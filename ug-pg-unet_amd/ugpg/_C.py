@@ -46,7 +46,7 @@ SIGNATURES = {
     "ugpg_bn_finalize": (_i, [_p, _i, _i, _p, _p, _p, _p, _p, _f, _f, _p, _p, _p, _p, _p]),
     "ugpg_bn_eval_params": (_i, [_p, _p, _p, _p, _f, _i, _p, _p, _p]),
     "ugpg_bn_relu_bwd_workspace": (_sz, [_i64, _i]),
-    "ugpg_bn_relu_bwd": (_i, [_p, _p, _i64, _i, _p, _p, _p, _p, _p, _p, _p, _i, _p, _sz, _p]),
+    "ugpg_bn_relu_bwd": (_i, [_p, _p, _i64, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i, _p, _sz, _p]),
     "ugpg_bn_relu_apply": (_i, [Src, _i64, _p, _p]),
     "ugpg_maxpool2_fwd": (_i, [Src, _i, _i, _i, _p, _p, _p]),
     "ugpg_maxpool2_bwd": (_i, [_p, _p, _i, _i, _i, _i, _p, _i, _p]),

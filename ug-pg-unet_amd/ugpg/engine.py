@@ -107,14 +107,14 @@ def _bn_relu_wgrad(conv, bn, y, st, in_srcs, dy, grads):
     mean, invstd, scale, shift = st
     if mean is None:
         raise RuntimeError("backward through an eval-mode BatchNorm is not supported")
+    # the conv bias gradient (sum of dy) comes out of the BN-backward reduction
+    db = grads.get(conv.bias) if conv.bias is not None else None
     ops.bn_relu_bwd(dy, y, mean, invstd, scale, shift, dy, grads.get(bn.weight),
-                    grads.get(bn.bias))
-    dw, db = grads.get(conv.weight), grads.get(conv.bias)
-    if dw is not None or db is not None:
-        if dw is None:
-            dw = torch.empty_like(conv.weight)
+                    grads.get(bn.bias), db)
+    dw = grads.get(conv.weight)
+    if dw is not None:
         co, ci = conv.weight.shape[0], conv.weight.shape[1]
-        ops.conv3x3_wgrad(in_srcs, dy, dw, db, ci, flops=2.0 * dy.numel() / co * co * 9 * ci)
+        ops.conv3x3_wgrad(in_srcs, dy, dw, None, ci, flops=2.0 * dy.numel() / co * co * 9 * ci)
 
 
 def double_conv_backward(mod, ctx: BlockCtx, da2, targets, acc_flags, grads, pad_out=None):

@@ -181,13 +181,14 @@ def bn_eval_params(gamma, beta, rm, rv, eps):
     return scale, shift
 
 
-def bn_relu_bwd(da, y, mean, invstd, scale, shift, dy, dgamma, dbeta, accumulate=0):
+def bn_relu_bwd(da, y, mean, invstd, scale, shift, dy, dgamma, dbeta, dconv_bias=None,
+                accumulate=0):
     c = y.shape[-1]
     npix = y.numel() // c
     ws = workspace(lib.ugpg_bn_relu_bwd_workspace(npix, c), y.device)
     check(lib.ugpg_bn_relu_bwd(ptr(da), ptr(y), npix, c, ptr(mean), ptr(invstd), ptr(scale),
-                               ptr(shift), ptr(dy), ptr(dgamma), ptr(dbeta), int(accumulate),
-                               ptr(ws), ws.numel(), stream()), "bn_relu_bwd")
+                               ptr(shift), ptr(dy), ptr(dgamma), ptr(dbeta), ptr(dconv_bias),
+                               int(accumulate), ptr(ws), ws.numel(), stream()), "bn_relu_bwd")
 
 
 # ------------------------------------------------------------------ pool / resize
