@@ -214,8 +214,27 @@ int ugpg_linear_fwd(const float* x, const float* w, const float* b, int M, int N
 /* given dy (already masked by relu if any): dx = dy*w, dw = dy^T x, db = sum dy */
 int ugpg_linear_bwd(const float* x, const float* w, const float* dy, int M, int N, int K,
                     float* dx, float* dw, float* db, void* stream);
-/* in-place relu backward mask: dy *= (y > 0) */
-int ugpg_relu_bwd(const float* y, float* dy, int64_t n, void* stream);
+/* nn.Dropout mask: mask[i] = (u_i >= p) / (1-p), u_i = counter hash of (seed, i) */
+int ugpg_dropout_mask(float* mask, int64_t n, float p, uint64_t seed, void* stream);
+/* Herlev uncertainty-guided CE (train_herlev.py:253-296), K > 2 classes:
+ *   base = CE(x, y; class_weights) (weighted mean), u_b = H(softmax(prev_b))/log K,
+ *   final = mean_b(CE_b * (1 + alpha*u_b))  (prev == NULL: final = base)
+ * out = [final, base, mean(1+alpha*u), std(1+alpha*u), #(argmax == y)];
+ * weights[b] = 1+alpha*u_b. */
+int ugpg_ce_ug_fwd(const float* x, const int64_t* y, const float* prev,
+                   const float* class_weights, int B, int K, float alpha, float* out,
+                   float* weights, void* stream);
+/* d final / d x (weights == NULL: gradient of the class-weighted base CE) */
+int ugpg_ce_ug_bwd(const float* x, const int64_t* y, const float* weights,
+                   const float* class_weights, int B, int K, const float* gout, float* dx,
+                   void* stream);
+/* torch.optim.Adam rule (no amsgrad): g += wd*p; m = lerp(m, g, 1-b1);
+ * v = b2*v + (1-b2)*g^2; p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps) */
+int ugpg_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                   int64_t n, float lr, float beta1, float beta2, float eps, float weight_decay,
+                   int64_t step, float grad_scale, void* stream);
+/* relu backward: dx = dy * (y > 0)  (dx may alias dy) */
+int ugpg_relu_bwd(const float* y, const float* dy, float* dx, int64_t n, void* stream);
 /* elementwise y = x * mask (dropout with a precomputed scaled mask) */
 int ugpg_mul(const float* x, const float* m, float* y, int64_t n, void* stream);
 

@@ -134,6 +134,32 @@ def test_trainer_epoch_golden(dev):
         assert abs(tup[4] - ref[4]) <= 1e-5 and abs(tup[5] - ref[5]) <= 1e-5
 
 
+def test_train_progressive_pipeline(dev, tmp_path):
+    """Config 5 in miniature: stages 1->4 with weight transfer, U-map from stage s-1,
+    validation, best-Dice checkpoints in the reference's dict format."""
+    from torch.utils.data import DataLoader, TensorDataset
+    import ugpg
+    torch.manual_seed(0)
+    tr = ugpg.UncertaintyGuidedProgressiveTrainer(3, 1, device=dev, uncertainty_alpha=1.0)
+    for s in tr.stage_configs:
+        tr.stage_configs[s]["epochs_per_stage"] = 1
+    x = G.randn(91, (4, 3, 256, 256), "x")
+    t = G.bernoulli(92, (4, 1, 256, 256), 0.3, "t")
+    loader = DataLoader(TensorDataset(x, t), batch_size=2)
+    tr.train_progressive(loader, loader, max_stages=4, save_dir=str(tmp_path))
+    assert len(tr.history["train_loss"]) == 4 and tr.history["stage_transitions"] == [0, 1, 2, 3]
+    assert all(np.isfinite(tr.history["train_loss"])) and all(0 <= d <= 1 for d in tr.history["val_dice"])
+    for s in range(1, 5):
+        ck = tmp_path / f"ug_pgunet_stage{s}_best.pth"
+        if not ck.exists():
+            continue  # saved only when val Dice improves on 0
+        d = torch.load(ck, map_location="cpu", weights_only=True)
+        assert set(d) == {"stage", "epoch", "model_state_dict", "optimizer_state_dict", "val_dice",
+                          "train_dice", "uncertainty_alpha", "history"}
+        assert list(d["model_state_dict"]) == [k for k, _, _ in O.state_spec(s, 3, 1)]
+        assert set(d["optimizer_state_dict"]["state"][0]) == {"step", "square_avg"}
+
+
 def test_rmsprop_step_matches_oracle(dev):
     """Two ugpg RMSprop steps (flat single-launch path) == the oracle's
     torch.optim.RMSprop rule applied to the same (GPU-computed) gradients."""

@@ -342,7 +342,7 @@ def test_avgpool_linear(dev):
     yo = ops.linear_fwd(out, w.detach().float().to(dev), b.detach().float().to(dev), True)
     close(yo.cpu(), yr, 1e-5, "linear fwd")
     dyd = dy.to(dev).contiguous()
-    ops.relu_bwd_(yo, dyd)
+    dyd = ops.relu_bwd(yo, dyd)
     dx = torch.empty(B, C, device=dev)
     dw = torch.empty(256, C, device=dev)
     db = torch.empty(256, device=dev)

@@ -128,6 +128,19 @@ def test_models_refuse_cpu_execution():
         m(torch.zeros(1, 3, 32, 32))
 
 
+@pytest.mark.parametrize("stage", [1, 2, 3, 4])
+def test_herlev_model_checkpoint_format(stage):
+    """Key layout of the reference HerlevClassificationModel (train_herlev.py:29-121);
+    the oracle spec is pinned by g7 (loaded strictly into the reference model)."""
+    from ugpg.herlev import HerlevClassificationModel
+    m = HerlevClassificationModel(stage, 7)
+    want = [k for k, _, _ in O.state_spec(stage, 3, 1, key_prefix="unet.")]
+    want += [k for k, _, _ in O.herlev_head_spec(512, 7)]
+    assert list(m.state_dict().keys()) == want
+    state = G.make_state(O.state_spec(stage, 3, 1, key_prefix="unet.") + O.herlev_head_spec(512, 7), 3)
+    m.load_state_dict(state, strict=True)
+
+
 def test_shard_helper():
     from ugpg.dist import shard
     x = torch.arange(16).view(16, 1)

@@ -729,10 +729,10 @@ __global__ void linear_bwd_dw_kernel(const float* x, const float* dy, int M, int
     }
 }
 
-__global__ void relu_bwd_kernel(const float* y, float* dy, int64_t n) {
+__global__ void relu_bwd_kernel(const float* y, const float* dy, float* dx, int64_t n) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x)
-        if (!(y[i] > 0.f)) dy[i] = 0.f;
+        dx[i] = y[i] > 0.f ? dy[i] : 0.f;
 }
 
 __global__ void mul_kernel(const float* x, const float* m, float* y, int64_t n) {
@@ -1061,10 +1061,11 @@ extern "C" int ugpg_linear_bwd(const float* x, const float* w, const float* dy, 
     return check_launch("linear_bwd_dw");
 }
 
-extern "C" int ugpg_relu_bwd(const float* y, float* dy, int64_t n, void* stream) {
-    UGPG_REQUIRE(y && dy, "relu_bwd");
+extern "C" int ugpg_relu_bwd(const float* y, const float* dy, float* dx, int64_t n,
+                             void* stream) {
+    UGPG_REQUIRE(y && dy && dx, "relu_bwd");
     hipLaunchKernelGGL(relu_bwd_kernel, dim3(stream_grid(n)), dim3(256), 0, as_stream(stream), y,
-                       dy, n);
+                       dy, dx, n);
     return check_launch("relu_bwd");
 }
 

@@ -74,7 +74,11 @@ SIGNATURES = {
     "ugpg_avgpool_bwd": (_i, [_p, _i, _i, _i, _p, _i, _p]),
     "ugpg_linear_fwd": (_i, [_p, _p, _p, _i, _i, _i, _i, _p, _p]),
     "ugpg_linear_bwd": (_i, [_p, _p, _p, _i, _i, _i, _p, _p, _p, _p]),
-    "ugpg_relu_bwd": (_i, [_p, _p, _i64, _p]),
+    "ugpg_dropout_mask": (_i, [_p, _i64, _f, C.c_uint64, _p]),
+    "ugpg_ce_ug_fwd": (_i, [_p, _p, _p, _p, _i, _i, _f, _p, _p, _p]),
+    "ugpg_ce_ug_bwd": (_i, [_p, _p, _p, _p, _i, _i, _p, _p, _p]),
+    "ugpg_adam_step": (_i, [_p, _p, _p, _p, _i64, _f, _f, _f, _f, _f, _i64, _f, _p]),
+    "ugpg_relu_bwd": (_i, [_p, _p, _p, _i64, _p]),
     "ugpg_mul": (_i, [_p, _p, _p, _i64, _p]),
 }
 

@@ -395,8 +395,40 @@ def linear_bwd(x, w, dy, dx, dw, db):
                               stream()), "linear_bwd")
 
 
-def relu_bwd_(y, dy):
-    check(lib.ugpg_relu_bwd(ptr(y), ptr(dy), y.numel(), stream()), "relu_bwd")
+def dropout_mask(n, p, seed, device):
+    m = torch.empty(n, dtype=F32, device=device)
+    check(lib.ugpg_dropout_mask(ptr(m), n, float(p), int(seed) & ((1 << 64) - 1), stream()),
+          "dropout_mask")
+    return m
+
+
+def ce_ug_fwd(x, y, prev, class_weights, alpha, out=None):
+    B, K = x.shape
+    out = empty(5, like=x) if out is None else out
+    wts = empty(B, like=x) if prev is not None else None
+    check(lib.ugpg_ce_ug_fwd(_f32(x.contiguous()), ptr(y.contiguous()), ptr(prev), ptr(class_weights),
+                             B, K, float(alpha), ptr(out), ptr(wts), stream()), "ce_ug_fwd")
+    return out, wts
+
+
+def ce_ug_bwd(x, y, wts, class_weights, gout):
+    B, K = x.shape
+    dx = torch.empty_like(x)
+    check(lib.ugpg_ce_ug_bwd(ptr(x), ptr(y), ptr(wts), ptr(class_weights), B, K, ptr(gout),
+                             ptr(dx), stream()), "ce_ug_bwd")
+    return dx
+
+
+def adam_step(p, g, m, v, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0):
+    check(lib.ugpg_adam_step(_f32(p), _f32(g), _f32(m), _f32(v), p.numel(), float(lr),
+                             float(beta1), float(beta2), float(eps), float(weight_decay), int(step),
+                             float(grad_scale), stream()), "adam_step")
+
+
+def relu_bwd(y, dy, out=None):
+    dx = torch.empty_like(dy) if out is None else out
+    check(lib.ugpg_relu_bwd(ptr(y), ptr(dy), ptr(dx), y.numel(), stream()), "relu_bwd")
+    return dx
 
 
 def mul(x, m):

@@ -73,3 +73,65 @@ class RMSprop(Optimizer):
                     ops.rmsprop_step(p.data, g, self.state[p]["square_avg"], lr, a, eps, wd,
                                      self.grad_scale)
         return loss
+
+
+class Adam(Optimizer):
+    """torch.optim.Adam rule on libugpg (Herlev trainer, train_herlev.py:178-194);
+    state layout {'step', 'exp_avg', 'exp_avg_sq'} as in torch; flat single launch
+    when parameters, grads and moments are contiguous runs."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0,
+                 amsgrad=False, foreach=None, maximize=False, capturable=False,
+                 differentiable=False, fused=None):
+        if amsgrad or maximize or differentiable:
+            raise NotImplementedError("ugpg Adam implements amsgrad=False, maximize=False")
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False,
+                        foreach=None, maximize=False, capturable=False, differentiable=False,
+                        fused=None)
+        super().__init__(params, defaults)
+        self.grad_scale = 1.0
+
+    def _init_state(self, params):
+        fresh = [p for p in params if len(self.state[p]) == 0]
+        if not fresh:
+            return
+        total = sum(p.numel() for p in fresh)
+        m = torch.zeros(total, dtype=torch.float32, device=fresh[0].device)
+        v = torch.zeros(total, dtype=torch.float32, device=fresh[0].device)
+        off = 0
+        for p in fresh:
+            n = p.numel()
+            self.state[p]["step"] = torch.tensor(0.0)
+            self.state[p]["exp_avg"] = m[off:off + n].view_as(p)
+            self.state[p]["exp_avg_sq"] = v[off:off + n].view_as(p)
+            off += n
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for group in self.param_groups:
+            params = [p for p in group["params"] if p.grad is not None]
+            if not params:
+                continue
+            self._init_state(params)
+            for p in params:
+                self.state[p]["step"] += 1
+            b1, b2 = group["betas"]
+            lr, eps, wd = group["lr"], group["eps"], group["weight_decay"]
+            steps = {int(self.state[p]["step"]) for p in params}
+            runs = [contiguous_run(params), contiguous_run([p.grad for p in params]),
+                    contiguous_run([self.state[p]["exp_avg"] for p in params]),
+                    contiguous_run([self.state[p]["exp_avg_sq"] for p in params])]
+            if len(steps) == 1 and all(r is not None for r in runs):
+                (pf, _, _), (gf, _, _), (mf, _, _), (vf, _, _) = runs
+                ops.adam_step(pf, gf, mf, vf, lr, b1, b2, eps, wd, steps.pop(), self.grad_scale)
+            else:
+                for p in params:
+                    st = self.state[p]
+                    g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+                    ops.adam_step(p.data, g, st["exp_avg"], st["exp_avg_sq"], lr, b1, b2, eps, wd,
+                                  int(st["step"]), self.grad_scale)
+        return loss
