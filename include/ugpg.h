@@ -34,6 +34,10 @@ extern "C" {
 
 const char* ugpg_version(void);
 const char* ugpg_last_error(void);
+/* Tuning knobs for benchmarking (process-global; not for production use):
+ *   "fwd_cfg": force the 3x3 conv tile config (0 = 16x16x64, 1 = 8x16x128,
+ *              2 = 8x8x64) where it is legal for the shape; -1 = heuristic. */
+int ugpg_set_tuning(const char* key, int value);
 
 /* A lazily-activated NHWC operand: value = relu(scale[c]*x + shift[c]) when
  * scale != NULL (train/eval BatchNorm + ReLU folded into the consumer's load,

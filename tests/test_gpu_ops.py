@@ -49,6 +49,8 @@ CONV_CASES = [
     (2, 256, 256, 64, 0, 64, True),    # CFG_L (16x16 tile), multi-tile wgrad splits
     (4, 128, 128, 64, 0, 128, False),  # CFG_W (8x16 x 128)
     (2, 256, 256, 64, 64, 64, True),   # Up4-shaped: concat dgrad must not straddle the split
+    (4, 256, 256, 8, 0, 64, False),    # Inc-shaped image layer: narrow-input wgrad, many splits
+    (3, 40, 24, 8, 0, 128, True),      # ragged 8x16 wgrad tiles, 2 co blocks, lazy affine
 ]
 BIG = {5, 6, 7}
 
@@ -143,6 +145,11 @@ def test_conv3x3_dgrad_wgrad(dev, case):
     ops.conv3x3_wgrad(srcs, nhwc(dy).to(dev), dw, db, cin_real)
     close(dw.cpu(), wd.grad, 2e-5, "wgrad")
     close(db.cpu(), bd.grad, 2e-5, "bias grad")
+    if cin <= 8:
+        # without a bias grad the narrow-input kernel (conv3x3_wgrad_c8_kernel) runs
+        dw8 = torch.empty(Cout, cin_real, 3, 3, device=dev)
+        ops.conv3x3_wgrad(srcs, nhwc(dy).to(dev), dw8, None, cin_real)
+        close(dw8.cpu(), wd.grad, 2e-5, "wgrad (narrow input)")
 
 
 @pytest.mark.parametrize("C,npix", [(64, 5000), (512, 300), (128, 70000)])

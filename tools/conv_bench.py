@@ -1,0 +1,105 @@
+"""Per-layer conv kernel micro-benchmark (Stage-4, bs16) -- all variants in one
+process, interleaved rounds (cdna_hip_programming.md §5.4 rule 24).
+
+    python tools/conv_bench.py [--rounds 3] [--cfgs -1,0,1,2] [--wgrad]
+"""
+import argparse
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path[:0] = [str(ROOT), str(ROOT / "ug-pg-unet_amd")]
+
+import torch  # noqa: E402
+
+from ugpg import ops  # noqa: E402
+from ugpg._C import lib  # noqa: E402
+
+B = 16
+# name, H, C0, C1, Cout  (forward convs of PGUNet4; C1 = upsampled half of Up's concat)
+LAYERS = [("inc.0", 256, 8, 0, 64), ("inc.3", 256, 64, 0, 64),
+          ("down1.0", 128, 64, 0, 128), ("down1.3", 128, 128, 0, 128),
+          ("down2.0", 64, 128, 0, 256), ("down2.3", 64, 256, 0, 256),
+          ("down3.0", 32, 256, 0, 512), ("down3.3", 32, 512, 0, 512),
+          ("down4.0", 16, 512, 0, 512), ("down4.3", 16, 512, 0, 512),
+          ("up1.0", 32, 512, 512, 256), ("up1.3", 32, 256, 0, 256),
+          ("up2.0", 64, 256, 256, 128), ("up2.3", 64, 128, 0, 128),
+          ("up3.0", 128, 128, 128, 64), ("up3.3", 128, 64, 0, 64),
+          ("up4.0", 256, 64, 64, 64), ("up4.3", 256, 64, 0, 64)]
+
+
+def timeit(fn, iters=5):
+    fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--cfgs", default="-1,0,1,2")
+    ap.add_argument("--wgrad", action="store_true")
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    cfgs = [int(c) for c in a.cfgs.split(",")]
+    rows = {}
+    for name, H, C0, C1, Cout in LAYERS:
+        cin = C0 + C1
+        real_cin = 3 if cin == 8 else cin
+        srcs = [ops.Act(torch.randn(B, H, H, C0, device=dev),
+                        torch.rand(C0, device=dev) + 0.5, torch.randn(C0, device=dev) * 0.1)]
+        if C1:
+            srcs.append(ops.Act(torch.randn(B, H, H, C1, device=dev)))
+        w = torch.randn(Cout, real_cin, 3, 3, device=dev) * 0.05
+        wpk = ops.pack_conv3x3(w, cin, 0)
+        out = torch.empty(B, H, H, Cout, device=dev)
+        bias = torch.zeros(Cout, device=dev)
+        flops = 2.0 * B * H * H * Cout * 9 * real_cin
+        fns = {}
+        for c in cfgs:
+            def f(c=c):
+                lib.ugpg_set_tuning(b"fwd_cfg", c)
+                nt = ops.conv_ntiles(B, H, H, cin, Cout)
+                st = torch.empty(3 * Cout * nt, device=dev)
+                ops.conv3x3_fwd(srcs, wpk, bias, Cout, [out], stats=st)
+            fns[f"fwd{c}"] = f
+        if real_cin % 64 == 0:
+            dy = torch.randn(B, H, H, Cout, device=dev)
+            wpk1 = ops.pack_conv3x3(w, real_cin, 1)
+            d0 = torch.empty(B, H, H, C0, device=dev)
+            d1 = torch.empty(B, H, H, C1, device=dev) if C1 else None
+            for c in cfgs:
+                def g(c=c):
+                    lib.ugpg_set_tuning(b"fwd_cfg", c)
+                    ops.conv3x3_fwd([ops.Act(dy)], wpk1, None, real_cin, [d0, d1] if C1 else [d0],
+                                    split=C0 if C1 else None)
+                fns[f"dgrad{c}"] = g
+        if a.wgrad:
+            dy = torch.randn(B, H, H, Cout, device=dev)
+            dw = torch.empty_like(w)
+            fns["wgrad"] = lambda: ops.conv3x3_wgrad(srcs, dy, dw, None, real_cin)
+        res = {k: [] for k in fns}
+        for _ in range(a.rounds):
+            for k, f in fns.items():
+                try:
+                    res[k].append(timeit(f))
+                except RuntimeError as e:
+                    res[k].append(float("nan"))
+        lib.ugpg_set_tuning(b"fwd_cfg", -1)
+        rows[name] = {k: (min(v), flops / (min(v) * 1e-3) / 1e12) for k, v in res.items()}
+        print(name, " ".join(f"{k}={v[0]:.3f}ms/{v[1]:.0f}TF" for k, v in rows[name].items()),
+              flush=True)
+    tot = {}
+    for r in rows.values():
+        for k, (ms, _) in r.items():
+            tot[k] = tot.get(k, 0.0) + ms
+    print("TOTAL", " ".join(f"{k}={v:.2f}ms" for k, v in tot.items()))
+
+
+if __name__ == "__main__":
+    main()

@@ -39,8 +39,8 @@ struct ConvFwdArgs {
     int tiles_x, tiles_y, ntiles;
 };
 
-template <int TH, int TW, int BN, int BKC, int WM, int WN>
-__global__ void __launch_bounds__(256) conv3x3_fwd_kernel(ConvFwdArgs a) {
+template <int TH, int TW, int BN, int BKC, int WM, int WN, int MINW = 1>
+__global__ void __launch_bounds__(256, MINW) conv3x3_fwd_kernel(ConvFwdArgs a) {
     constexpr int BM = TH * TW, HWD = TW + 2, NHALO = (TH + 2) * HWD;
     constexpr int WTM = BM / WM, WTN = BN / WN, MT = WTM / 32, NT = WTN / 32;
     constexpr int AP = BKC + 4;  // +16 B per halo pixel: spreads ds_read_b128 over banks
@@ -438,31 +438,164 @@ __global__ void __launch_bounds__(256) conv3x3_wgrad_kernel(WgradArgs a) {
     if (do_db) a.dbpart[(size_t)split * a.Cout + co0 + tid] = dbacc;
 }
 
-// Fixed-order split-K reduction.  Block = 64 consecutive ci of one (t, co) row
-// x 4 split-groups; each thread sums every 4th split, then a 4-way LDS combine
-// (deterministic: the summation tree depends only on nsplit).
+// ---------------------------------------------------------------------------
+// Weight gradient for a narrow input (Cin <= 8: the RGB image padded to 8).
+// GEMM M = 64 co, N = (tap, ci) = 72 columns (3 MFMA column blocks of 32, last
+// partly padding), K = pixels.  3 waves, wave w owns column block w and both
+// 32-row co blocks over all k-steps (no cross-wave reduction).  Same partial
+// layout as the generic kernel, so the split-K reduce is shared.
+// ---------------------------------------------------------------------------
+template <int TH, int TW>
+__global__ void __launch_bounds__(192) conv3x3_wgrad_c8_kernel(WgradArgs a) {
+    constexpr int P = TH * TW, HWD = TW + 2, NHALO = (TH + 2) * HWD;
+    constexpr int NT = 192;
+    constexpr int DY_VEC = P * 16, X_VEC = NHALO * 2;
+    constexpr int DY_PER = (DY_VEC + NT - 1) / NT, X_PER = (X_VEC + NT - 1) / NT;
+    __shared__ __attribute__((aligned(16))) float smem[P * 64 + NHALO * 8];
+    float* dys = smem;
+    float* xs = smem + P * 64;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int NCO = a.Cout / 64;
+    const int nb = blockIdx.x % NCO, split = blockIdx.x / NCO;
+    const int co0 = nb * 64;
+    const int t_begin = split * a.tps, t_end = min(a.ntiles, t_begin + a.tps);
+    const int tpi = a.tiles_x * a.tiles_y;
+    const int Cs = a.C0;  // <= 8
+
+    // this lane's B column: j = 32*wave + (lane&31) -> (tap, ci); j >= 72 is padding
+    const int j = 32 * wave + (lane & 31);
+    const bool jvalid = j < 72;
+    const int jt = jvalid ? j / 8 : 0, jc = j % 8;
+    const int joff = ((jt / 3) * HWD + (jt % 3)) * 8 + jc;
+
+    f32x4 rdy[DY_PER], rx[X_PER];
+    unsigned xvalid = 0;
+    auto gload = [&](int tile) {
+        const int b = tile / tpi, trem = tile % tpi;
+        const int ty0 = (trem / a.tiles_x) * TH, tx0 = (trem % a.tiles_x) * TW;
+#pragma unroll
+        for (int v = 0; v < DY_PER; ++v) {
+            const int idx = tid + v * NT;
+            f32x4 val = {0.f, 0.f, 0.f, 0.f};
+            if (idx < DY_VEC) {
+                const int p = idx >> 4, q = idx & 15;
+                const int gy = ty0 + p / TW, gx = tx0 + p % TW;
+                if (gy < a.H && gx < a.W)
+                    val = *reinterpret_cast<const f32x4*>(
+                        a.dy + ((size_t)(b * a.H + gy) * a.W + gx) * a.Cout + co0 + q * 4);
+            }
+            rdy[v] = val;
+        }
+        xvalid = 0;
+#pragma unroll
+        for (int v = 0; v < X_PER; ++v) {
+            const int idx = tid + v * NT;
+            f32x4 val = {0.f, 0.f, 0.f, 0.f};
+            if (idx < X_VEC) {
+                const int hp = idx >> 1, q = idx & 1;
+                const int gy = ty0 - 1 + hp / HWD, gx = tx0 - 1 + hp % HWD;
+                if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W && q * 4 < Cs) {
+                    val = *reinterpret_cast<const f32x4*>(
+                        a.src0 + ((size_t)(b * a.H + gy) * a.W + gx) * Cs + q * 4);
+                    xvalid |= 1u << v;
+                }
+            }
+            rx[v] = val;
+        }
+    };
+    auto lstore = [&]() {
+#pragma unroll
+        for (int v = 0; v < DY_PER; ++v) {
+            const int idx = tid + v * NT;
+            if (idx < DY_VEC) *reinterpret_cast<f32x4*>(&dys[idx * 4]) = rdy[v];
+        }
+#pragma unroll
+        for (int v = 0; v < X_PER; ++v) {
+            const int idx = tid + v * NT;
+            if (idx < X_VEC) {
+                f32x4 val = rx[v];
+                if ((xvalid >> v) & 1u) val = act_apply4(val, a.sc0, a.sh0, (idx & 1) * 4);
+                *reinterpret_cast<f32x4*>(&xs[idx * 4]) = val;
+            }
+        }
+    };
+
+    f32x16 acc0, acc1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0.f;
+    if (t_begin < t_end) gload(t_begin);
+    for (int tile = t_begin; tile < t_end; ++tile) {
+        __syncthreads();
+        lstore();
+        __syncthreads();
+        if (tile + 1 < t_end) gload(tile + 1);
+#pragma unroll 4
+        for (int ks = 0; ks < P / 2; ++ks) {
+            const int p = 2 * ks + (lane >> 5);
+            const float a0 = dys[p * 64 + (lane & 31)];
+            const float a1 = dys[p * 64 + 32 + (lane & 31)];
+            const float bv = jvalid ? xs[((p / TW) * HWD + (p % TW)) * 8 + joff] : 0.f;
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, bv, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, bv, acc1, 0, 0, 0);
+        }
+    }
+    if (!jvalid || jc >= a.Cin) return;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int co = co0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        a.part[((size_t)(split * 9 + jt) * a.Cout + co) * a.Cin + jc] = acc0[r];
+        a.part[((size_t)(split * 9 + jt) * a.Cout + co + 32) * a.Cin + jc] = acc1[r];
+    }
+}
+
+// Fixed-order split-K reduction over the flat [9][Cout][Cin] partial slabs.
+// Block = 64 consecutive slab elements (16 lanes x float4) x 16 split-groups;
+// thread (g, l) sums splits g, g+16, ... in order, then a fixed 16-way LDS tree
+// (deterministic: the summation order depends only on nsplit).
+constexpr int WR_GROUPS = 16;
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* part, const float* dbpart,
                                                            int nsplit, int Cout, int Cin,
                                                            int Cin_real, float* dw, float* db,
                                                            int accumulate) {
-    __shared__ float red[4][64];
-    const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
-    const int ncb = (Cin_real + 63) / 64;
-    const int64_t rows = (int64_t)9 * Cout;
-    for (int64_t bi = blockIdx.x; bi < rows * ncb; bi += gridDim.x) {
-        const int64_t r = bi / ncb;  // (t, co)
-        const int ci = (int)(bi % ncb) * 64 + lane;
-        const int co = (int)(r % Cout), t = (int)(r / Cout);
-        float s = 0.f;
-        if (ci < Cin_real)
-            for (int k = grp; k < nsplit; k += 4)
-                s += part[((size_t)(k * 9 + t) * Cout + co) * Cin + ci];
-        red[grp][lane] = s;
+    __shared__ f32x4 red[WR_GROUPS][16];
+    const int l = threadIdx.x & 15, grp = threadIdx.x >> 4;
+    const int64_t slab = (int64_t)9 * Cout * Cin;  // multiple of 4 (Cin % 4 == 0)
+    const int64_t nvec = slab / 4;
+    for (int64_t v0 = (int64_t)blockIdx.x * 16; v0 < nvec; v0 += (int64_t)gridDim.x * 16) {
+        const int64_t v = v0 + l;
+        f32x4 s = {0.f, 0.f, 0.f, 0.f};
+        if (v < nvec) {
+            const f32x4* p = reinterpret_cast<const f32x4*>(part) + v;
+            int k = grp;
+            for (; k + 3 * WR_GROUPS < nsplit; k += 4 * WR_GROUPS) {
+                const f32x4 a0 = p[(size_t)k * nvec], a1 = p[(size_t)(k + WR_GROUPS) * nvec];
+                const f32x4 a2 = p[(size_t)(k + 2 * WR_GROUPS) * nvec];
+                const f32x4 a3 = p[(size_t)(k + 3 * WR_GROUPS) * nvec];
+                s += a0;
+                s += a1;
+                s += a2;
+                s += a3;
+            }
+            for (; k < nsplit; k += WR_GROUPS) s += p[(size_t)k * nvec];
+        }
+        red[grp][l] = s;
         __syncthreads();
-        if (grp == 0 && ci < Cin_real) {
-            s = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
-            const size_t o = ((size_t)co * Cin_real + ci) * 9 + t;
-            dw[o] = accumulate ? dw[o] + s : s;
+        if (threadIdx.x < 64) {
+            // 64 threads: element e = 4*l' + j of this block's 64-element run
+            const int lv = threadIdx.x >> 2, j = threadIdx.x & 3;
+            float acc = 0.f;
+#pragma unroll
+            for (int g = 0; g < WR_GROUPS; ++g) acc += red[g][lv][j];
+            const int64_t e = (v0 + lv) * 4 + j;
+            if (v0 + lv < nvec) {
+                const int ci = (int)(e % Cin);
+                const int64_t r = e / Cin;
+                const int co = (int)(r % Cout), t = (int)(r / Cout);
+                if (ci < Cin_real) {
+                    const size_t o = ((size_t)co * Cin_real + ci) * 9 + t;
+                    dw[o] = accumulate ? dw[o] + acc : acc;
+                }
+            }
         }
         __syncthreads();
     }
@@ -504,18 +637,25 @@ __global__ void pack_conv3x3_kernel(const float* w, float* wpk, int Cout, int Ci
 // ---------------------------------------------------------------------------
 namespace {
 
-enum FwdCfg { CFG_L = 0, CFG_W = 1, CFG_S = 2 };
+// (A CFG_W variant register-capped to 3 waves/SIMD spills 7 VGPRs and measured
+// 5-30% slower on every layer: 2 blocks/CU it is.)
+enum FwdCfg { CFG_L = 0, CFG_W = 1, CFG_S = 2, NUM_CFG = 3 };
 struct FwdShape {
     int th, tw, bn;
 };
-const FwdShape kFwd[3] = {{16, 16, 64}, {8, 16, 128}, {8, 8, 64}};
+const FwdShape kFwd[NUM_CFG] = {{16, 16, 64}, {8, 16, 128}, {8, 8, 64}};
 
 int64_t fwd_blocks(int cfg, int B, int H, int W, int Cout) {
     const FwdShape& s = kFwd[cfg];
     return (int64_t)B * cdiv(H, s.th) * cdiv(W, s.tw) * (Cout / s.bn);
 }
 
+int g_force_fwd_cfg = -1;  // tuning knob (ugpg_set_tuning("fwd_cfg", k)); -1 = heuristic
+
 int pick_fwd_cfg(int B, int H, int W, int Cout, int split) {
+    if (g_force_fwd_cfg >= 0 && g_force_fwd_cfg < NUM_CFG && Cout % kFwd[g_force_fwd_cfg].bn == 0 &&
+        split % kFwd[g_force_fwd_cfg].bn == 0)
+        return g_force_fwd_cfg;
     // prefer the larger tiles while they still give >= 2 blocks per CU; a block
     // must not straddle the output split (its BN must divide `split`)
     const int64_t want = 512;
@@ -552,17 +692,45 @@ WgradPlan wgrad_plan(int B, int H, int W, int Cin, int Cout) {
     return p;
 }
 
-template <int TH, int TW, int BN, int BKC, int WM, int WN>
+// Narrow-input wgrad (conv3x3_wgrad_c8_kernel): 8x16-pixel tiles, 4 blocks/CU by
+// LDS (38.5 KB) -> aim for 1024 blocks.
+constexpr int WG8_TH = 8, WG8_TW = 16;
+
+static bool wgrad_use_c8(int C0, int C1, const void* db) { return C1 == 0 && C0 <= 8 && !db; }
+
+WgradPlan wgrad_plan_c8(int B, int H, int W, int Cout) {
+    WgradPlan p;
+    p.tiles_x = (int)cdiv(W, WG8_TW);
+    p.tiles_y = (int)cdiv(H, WG8_TH);
+    p.ntiles = B * p.tiles_x * p.tiles_y;
+    int64_t ns = cdiv(1024, Cout / 64);
+    if (ns > p.ntiles) ns = p.ntiles;
+    if (ns < 1) ns = 1;
+    p.tps = (int)cdiv(p.ntiles, ns);
+    p.nsplit = (int)cdiv(p.ntiles, p.tps);
+    return p;
+}
+
+template <int TH, int TW, int BN, int BKC, int WM, int WN, int MINW = 1>
 void launch_fwd(const ConvFwdArgs& a, hipStream_t st) {
     const unsigned grid = (unsigned)((int64_t)a.ntiles * (a.Cout / BN));
-    hipLaunchKernelGGL((conv3x3_fwd_kernel<TH, TW, BN, BKC, WM, WN>), dim3(grid), dim3(256), 0, st,
-                       a);
+    hipLaunchKernelGGL((conv3x3_fwd_kernel<TH, TW, BN, BKC, WM, WN, MINW>), dim3(grid), dim3(256),
+                       0, st, a);
 }
 
 }  // namespace
 }  // namespace ugpg
 
 using namespace ugpg;
+
+extern "C" int ugpg_set_tuning(const char* key, int value) {
+    if (key && std::string(key) == "fwd_cfg") {
+        g_force_fwd_cfg = value;
+        return UGPG_OK;
+    }
+    set_error("set_tuning: unknown key '%s'", key ? key : "(null)");
+    return UGPG_ERR_INVALID;
+}
 
 extern "C" int ugpg_conv3x3_fwd_ntiles(int B, int H, int W, int Cin, int Cout) {
     (void)Cin;
@@ -665,8 +833,10 @@ static int wgrad_check(const ugpg_wgrad_t* p) {
 
 extern "C" size_t ugpg_conv3x3_wgrad_workspace(const ugpg_wgrad_t* p) {
     if (wgrad_check(p)) return 0;
-    const int Cin = p->src[0].C + (p->src[1].data ? p->src[1].C : 0);
-    WgradPlan w = wgrad_plan(p->B, p->H, p->W, Cin, p->Cout);
+    const int C0 = p->src[0].C, C1 = p->src[1].data ? p->src[1].C : 0;
+    const int Cin = C0 + C1;
+    WgradPlan w = wgrad_use_c8(C0, C1, p->db) ? wgrad_plan_c8(p->B, p->H, p->W, p->Cout)
+                                              : wgrad_plan(p->B, p->H, p->W, Cin, p->Cout);
     return ((size_t)w.nsplit * 9 * p->Cout * Cin + (size_t)w.nsplit * p->Cout) * sizeof(float);
 }
 
@@ -675,7 +845,9 @@ extern "C" int ugpg_conv3x3_wgrad(const ugpg_wgrad_t* p, void* ws, size_t ws_byt
     if (int e = wgrad_check(p)) return e;
     const int C0 = p->src[0].C, C1 = p->src[1].data ? p->src[1].C : 0;
     const int Cin = C0 + C1;
-    WgradPlan w = wgrad_plan(p->B, p->H, p->W, Cin, p->Cout);
+    const bool c8 = wgrad_use_c8(C0, C1, p->db);
+    WgradPlan w = c8 ? wgrad_plan_c8(p->B, p->H, p->W, p->Cout)
+                     : wgrad_plan(p->B, p->H, p->W, Cin, p->Cout);
     const size_t need = ugpg_conv3x3_wgrad_workspace(p);
     if (!ws || ws_bytes < need) {
         set_error("conv3x3_wgrad: workspace %zu < %zu", ws_bytes, need);
@@ -704,11 +876,17 @@ extern "C" int ugpg_conv3x3_wgrad(const ugpg_wgrad_t* p, void* ws, size_t ws_byt
     a.nsplit = w.nsplit;
     a.tps = w.tps;
     hipStream_t st = as_stream(stream);
-    const unsigned grid = (unsigned)((p->Cout / 64) * cdiv(Cin, 64) * w.nsplit);
-    hipLaunchKernelGGL((conv3x3_wgrad_kernel<WG_TH, WG_TW>), dim3(grid), dim3(256), 0, st, a);
+    if (c8) {
+        const unsigned grid = (unsigned)((p->Cout / 64) * w.nsplit);
+        hipLaunchKernelGGL((conv3x3_wgrad_c8_kernel<WG8_TH, WG8_TW>), dim3(grid), dim3(192), 0, st,
+                           a);
+    } else {
+        const unsigned grid = (unsigned)((p->Cout / 64) * cdiv(Cin, 64) * w.nsplit);
+        hipLaunchKernelGGL((conv3x3_wgrad_kernel<WG_TH, WG_TW>), dim3(grid), dim3(256), 0, st, a);
+    }
     if (int e = check_launch("conv3x3_wgrad")) return e;
     const int Cr = p->Cin_real > 0 ? p->Cin_real : Cin;
-    int64_t rblocks = (int64_t)9 * p->Cout * cdiv(Cr, 64);
+    int64_t rblocks = cdiv((int64_t)9 * p->Cout * Cin / 4, 16);
     if (rblocks > 4096) rblocks = 4096;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)rblocks), dim3(256), 0, st, a.part,
                        a.dbpart, w.nsplit, p->Cout, Cin, Cr, p->dw, p->db, p->accumulate);

@@ -403,14 +403,33 @@ __device__ __forceinline__ double block_tree_sum(double v) {
 }
 
 // one block per output element (nc*(C+1) of them)
-__global__ void __launch_bounds__(256) head_bwd_finalize_kernel(const float* part, int nblk, int nc,
-                                                                int C, float* dw, float* db) {
+// Block = 64 consecutive outputs x 16 partial-groups (coalesced along the
+// outputs); thread (g, l) sums partial blocks g, g+16, ... then a fixed 16-way
+// combine.
+__global__ void __launch_bounds__(1024) head_bwd_finalize_kernel(const float* part, int nblk, int nc,
+                                                                 int C, float* dw, float* db) {
+    __shared__ double red[16][64];
     const int total = nc * (C + 1);
-    const int e = blockIdx.x;
+    const int l = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int e = blockIdx.x * 64 + l;
     double s = 0;
-    for (int i = threadIdx.x; i < nblk; i += 256) s += part[(size_t)i * total + e];
-    s = block_tree_sum(s);
-    if (threadIdx.x == 0) {
+    if (e < total) {
+        int i = g;
+        for (; i + 48 < nblk; i += 64) {
+            const float a0 = part[(size_t)i * total + e], a1 = part[(size_t)(i + 16) * total + e];
+            const float a2 = part[(size_t)(i + 32) * total + e];
+            const float a3 = part[(size_t)(i + 48) * total + e];
+            s += a0;
+            s += a1;
+            s += a2;
+            s += a3;
+        }
+        for (; i < nblk; i += 16) s += part[(size_t)i * total + e];
+    }
+    red[g][l] = s;
+    __syncthreads();
+    if (g == 0 && e < total) {
+        for (int q = 1; q < 16; ++q) s += red[q][l];
         const int k = e / (C + 1), c = e % (C + 1);
         if (c < C) dw[(size_t)k * C + c] = (float)s;
         else if (db) db[k] = (float)s;
@@ -901,7 +920,7 @@ extern "C" int ugpg_head_bwd(ugpg_src_t s, int64_t npix, const float* w, int nc,
     hipLaunchKernelGGL(head_bwd_kernel, dim3(nblk), dim3(256), 0, st, s.data, s.scale, s.shift,
                        npix, s.C, w, nc, dh, da, acc_da, ppb, static_cast<float*>(ws), nblk);
     if (int e = check_launch("head_bwd")) return e;
-    hipLaunchKernelGGL(head_bwd_finalize_kernel, dim3(nc * (s.C + 1)), dim3(256), 0,
+    hipLaunchKernelGGL(head_bwd_finalize_kernel, dim3((unsigned)cdiv(nc * (s.C + 1), 64)), dim3(1024), 0,
                        st, static_cast<const float*>(ws), nblk, nc, s.C, dw, db);
     return check_launch("head_bwd_finalize");
 }

@@ -38,6 +38,7 @@ class WgradDesc(C.Structure):
 SIGNATURES = {
     "ugpg_version": (C.c_char_p, []),
     "ugpg_last_error": (C.c_char_p, []),
+    "ugpg_set_tuning": (_i, [C.c_char_p, _i]),
     "ugpg_conv3x3_fwd": (_i, [C.POINTER(ConvDesc), _p]),
     "ugpg_conv3x3_fwd_ntiles": (_i, [_i, _i, _i, _i, _i]),
     "ugpg_pack_conv3x3": (_i, [_p, _p, _i, _i, _i, _i, _p]),
