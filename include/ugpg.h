@@ -50,7 +50,13 @@ typedef struct {
 } ugpg_src_t;
 
 /* ---- 3x3 convolution, padding 1, stride 1 (UG_unet_parts.py:10,13) ---------
- * Implicit GEMM on v_mfma_f32_32x32x2_f32 with LDS-staged halo tiles.
+ * Implicit GEMM with LDS-staged halo tiles, in one of two fp32-accurate
+ * arithmetic forms selected by the weight pack format `wfmt`:
+ *   UGPG_WFMT_F32: v_mfma_f32_32x32x2_f32 (exact fp32 FMA chains);
+ *   UGPG_WFMT_X6:  split-bf16 -- every operand split exactly into 3 bf16 pieces,
+ *                  6 v_mfma_f32_32x32x16_bf16 products per k-step with fp32
+ *                  accumulation (product error < 2^-25 relative, below one fp32
+ *                  rounding); needs K channels % 16 == 0 and N % 64 == 0.
  * Input = channel-concat of src[0] and src[1] (src[1].data may be NULL):
  * this is the concat-free `torch.cat([x2, x1], dim=1)` of Up (UG_unet_parts.py:80).
  * Cin = src[0].C + src[1].C must be a multiple of 8 (pad the image to 8 channels).
@@ -62,28 +68,35 @@ typedef struct {
 typedef struct {
     int B, H, W;
     ugpg_src_t src[2];
-    const float* wpk;      /* packed by ugpg_pack_conv3x3 */
+    const void* wpk;       /* packed by ugpg_pack_conv3x3 in format wfmt */
     const float* bias;     /* [Cout] or NULL */
     int Cout;
     float* out[2];
     int out_split;
     int accumulate[2];
     float* stats;
+    int wfmt;              /* UGPG_WFMT_F32 or UGPG_WFMT_X6 */
 } ugpg_conv_t;
+
+#define UGPG_WFMT_F32 0
+#define UGPG_WFMT_X6 1
 
 /* Replaces aten::convolution forward (cuDNN/oneDNN) for DoubleConv's 3x3 convs. */
 int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream);
 /* number of BatchNorm partial tiles the forward writes (size stats as 3*Cout*ntiles) */
-int ugpg_conv3x3_fwd_ntiles(int B, int H, int W, int Cin, int Cout);
+int ugpg_conv3x3_fwd_ntiles(int B, int H, int W, int Cin, int Cout, int wfmt);
 
 /* Weight repack from OIHW fp32 [Cout][Cin][3][3].
- *  mode 0 (forward):  wpk[Cin_pad/8][9][Cout][8],    wpk = W[co][ci][t]
- *  mode 1 (dgrad):    wpk[Cout/8][9][Cin_pad][8],    wpk = W[co][ci][8-t]
+ *  mode 0 (forward):  N = Cout, K = Cin_pad, wpk = W[co][ci][t]
+ *  mode 1 (dgrad):    N = Cin_pad, K = Cout,  wpk = W[co][ci][8-t]
  *    (the data-gradient of a 3x3/p1 conv is the forward conv of dY with the
  *     180-degree-rotated, channel-transposed kernel; replaces aten
- *     convolution_backward's grad_input) */
-int ugpg_pack_conv3x3(const float* w_oihw, float* wpk, int Cout, int Cin, int Cin_pad,
-                      int mode, void* stream);
+ *     convolution_backward's grad_input)
+ *  wfmt F32: fp32 [K/8][9][N][8];  wfmt X6: bf16 [N/64][K/16][3 pieces][2][9][64][8]
+ *  ugpg_pack_conv3x3_bytes gives the size of wpk. */
+size_t ugpg_pack_conv3x3_bytes(int Cout, int Cin_pad, int wfmt);
+int ugpg_pack_conv3x3(const float* w_oihw, void* wpk, int Cout, int Cin, int Cin_pad,
+                      int mode, int wfmt, void* stream);
 
 /* Weight gradient (aten convolution_backward grad_weight/grad_bias, K3):
  *   dw[co][ci][ky][kx] (+)= sum_p dy[p][co] * act(x)[p + (ky-1,kx-1)][ci]
@@ -99,6 +112,8 @@ typedef struct {
     int Cin_real;
     float* db;             /* [Cout] or NULL */
     int accumulate;
+    int math;              /* UGPG_WFMT_X6: split-bf16 MFMA where the shape allows
+                              (db == NULL, 64-channel sources); else fp32 MFMA */
 } ugpg_wgrad_t;
 size_t ugpg_conv3x3_wgrad_workspace(const ugpg_wgrad_t* p);
 int ugpg_conv3x3_wgrad(const ugpg_wgrad_t* p, void* ws, size_t ws_bytes, void* stream);

@@ -44,7 +44,12 @@ def perturbed_state(state, seed, rel=1e-7):
     return out
 
 
-FLOOR_PERTURBATIONS = ((7, 1e-7), (8, 1e-7), (9, 1e-7), (10, 1e-6), (11, 1e-6))
+# the 5e-6 level matches the measured forward deviation of deep layers of ANY fp32
+# evaluation order vs fp64 (tools/debug_parity.py: 3-7e-6 relative at down4/up1
+# for both the fp32-MFMA and the split-bf16 conv), so the floor covers the
+# ReLU/argmax near-tie flips such a deviation triggers
+FLOOR_PERTURBATIONS = ((7, 1e-7), (8, 1e-7), (9, 1e-7), (10, 1e-6), (11, 1e-6), (12, 5e-6),
+                       (13, 5e-6))
 
 
 def noise_floor(stage, state, x, t, g32, g64, umap=None, alpha=1.0, seeds=FLOOR_PERTURBATIONS):

@@ -46,7 +46,7 @@ def test_library_is_gfx950_code():
 def test_invalid_arguments_fail_loudly_without_gpu():
     """Argument validation runs on the host and reports through ugpg_last_error."""
     from ugpg import _C
-    rc = _C.lib.ugpg_pack_conv3x3(None, None, 64, 3, 1, 0, None)
+    rc = _C.lib.ugpg_pack_conv3x3(None, None, 64, 3, 1, 0, 0, None)
     assert rc == -1
     assert b"pack_conv3x3" in _C.lib.ugpg_last_error()
 

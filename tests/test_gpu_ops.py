@@ -51,12 +51,24 @@ CONV_CASES = [
     (2, 256, 256, 64, 64, 64, True),   # Up4-shaped: concat dgrad must not straddle the split
     (4, 256, 256, 8, 0, 64, False),    # Inc-shaped image layer: narrow-input wgrad, many splits
     (3, 40, 24, 8, 0, 128, True),      # ragged 8x16 wgrad tiles, 2 co blocks, lazy affine
+    (2, 4, 4, 512, 0, 512, True),      # Down4 of a 64^2 stage: 4x4 image in a 8x16 tile
+    (2, 8, 8, 256, 256, 256, True),    # Up1 of a 64^2 stage
 ]
 BIG = {5, 6, 7}
 
 
+@pytest.fixture(params=["x6", "f32"])
+def math(request):
+    """Both conv arithmetic forms: split-bf16 (default) and fp32 MFMA."""
+    from ugpg import ops
+    old = ops.conv_math()
+    ops.set_conv_math(request.param)
+    yield request.param
+    ops.set_conv_math(old)
+
+
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv3x3_fwd_stats(dev, case):
+def test_conv3x3_fwd_stats(dev, case, math):
     from ugpg import ops
     B, H, W, C0, C1, Cout, affine = case
     cin = C0 + C1
@@ -80,7 +92,8 @@ def test_conv3x3_fwd_stats(dev, case):
         srcs.append(ops.Act(nhwc(x1).to(dev), g(sc1), g(sh1)))
     wpk = ops.pack_conv3x3(w.to(dev), cin, 0)
     out = torch.empty(B, H, W, Cout, device=dev)
-    nt = ops.conv_ntiles(B, H, W, cin, Cout)
+    assert wpk.ugpg_fmt == (ops.WFMT_X6 if math == "x6" and cin % 16 == 0 else ops.WFMT_F32)
+    nt = ops.conv_ntiles(B, H, W, cin, Cout, wpk)
     stats = torch.empty(3 * Cout * nt, device=dev)
     ops.conv3x3_fwd(srcs, wpk, b.to(dev), Cout, [out], stats=stats)
     close(nchw(out.cpu()), ref, 2e-5, "conv fwd")
@@ -101,7 +114,7 @@ def test_conv3x3_fwd_stats(dev, case):
 
 
 @pytest.mark.parametrize("case", CONV_CASES[:5] + CONV_CASES[7:])
-def test_conv3x3_dgrad_wgrad(dev, case):
+def test_conv3x3_dgrad_wgrad(dev, case, math):
     from ugpg import ops
     B, H, W, C0, C1, Cout, affine = case
     cin = C0 + C1
@@ -145,11 +158,36 @@ def test_conv3x3_dgrad_wgrad(dev, case):
     ops.conv3x3_wgrad(srcs, nhwc(dy).to(dev), dw, db, cin_real)
     close(dw.cpu(), wd.grad, 2e-5, "wgrad")
     close(db.cpu(), bd.grad, 2e-5, "bias grad")
-    if cin <= 8:
-        # without a bias grad the narrow-input kernel (conv3x3_wgrad_c8_kernel) runs
-        dw8 = torch.empty(Cout, cin_real, 3, 3, device=dev)
-        ops.conv3x3_wgrad(srcs, nhwc(dy).to(dev), dw8, None, cin_real)
-        close(dw8.cpu(), wd.grad, 2e-5, "wgrad (narrow input)")
+    # without a bias grad (the model's call): the narrow-input kernel for the image
+    # layer, the split-bf16 kernel for 64-channel sources under math "x6"
+    dw2 = torch.empty(Cout, cin_real, 3, 3, device=dev)
+    ops.conv3x3_wgrad(srcs, nhwc(dy).to(dev), dw2, None, cin_real)
+    close(dw2.cpu(), wd.grad, 2e-5, f"wgrad without db ({math})")
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 64, 64, 64), (2, 32, 32, 512, 512), (2, 16, 16, 256, 128)])
+def test_conv_x6_is_fp32_class(dev, shape):
+    """The split-bf16 form must be as accurate as fp32 MFMA: error vs an fp64
+    reference (max and RMS over the output) within 1.5x of the fp32 path's."""
+    from ugpg import ops
+    B, H, W, cin, cout = shape
+    x = rnd((B, cin, H, W), 31, "x")
+    w = rnd((cout, cin, 3, 3), 32, "w", 1.0 / (3 * cin ** 0.5))
+    ref = F.conv2d(x.double(), w.double(), None, padding=1)
+    errs = {}
+    old = ops.conv_math()
+    try:
+        for m in ("x6", "f32"):
+            ops.set_conv_math(m)
+            wpk = ops.pack_conv3x3(w.to(dev), cin, 0)
+            out = torch.empty(B, H, W, cout, device=dev)
+            ops.conv3x3_fwd([ops.Act(nhwc(x).to(dev))], wpk, None, cout, [out])
+            d = nchw(out.cpu()).double() - ref
+            errs[m] = (d.abs().max().item(), d.pow(2).mean().sqrt().item())
+    finally:
+        ops.set_conv_math(old)
+    print("conv error vs fp64 (max, rms):", errs)
+    assert errs["x6"][0] <= 1.5 * errs["f32"][0] and errs["x6"][1] <= 1.5 * errs["f32"][1], errs
 
 
 @pytest.mark.parametrize("C,npix", [(64, 5000), (512, 300), (128, 70000)])

@@ -42,7 +42,8 @@ def timeit(fn, iters=5):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--cfgs", default="-1,0,1,2")
+    ap.add_argument("--cfgs", default="-1", help="fp32 tile configs (-1 = heuristic)")
+    ap.add_argument("--maths", default="x6,f32")
     ap.add_argument("--wgrad", action="store_true")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
@@ -56,33 +57,42 @@ def main():
         if C1:
             srcs.append(ops.Act(torch.randn(B, H, H, C1, device=dev)))
         w = torch.randn(Cout, real_cin, 3, 3, device=dev) * 0.05
-        wpk = ops.pack_conv3x3(w, cin, 0)
         out = torch.empty(B, H, H, Cout, device=dev)
         bias = torch.zeros(Cout, device=dev)
         flops = 2.0 * B * H * H * Cout * 9 * real_cin
         fns = {}
-        for c in cfgs:
-            def f(c=c):
-                lib.ugpg_set_tuning(b"fwd_cfg", c)
-                nt = ops.conv_ntiles(B, H, H, cin, Cout)
-                st = torch.empty(3 * Cout * nt, device=dev)
-                ops.conv3x3_fwd(srcs, wpk, bias, Cout, [out], stats=st)
-            fns[f"fwd{c}"] = f
-        if real_cin % 64 == 0:
-            dy = torch.randn(B, H, H, Cout, device=dev)
-            wpk1 = ops.pack_conv3x3(w, real_cin, 1)
-            d0 = torch.empty(B, H, H, C0, device=dev)
-            d1 = torch.empty(B, H, H, C1, device=dev) if C1 else None
-            for c in cfgs:
-                def g(c=c):
+        for m in a.maths.split(","):
+            ops.set_conv_math(m)
+            wpk = ops.pack_conv3x3(w, cin, 0)
+            wpk1 = ops.pack_conv3x3(w, real_cin, 1) if real_cin % 64 == 0 else None
+            nt = ops.conv_ntiles(B, H, H, cin, Cout, wpk)
+            st = torch.empty(3 * Cout * nt, device=dev)
+            for c in (cfgs if m == "f32" else [-1]):
+                tag = m if c == -1 else f"{m}{c}"
+
+                def f(c=c, wpk=wpk, st=st):
                     lib.ugpg_set_tuning(b"fwd_cfg", c)
-                    ops.conv3x3_fwd([ops.Act(dy)], wpk1, None, real_cin, [d0, d1] if C1 else [d0],
-                                    split=C0 if C1 else None)
-                fns[f"dgrad{c}"] = g
+                    ops.conv3x3_fwd(srcs, wpk, bias, Cout, [out], stats=st)
+                fns[f"fwd_{tag}"] = f
+                if wpk1 is not None:
+                    dy = torch.randn(B, H, H, Cout, device=dev)
+                    d0 = torch.empty(B, H, H, C0, device=dev)
+                    d1 = torch.empty(B, H, H, C1, device=dev) if C1 else None
+
+                    def g(c=c, wpk1=wpk1, dy=dy, d0=d0, d1=d1):
+                        lib.ugpg_set_tuning(b"fwd_cfg", c)
+                        ops.conv3x3_fwd([ops.Act(dy)], wpk1, None, real_cin,
+                                        [d0, d1] if C1 else [d0], split=C0 if C1 else None)
+                    fns[f"dgrad_{tag}"] = g
+        ops.set_conv_math("x6")
         if a.wgrad:
             dy = torch.randn(B, H, H, Cout, device=dev)
             dw = torch.empty_like(w)
-            fns["wgrad"] = lambda: ops.conv3x3_wgrad(srcs, dy, dw, None, real_cin)
+            for m in a.maths.split(","):
+                def wg(m=m):
+                    ops.set_conv_math(m)
+                    ops.conv3x3_wgrad(srcs, dy, dw, None, real_cin)
+                fns[f"wgrad_{m}"] = wg
         res = {k: [] for k in fns}
         for _ in range(a.rounds):
             for k, f in fns.items():
@@ -91,6 +101,7 @@ def main():
                 except RuntimeError as e:
                     res[k].append(float("nan"))
         lib.ugpg_set_tuning(b"fwd_cfg", -1)
+        ops.set_conv_math("x6")
         rows[name] = {k: (min(v), flops / (min(v) * 1e-3) / 1e12) for k, v in res.items()}
         print(name, " ".join(f"{k}={v[0]:.3f}ms/{v[1]:.0f}TF" for k, v in rows[name].items()),
               flush=True)

@@ -16,28 +16,10 @@
 // MFMA k-permutation: lane l (h = l>>5) feeds k-slot h of step s with input channel
 // 8g + 4h + s for both operands, so each lane's 4 consecutive channels come from one
 // 16-byte ds_read_b128 for A and one for B.
-#include "common.h"
+#include "conv_common.h"
 
 namespace ugpg {
 
-struct ConvFwdArgs {
-    const float* src0;
-    const float* sc0;
-    const float* sh0;
-    int C0;
-    const float* src1;
-    const float* sc1;
-    const float* sh1;
-    int C1;
-    const float* wpk;
-    const float* bias;
-    float* out0;
-    float* out1;
-    int split, acc0, acc1;
-    float* stats;
-    int B, H, W, Cin, Cout;
-    int tiles_x, tiles_y, ntiles;
-};
 
 template <int TH, int TW, int BN, int BKC, int WM, int WN, int MINW = 1>
 __global__ void __launch_bounds__(256, MINW) conv3x3_fwd_kernel(ConvFwdArgs a) {
@@ -90,7 +72,7 @@ __global__ void __launch_bounds__(256, MINW) conv3x3_fwd_kernel(ConvFwdArgs a) {
             }
             ra[v] = val;
         }
-        const float* wsrc = a.wpk + (size_t)c * G * 9 * a.Cout * 8;
+        const float* wsrc = static_cast<const float*>(a.wpk) + (size_t)c * G * 9 * a.Cout * 8;
 #pragma unroll
         for (int v = 0; v < B_PER; ++v) {
             const int idx = tid + v * 256;
@@ -186,92 +168,7 @@ __global__ void __launch_bounds__(256, MINW) conv3x3_fwd_kernel(ConvFwdArgs a) {
         }
     }
 
-    // ---- epilogue: bias, store, BatchNorm partials ----
-    const int vh = min(TH, a.H - ty0), vw = min(TW, a.W - tx0);
-    float* out;
-    int ostride, ocol0, oacc;
-    if (n0 < a.split) {
-        out = a.out0;
-        ostride = a.split;
-        ocol0 = n0;
-        oacc = a.acc0;
-    } else {
-        out = a.out1;
-        ostride = a.Cout - a.split;
-        ocol0 = n0 - a.split;
-        oacc = a.acc1;
-    }
-    float psum[NT];
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-        const int nl = wn * WTN + nt * 32 + (lane & 31);
-        const float bv = a.bias ? a.bias[n0 + nl] : 0.f;
-        psum[nt] = 0.f;
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = wm * WTM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                const int py = m / TW, px = m % TW;
-                const float v = acc[mt][nt][r] + bv;
-                acc[mt][nt][r] = v;
-                if (py < vh && px < vw) {
-                    const size_t o =
-                        ((size_t)(b * a.H + ty0 + py) * a.W + tx0 + px) * ostride + ocol0 + nl;
-                    out[o] = oacc ? out[o] + v : v;
-                    psum[nt] += v;
-                }
-            }
-    }
-    if (a.stats == nullptr) return;
-    float* red = smem;            // [WM][BN]
-    float* tot = smem + WM * BN;  // [BN]
-    const float cnt = (float)(vh * vw);
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-        const float s = psum[nt] + __shfl_xor(psum[nt], 32, 64);
-        if (lane < 32) red[wm * BN + wn * WTN + nt * 32 + lane] = s;
-    }
-    __syncthreads();
-    if (tid < BN) {
-        float s = 0.f;
-#pragma unroll
-        for (int w = 0; w < WM; ++w) s += red[w * BN + tid];
-        tot[tid] = s;
-    }
-    __syncthreads();
-    float pq[NT];
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-        const int nl = wn * WTN + nt * 32 + (lane & 31);
-        const float mu = tot[nl] / cnt;
-        float q = 0.f;
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = wm * WTM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                if (m / TW < vh && m % TW < vw) {
-                    const float d = acc[mt][nt][r] - mu;
-                    q = fmaf(d, d, q);
-                }
-            }
-        pq[nt] = q + __shfl_xor(q, 32, 64);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
-        if (lane < 32) red[wm * BN + wn * WTN + nt * 32 + lane] = pq[nt];
-    __syncthreads();
-    if (tid < BN) {
-        float q = 0.f;
-#pragma unroll
-        for (int w = 0; w < WM; ++w) q += red[w * BN + tid];
-        const size_t n = n0 + tid, T = a.ntiles;
-        a.stats[(0 * (size_t)a.Cout + n) * T + tile] = cnt;
-        a.stats[(1 * (size_t)a.Cout + n) * T + tile] = tot[tid];
-        a.stats[(2 * (size_t)a.Cout + n) * T + tile] = q;
-    }
+    conv_epilogue<TH, TW, BN, WM, WN, MT, NT, false>(a, acc, smem, tile, b, ty0, tx0, n0, wm, wn);
 }
 
 // ---------------------------------------------------------------------------
@@ -280,22 +177,6 @@ __global__ void __launch_bounds__(256, MINW) conv3x3_fwd_kernel(ConvFwdArgs a) {
 // tiles of one split.  Operands from LDS: dy tile [P][64], activated input halo
 // [(TH+2)(TW+2)][64]; one MFMA k-step = 2 pixels.
 // ---------------------------------------------------------------------------
-struct WgradArgs {
-    const float* src0;
-    const float* sc0;
-    const float* sh0;
-    int C0;
-    const float* src1;
-    const float* sc1;
-    const float* sh1;
-    int C1;
-    const float* dy;
-    int Cout, Cin;
-    float* part;
-    float* dbpart;
-    int B, H, W;
-    int tiles_x, tiles_y, ntiles, nsplit, tps;
-};
 
 template <int TH, int TW>
 __global__ void __launch_bounds__(256) conv3x3_wgrad_kernel(WgradArgs a) {
@@ -671,10 +552,10 @@ struct WgradPlan {
     int tiles_x, tiles_y, ntiles, nsplit, tps;
 };
 
-WgradPlan wgrad_plan(int B, int H, int W, int Cin, int Cout) {
+WgradPlan wgrad_plan(int B, int H, int W, int Cin, int Cout, int th = WG_TH, int tw = WG_TW) {
     WgradPlan p;
-    p.tiles_x = (int)cdiv(W, WG_TW);
-    p.tiles_y = (int)cdiv(H, WG_TH);
+    p.tiles_x = (int)cdiv(W, tw);
+    p.tiles_y = (int)cdiv(H, th);
     p.ntiles = B * p.tiles_x * p.tiles_y;
     const int64_t base = (int64_t)(Cout / 64) * cdiv(Cin, 64);
     // 2 co-resident blocks per CU (232 VGPR+AGPR, 44 KB LDS): aim for a multiple of 512
@@ -732,8 +613,10 @@ extern "C" int ugpg_set_tuning(const char* key, int value) {
     return UGPG_ERR_INVALID;
 }
 
-extern "C" int ugpg_conv3x3_fwd_ntiles(int B, int H, int W, int Cin, int Cout) {
+extern "C" int ugpg_conv3x3_fwd_ntiles(int B, int H, int W, int Cin, int Cout, int wfmt) {
     (void)Cin;
+    if (wfmt == UGPG_WFMT_X6)
+        return (int)(B * cdiv(H, fwd_x6_tile_h(W)) * cdiv(W, fwd_x6_tile_w(W)));
     const int cfg = pick_fwd_cfg(B, H, W, Cout, Cout);
     return (int)(B * cdiv(H, kFwd[cfg].th) * cdiv(W, kFwd[cfg].tw));
 }
@@ -752,6 +635,14 @@ extern "C" int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream) {
     if (p->out_split <= 0 || p->out_split > p->Cout || p->out_split % 64 ||
         (p->out_split < p->Cout && !p->out[1])) {
         set_error("conv3x3_fwd: bad out_split %d (Cout %d)", p->out_split, p->Cout);
+        return UGPG_ERR_INVALID;
+    }
+    if (p->wfmt != UGPG_WFMT_F32 && p->wfmt != UGPG_WFMT_X6) {
+        set_error("conv3x3_fwd: unknown weight format %d", p->wfmt);
+        return UGPG_ERR_INVALID;
+    }
+    if (p->wfmt == UGPG_WFMT_X6 && (C0 % 16 || C1 % 16)) {
+        set_error("conv3x3_fwd: split-bf16 path needs 16-channel sources (C0=%d C1=%d)", C0, C1);
         return UGPG_ERR_INVALID;
     }
     ConvFwdArgs a;
@@ -776,6 +667,14 @@ extern "C" int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream) {
     a.W = p->W;
     a.Cin = Cin;
     a.Cout = p->Cout;
+    hipStream_t st = as_stream(stream);
+    if (p->wfmt == UGPG_WFMT_X6) {
+        a.tiles_x = (int)cdiv(p->W, fwd_x6_tile_w(p->W));
+        a.tiles_y = (int)cdiv(p->H, fwd_x6_tile_h(p->W));
+        a.ntiles = p->B * a.tiles_x * a.tiles_y;
+        launch_fwd_x6(a, st);
+        return check_launch("conv3x3_fwd_x6");
+    }
     const int cfg = pick_fwd_cfg(p->B, p->H, p->W, p->Cout, p->out_split);
     if (p->out_split % kFwd[cfg].bn) {
         set_error("conv3x3_fwd: out_split %d not a multiple of the tile width %d", p->out_split,
@@ -787,7 +686,6 @@ extern "C" int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream) {
     a.tiles_x = (int)cdiv(p->W, s.tw);
     a.tiles_y = (int)cdiv(p->H, s.th);
     a.ntiles = p->B * a.tiles_x * a.tiles_y;
-    hipStream_t st = as_stream(stream);
     switch (cfg) {
         case CFG_L:
             if (bk16) launch_fwd<16, 16, 64, 16, 4, 1>(a, st);
@@ -804,17 +702,32 @@ extern "C" int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream) {
     return check_launch("conv3x3_fwd");
 }
 
-extern "C" int ugpg_pack_conv3x3(const float* w, float* wpk, int Cout, int Cin, int Cin_pad,
-                                 int mode, void* stream) {
+extern "C" size_t ugpg_pack_conv3x3_bytes(int Cout, int Cin_pad, int wfmt) {
+    const size_t n = (size_t)Cin_pad * 9 * Cout;
+    return wfmt == UGPG_WFMT_X6 ? n * 3 * 2 : n * 4;
+}
+
+extern "C" int ugpg_pack_conv3x3(const float* w, void* wpk, int Cout, int Cin, int Cin_pad,
+                                 int mode, int wfmt, void* stream) {
     if (!w || !wpk || Cin_pad < Cin || Cin_pad % 8 || (mode == 1 && Cout % 8) || mode < 0 ||
-        mode > 1) {
-        set_error("pack_conv3x3: bad arguments (Cout=%d Cin=%d Cin_pad=%d mode=%d)", Cout, Cin,
-                  Cin_pad, mode);
+        mode > 1 || (wfmt != UGPG_WFMT_F32 && wfmt != UGPG_WFMT_X6)) {
+        set_error("pack_conv3x3: bad arguments (Cout=%d Cin=%d Cin_pad=%d mode=%d wfmt=%d)", Cout,
+                  Cin, Cin_pad, mode, wfmt);
         return UGPG_ERR_INVALID;
+    }
+    if (wfmt == UGPG_WFMT_X6) {
+        const int N = mode == 0 ? Cout : Cin_pad, K = mode == 0 ? Cin_pad : Cout;
+        if (N % 64 || K % 16) {
+            set_error("pack_conv3x3: split-bf16 format needs N %% 64 == 0 and K %% 16 == 0 "
+                      "(N=%d K=%d)", N, K);
+            return UGPG_ERR_INVALID;
+        }
+        launch_pack_x6(w, wpk, Cout, Cin, Cin_pad, mode, as_stream(stream));
+        return check_launch("pack_conv3x3_x6");
     }
     const int64_t total = (int64_t)Cin_pad * 9 * Cout;
     hipLaunchKernelGGL(pack_conv3x3_kernel, dim3(stream_grid(total)), dim3(256), 0,
-                       as_stream(stream), w, wpk, Cout, Cin, Cin_pad, mode);
+                       as_stream(stream), w, static_cast<float*>(wpk), Cout, Cin, Cin_pad, mode);
     return check_launch("pack_conv3x3");
 }
 
@@ -831,12 +744,25 @@ static int wgrad_check(const ugpg_wgrad_t* p) {
     return UGPG_OK;
 }
 
+enum WgradKind { WG_GENERIC, WG_C8, WG_X6 };
+
+static WgradKind wgrad_kind(const ugpg_wgrad_t* p, int C0, int C1) {
+    if (wgrad_use_c8(C0, C1, p->db)) return WG_C8;
+    if (p->math == UGPG_WFMT_X6 && !p->db && C0 % 64 == 0 && C1 % 64 == 0) return WG_X6;
+    return WG_GENERIC;
+}
+
+static WgradPlan wgrad_plan_for(const ugpg_wgrad_t* p, WgradKind k, int Cin) {
+    if (k == WG_C8) return wgrad_plan_c8(p->B, p->H, p->W, p->Cout);
+    if (k == WG_X6) return wgrad_plan(p->B, p->H, p->W, Cin, p->Cout, WGX6_TH, WGX6_TW);
+    return wgrad_plan(p->B, p->H, p->W, Cin, p->Cout);
+}
+
 extern "C" size_t ugpg_conv3x3_wgrad_workspace(const ugpg_wgrad_t* p) {
     if (wgrad_check(p)) return 0;
     const int C0 = p->src[0].C, C1 = p->src[1].data ? p->src[1].C : 0;
     const int Cin = C0 + C1;
-    WgradPlan w = wgrad_use_c8(C0, C1, p->db) ? wgrad_plan_c8(p->B, p->H, p->W, p->Cout)
-                                              : wgrad_plan(p->B, p->H, p->W, Cin, p->Cout);
+    WgradPlan w = wgrad_plan_for(p, wgrad_kind(p, C0, C1), Cin);
     return ((size_t)w.nsplit * 9 * p->Cout * Cin + (size_t)w.nsplit * p->Cout) * sizeof(float);
 }
 
@@ -845,9 +771,8 @@ extern "C" int ugpg_conv3x3_wgrad(const ugpg_wgrad_t* p, void* ws, size_t ws_byt
     if (int e = wgrad_check(p)) return e;
     const int C0 = p->src[0].C, C1 = p->src[1].data ? p->src[1].C : 0;
     const int Cin = C0 + C1;
-    const bool c8 = wgrad_use_c8(C0, C1, p->db);
-    WgradPlan w = c8 ? wgrad_plan_c8(p->B, p->H, p->W, p->Cout)
-                     : wgrad_plan(p->B, p->H, p->W, Cin, p->Cout);
+    const WgradKind kind = wgrad_kind(p, C0, C1);
+    WgradPlan w = wgrad_plan_for(p, kind, Cin);
     const size_t need = ugpg_conv3x3_wgrad_workspace(p);
     if (!ws || ws_bytes < need) {
         set_error("conv3x3_wgrad: workspace %zu < %zu", ws_bytes, need);
@@ -876,7 +801,9 @@ extern "C" int ugpg_conv3x3_wgrad(const ugpg_wgrad_t* p, void* ws, size_t ws_byt
     a.nsplit = w.nsplit;
     a.tps = w.tps;
     hipStream_t st = as_stream(stream);
-    if (c8) {
+    if (kind == WG_X6) {
+        launch_wgrad_x6(a, (unsigned)((p->Cout / 64) * (Cin / 64) * w.nsplit), st);
+    } else if (kind == WG_C8) {
         const unsigned grid = (unsigned)((p->Cout / 64) * w.nsplit);
         hipLaunchKernelGGL((conv3x3_wgrad_c8_kernel<WG8_TH, WG8_TW>), dim3(grid), dim3(192), 0, st,
                            a);

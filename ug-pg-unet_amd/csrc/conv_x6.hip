@@ -1,0 +1,459 @@
+// 3x3 / pad-1 convolution forward and data-gradient on bf16 MFMA with fp32
+// accuracy ("split-bf16 x6"), gfx950.
+//
+// Every fp32 operand x is split exactly into three bf16 pieces
+//     x = x0 + x1 + x2,  x0 = bf16(x), x1 = bf16(x - x0), x2 = bf16(x - x0 - x1)
+// (round-to-nearest; each remainder is exact in fp32, and 3 x 8 significand bits
+// cover fp32's 24).  A product keeps the six terms of order <= 2,
+//     a*b ~ a0 b0 + a0 b1 + a1 b0 + a0 b2 + a1 b1 + a2 b0,
+// dropping a1 b2 + a2 b1 + a2 b2, which is below 2^-25 |a b| -- under the
+// rounding error of one fp32 multiply.  bf16 x bf16 products are exact in the
+// fp32 accumulator, so each output is an fp32 sum of fp32-accurate products:
+// the same arithmetic class as the v_mfma_f32_32x32x2_f32 path in conv.hip, at
+// 6 x v_mfma_f32_32x32x16_bf16 (6 x 32 cycles) per 16-deep k-step instead of
+// 8 x v_mfma_f32_32x32x2_f32 (8 x 64 cycles): 2.67x the MFMA rate.
+//
+// Tile: 128 output pixels (4 x 32, or 8 x 16 for narrow images) x 64 output
+// channels, input channels in chunks of 16 (one MFMA k-step per tap).  The
+// activation halo is staged in LDS as three bf16 planes, split while staging
+// (after the lazy BatchNorm+ReLU of the producer); the weights arrive pre-split
+// by launch_pack_x6 in exactly the LDS image order.  4 waves as 2 (pixels) x 2
+// (channels), each a 64 x 32 output block = two 32x32 accumulators.
+//
+// LDS images (16-byte vectors of 8 bf16):
+//   A [piece 3][channel half 2][NHP]  pixel pitch 16 B, halo row pitch HS
+//   B [piece 3][channel half 2][tap 9][co 64]
+// Both fragment reads are single ds_read_b128 per (piece, tile) and conflict-free:
+// a 16-lane read group touches 16 distinct 16-B bank slots (32-wide tile: one
+// image row; 16-wide tile: permuted rows, see tile_pixel<16, true>, with HS=24).
+#include "conv_common.h"
+
+namespace ugpg {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void split3(f32x8 v, u32x4& p0, u32x4& p1, u32x4& p2) {
+    const bf16x8 h = __builtin_convertvector(v, bf16x8);
+    f32x8 r = v - __builtin_convertvector(h, f32x8);
+    const bf16x8 m = __builtin_convertvector(r, bf16x8);
+    r = r - __builtin_convertvector(m, f32x8);
+    const bf16x8 l = __builtin_convertvector(r, bf16x8);
+    p0 = __builtin_bit_cast(u32x4, h);
+    p1 = __builtin_bit_cast(u32x4, m);
+    p2 = __builtin_bit_cast(u32x4, l);
+}
+
+__device__ __forceinline__ f32x16 mfma16(u32x4 a, u32x4 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                   __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+
+// acc += a*b to fp32 accuracy from the pieces (smallest terms first)
+__device__ __forceinline__ f32x16 mfma_x6(const u32x4 (&a)[3], const u32x4 (&b)[3], f32x16 c) {
+    c = mfma16(a[2], b[0], c);
+    c = mfma16(a[1], b[1], c);
+    c = mfma16(a[0], b[2], c);
+    c = mfma16(a[1], b[0], c);
+    c = mfma16(a[0], b[1], c);
+    c = mfma16(a[0], b[0], c);
+    return c;
+}
+
+template <int TH, int TW, bool PERM16>
+__global__ void __launch_bounds__(256) conv3x3_fwd_x6_kernel(ConvFwdArgs a) {
+    constexpr int BN = 64, BKC = 16, WM = 2, WN = 2, MT = 2, NT = 1;
+    static_assert(TH * TW == 128, "tile must be 128 pixels");
+    constexpr int HWD = TW + 2;                  // halo width
+    constexpr int HS = PERM16 ? 24 : HWD;        // halo row pitch in the LDS image
+    constexpr int NHALO = (TH + 2) * HWD;        // staged halo pixels
+    constexpr int NHP0 = (TH + 2) * HS;
+    constexpr int NHP = NHP0 + (12 - NHP0 % 8) % 8;  // = 4 (mod 8): h planes 64 B apart mod 128
+    constexpr int A_ITEMS = NHALO * 2;           // (pixel, channel half) items
+    constexpr int A_PER = (A_ITEMS + 255) / 256;
+    constexpr int B_VEC = 6 * 9 * BN;            // 16-B vectors of the weight slab
+    constexpr int B_PER = (B_VEC + 255) / 256;
+    constexpr int A_VECS = 6 * NHP;
+    __shared__ __attribute__((aligned(16))) u32x4 smem[A_VECS + B_VEC];
+    u32x4* As = smem;
+    u32x4* Bs = smem + A_VECS;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int NB = a.Cout / BN;
+    const int nb = blockIdx.x % NB, tile = blockIdx.x / NB;
+    const int n0 = nb * BN;
+    const int tpi = a.tiles_x * a.tiles_y;
+    const int b = tile / tpi, trem = tile % tpi;
+    const int ty0 = (trem / a.tiles_x) * TH, tx0 = (trem % a.tiles_x) * TW;
+    const int nchunk = a.Cin / BKC;
+
+    f32x4 ra[A_PER][2];
+    u32x4 rb[B_PER];
+    unsigned avalid = 0;
+
+    auto gload = [&](int c) {
+        int cb = c * BKC;
+        const float* src = a.src0;
+        int Cs = a.C0;
+        if (cb >= a.C0) {
+            src = a.src1;
+            Cs = a.C1;
+            cb -= a.C0;
+        }
+        avalid = 0;
+#pragma unroll
+        for (int v = 0; v < A_PER; ++v) {
+            const int idx = tid + v * 256;
+            ra[v][0] = ra[v][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (idx < A_ITEMS) {
+                const int hp = idx >> 1, hh = idx & 1;
+                const int gy = ty0 - 1 + hp / HWD, gx = tx0 - 1 + hp % HWD;
+                if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
+                    const float* p = src + ((size_t)(b * a.H + gy) * a.W + gx) * Cs + cb + hh * 8;
+                    ra[v][0] = *reinterpret_cast<const f32x4*>(p);
+                    ra[v][1] = *reinterpret_cast<const f32x4*>(p + 4);
+                    avalid |= 1u << v;
+                }
+            }
+        }
+        const u32x4* wsrc = static_cast<const u32x4*>(a.wpk) + ((size_t)nb * nchunk + c) * B_VEC;
+#pragma unroll
+        for (int v = 0; v < B_PER; ++v) {
+            const int idx = tid + v * 256;
+            if (idx < B_VEC) rb[v] = wsrc[idx];
+        }
+    };
+
+    auto lstore = [&](int c) {
+        int cb = c * BKC;
+        const float* sc = a.sc0;
+        const float* sh = a.sh0;
+        if (cb >= a.C0) {
+            sc = a.sc1;
+            sh = a.sh1;
+            cb -= a.C0;
+        }
+#pragma unroll
+        for (int v = 0; v < A_PER; ++v) {
+            const int idx = tid + v * 256;
+            if (idx < A_ITEMS) {
+                const int hp = idx >> 1, hh = idx & 1;
+                f32x4 lo4 = ra[v][0], hi4 = ra[v][1];
+                if ((avalid >> v) & 1u) {
+                    lo4 = act_apply4(lo4, sc, sh, cb + hh * 8);
+                    hi4 = act_apply4(hi4, sc, sh, cb + hh * 8 + 4);
+                }
+                const f32x8 x = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
+                u32x4 p0, p1, p2;
+                split3(x, p0, p1, p2);
+                const int hl = (hp / HWD) * HS + hp % HWD;
+                As[(0 * 2 + hh) * NHP + hl] = p0;
+                As[(1 * 2 + hh) * NHP + hl] = p1;
+                As[(2 * 2 + hh) * NHP + hl] = p2;
+            }
+        }
+#pragma unroll
+        for (int v = 0; v < B_PER; ++v) {
+            const int idx = tid + v * 256;
+            if (idx < B_VEC) Bs[idx] = rb[v];
+        }
+    };
+
+    f32x16 acc[MT][NT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[mt][0][r] = 0.f;
+
+    const int hl = lane >> 5;
+    int aoff[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        const int m = tile_pixel<TW, PERM16>(wm * 64 + mt * 32 + (lane & 31));
+        aoff[mt] = hl * NHP + (m / TW) * HS + (m % TW);
+    }
+    const int boff = hl * 9 * BN + wn * 32 + (lane & 31);
+
+    auto ldfrag = [&](int t, u32x4 (&af)[MT][3], u32x4 (&bf)[3]) {
+        const int toff = (t / 3) * HS + (t % 3);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) af[mt][q] = As[q * 2 * NHP + aoff[mt] + toff];
+            bf[q] = Bs[q * 2 * 9 * BN + boff + t * BN];
+        }
+    };
+
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    for (int c = 0; c < nchunk; ++c) {
+        if (c + 1 < nchunk) gload(c + 1);
+        u32x4 fa[2][MT][3], fb[2][3];
+        ldfrag(0, fa[0], fb[0]);
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            if (t + 1 < 9) ldfrag(t + 1, fa[(t + 1) & 1], fb[(t + 1) & 1]);
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) acc[mt][0] = mfma_x6(fa[t & 1][mt], fb[t & 1], acc[mt][0]);
+        }
+        __syncthreads();
+        if (c + 1 < nchunk) {
+            lstore(c + 1);
+            __syncthreads();
+        }
+    }
+
+    conv_epilogue<TH, TW, BN, WM, WN, MT, NT, PERM16>(a, acc, reinterpret_cast<float*>(smem), tile,
+                                                      b, ty0, tx0, n0, wm, wn);
+}
+
+// ---------------------------------------------------------------------------
+// Split-bf16 weight gradient: dW[co][ci][t] = sum_p dy[p][co] * act(x)[p+t][ci].
+// Same block decomposition and partial layout as conv3x3_wgrad_kernel (64 co x
+// 64 ci x 9 taps per block, 4 waves as 2 (co) x 2 (ci) with nine 32x32
+// accumulators, deterministic split-K), but the K = pixel reduction runs on
+// v_mfma_f32_32x32x16_bf16: one k-step = one 16-pixel row of the 4 x 16 tile.
+// Both operands are pixel-major in LDS -- one 448-B record per pixel holding the
+// three bf16 pieces of its 64 channels (384 B + 64 B pad) -- and are read
+// transposed with ds_read_b64_tr_b16 (4 pixels x 16 channels per 16-lane group):
+// the tap shift is then just a constant record offset, and the 112-dword record
+// pitch puts any 4 consecutive pixels x 32 channels on 64 distinct banks.
+// ---------------------------------------------------------------------------
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void split3_4(f32x4 v, u32x2& p0, u32x2& p1, u32x2& p2) {
+    const bf16x4 h = __builtin_convertvector(v, bf16x4);
+    f32x4 r = v - __builtin_convertvector(h, f32x4);
+    const bf16x4 m = __builtin_convertvector(r, bf16x4);
+    r = r - __builtin_convertvector(m, f32x4);
+    const bf16x4 l = __builtin_convertvector(r, bf16x4);
+    p0 = __builtin_bit_cast(u32x2, h);
+    p1 = __builtin_bit_cast(u32x2, m);
+    p2 = __builtin_bit_cast(u32x2, l);
+}
+
+__device__ __forceinline__ u32x2 ds_read_tr(const char* lds_byte_addr) {
+    const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(lds_byte_addr));
+    return __builtin_bit_cast(u32x2, v);
+}
+
+constexpr int WX_REC = 448;  // bytes per pixel record: 3 pieces x 64 ch x 2 B + 64 B pad
+
+template <int TH, int TW>
+__global__ void __launch_bounds__(256, 2) conv3x3_wgrad_x6_kernel(WgradArgs a) {
+    static_assert(TW == 16, "one 16-pixel row per MFMA k-step");
+    constexpr int P = TH * TW, HWD = TW + 2, NHALO = (TH + 2) * HWD;
+    constexpr int DY_Q = P * 16, X_Q = NHALO * 16;  // float4 quads to stage
+    constexpr int DY_PER = (DY_Q + 255) / 256, X_PER = (X_Q + 255) / 256;
+    static_assert(X_PER <= 32, "halo too large");
+    __shared__ __attribute__((aligned(16))) char smem[(P + NHALO) * WX_REC];
+    char* dys = smem;
+    char* xs = smem + P * WX_REC;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int NCO = a.Cout / 64, NCI = a.Cin / 64;
+    const int nb = blockIdx.x % NCO;
+    const int rest = blockIdx.x / NCO;
+    const int cb = rest % NCI, split = rest / NCI;
+    const int co0 = nb * 64, ci0 = cb * 64;
+    const int t_begin = split * a.tps, t_end = min(a.ntiles, t_begin + a.tps);
+
+    const float* xsrc = a.src0;
+    const float* xsc = a.sc0;
+    const float* xsh = a.sh0;
+    int Cs = a.C0, cbase = ci0;
+    if (ci0 >= a.C0) {
+        xsrc = a.src1;
+        xsc = a.sc1;
+        xsh = a.sh1;
+        Cs = a.C1;
+        cbase = ci0 - a.C0;
+    }
+    const int tpi = a.tiles_x * a.tiles_y;
+
+    f32x4 rdy[DY_PER], rx[X_PER];
+    unsigned xvalid = 0;
+    auto gload = [&](int tile) {
+        const int b = tile / tpi, trem = tile % tpi;
+        const int ty0 = (trem / a.tiles_x) * TH, tx0 = (trem % a.tiles_x) * TW;
+#pragma unroll
+        for (int v = 0; v < DY_PER; ++v) {
+            const int idx = tid + v * 256;
+            f32x4 val = {0.f, 0.f, 0.f, 0.f};
+            if (idx < DY_Q) {
+                const int p = idx >> 4, q = idx & 15;
+                const int gy = ty0 + p / TW, gx = tx0 + p % TW;
+                if (gy < a.H && gx < a.W)
+                    val = *reinterpret_cast<const f32x4*>(
+                        a.dy + ((size_t)(b * a.H + gy) * a.W + gx) * a.Cout + co0 + q * 4);
+            }
+            rdy[v] = val;
+        }
+        xvalid = 0;
+#pragma unroll
+        for (int v = 0; v < X_PER; ++v) {
+            const int idx = tid + v * 256;
+            f32x4 val = {0.f, 0.f, 0.f, 0.f};
+            if (idx < X_Q) {
+                const int hp = idx >> 4, q = idx & 15;
+                const int gy = ty0 - 1 + hp / HWD, gx = tx0 - 1 + hp % HWD;
+                if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
+                    val = *reinterpret_cast<const f32x4*>(
+                        xsrc + ((size_t)(b * a.H + gy) * a.W + gx) * Cs + cbase + q * 4);
+                    xvalid |= 1u << v;
+                }
+            }
+            rx[v] = val;
+        }
+    };
+    // record layout: [piece][64 ch] bf16 at byte piece*128 + ch*2
+    auto put = [&](char* base, int rec, int q, f32x4 v) {
+        u32x2 p0, p1, p2;
+        split3_4(v, p0, p1, p2);
+        char* r = base + rec * WX_REC + q * 8;
+        *reinterpret_cast<u32x2*>(r) = p0;
+        *reinterpret_cast<u32x2*>(r + 128) = p1;
+        *reinterpret_cast<u32x2*>(r + 256) = p2;
+    };
+    auto lstore = [&]() {
+#pragma unroll
+        for (int v = 0; v < DY_PER; ++v) {
+            const int idx = tid + v * 256;
+            if (idx < DY_Q) put(dys, idx >> 4, idx & 15, rdy[v]);
+        }
+#pragma unroll
+        for (int v = 0; v < X_PER; ++v) {
+            const int idx = tid + v * 256;
+            if (idx < X_Q) {
+                f32x4 val = rx[v];
+                if ((xvalid >> v) & 1u) val = act_apply4(val, xsc, xsh, cbase + (idx & 15) * 4);
+                put(xs, idx >> 4, idx & 15, val);
+            }
+        }
+    };
+
+    f32x16 acc[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+    // transposed-read addresses: 16-lane group g = lane>>4 (h = g>>1 pixel half,
+    // g&1 channel half), lane li supplies row (pixel) li>>2, channels 4(li&3)..+3.
+    const int li = lane & 15, g = lane >> 4, hh = g >> 1;
+    const int pix_in = 8 * hh + (li >> 2);                  // + 4s for read s
+    const int ch_a = wm * 32 + 16 * (g & 1) + 4 * (li & 3);  // co within the block
+    const int ch_b = wn * 32 + 16 * (g & 1) + 4 * (li & 3);  // ci within the block
+    const char* abase = dys + pix_in * WX_REC + ch_a * 2;
+    const char* bbase = xs + pix_in * WX_REC + ch_b * 2;
+
+    if (t_begin < t_end) gload(t_begin);
+    for (int tile = t_begin; tile < t_end; ++tile) {
+        __syncthreads();
+        lstore();
+        __syncthreads();
+        if (tile + 1 < t_end) gload(tile + 1);
+#pragma unroll 1
+        for (int ks = 0; ks < TH; ++ks) {
+            u32x4 af[3];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const char* pa = abase + ks * TW * WX_REC + q * 128;
+                const u32x2 lo = ds_read_tr(pa), hi = ds_read_tr(pa + 4 * WX_REC);
+                af[q] = u32x4{lo.x, lo.y, hi.x, hi.y};
+            }
+            auto ldb = [&](int t, u32x4 (&bf)[3]) {
+                const char* pb = bbase + ((ks + t / 3) * HWD + (t % 3)) * WX_REC;
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    const u32x2 lo = ds_read_tr(pb + q * 128), hi = ds_read_tr(pb + q * 128 + 4 * WX_REC);
+                    bf[q] = u32x4{lo.x, lo.y, hi.x, hi.y};
+                }
+            };
+            u32x4 bfr[2][3];
+            ldb(0, bfr[0]);
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                if (t + 1 < 9) ldb(t + 1, bfr[(t + 1) & 1]);
+                acc[t] = mfma_x6(af, bfr[t & 1], acc[t]);
+            }
+        }
+    }
+
+    const int ci = ci0 + wn * 32 + (lane & 31);
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int co = co0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            a.part[((size_t)(split * 9 + t) * a.Cout + co) * a.Cin + ci] = acc[t][r];
+        }
+}
+
+void launch_wgrad_x6(const WgradArgs& a, unsigned grid, hipStream_t st) {
+    hipLaunchKernelGGL((conv3x3_wgrad_x6_kernel<WGX6_TH, WGX6_TW>), dim3(grid), dim3(256), 0, st,
+                       a);
+}
+
+// Weight pack for the split path.  mode 0 (forward): GEMM N = Cout, K channels =
+// Cin_pad; mode 1 (data gradient): N = Cin_pad, K channels = Cout, taps rotated
+// by 180 degrees.  Layout [N/64][K/16][piece][half][tap][64][8] bf16: the slab of
+// one (column block, chunk) is contiguous and equals the kernel's B LDS image.
+__global__ void pack_x6_kernel(const float* w, __bf16* wpk, int Cout, int Cin, int N, int K,
+                               int mode) {
+    const int nchunk = K / 16;
+    const int64_t total = (int64_t)N * K * 9;
+    const int64_t plane = 9 * 64 * 8;  // one (piece, half) sub-slab
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int j = (int)(e & 7);
+        int64_t r = e >> 3;
+        const int co = (int)(r % 64);
+        r /= 64;
+        const int t = (int)(r % 9);
+        r /= 9;
+        const int h = (int)(r % 2);
+        r /= 2;
+        const int chunk = (int)(r % nchunk), nb = (int)(r / nchunk);
+        const int n = nb * 64 + co, k = chunk * 16 + h * 8 + j;
+        float v;
+        if (mode == 0) v = k < Cin ? w[((size_t)n * Cin + k) * 9 + t] : 0.f;
+        else v = n < Cin ? w[((size_t)k * Cin + n) * 9 + (8 - t)] : 0.f;
+        const __bf16 p0 = (__bf16)v;
+        const float r1 = v - (float)p0;
+        const __bf16 p1 = (__bf16)r1;
+        const __bf16 p2 = (__bf16)(r1 - (float)p1);
+        const size_t base = ((size_t)(nb * nchunk + chunk) * 3 * 2) * plane;
+        const size_t off = ((size_t)t * 64 + co) * 8 + j;
+        wpk[base + (0 * 2 + h) * plane + off] = p0;
+        wpk[base + (1 * 2 + h) * plane + off] = p1;
+        wpk[base + (2 * 2 + h) * plane + off] = p2;
+    }
+}
+
+int fwd_x6_tile_w(int W) { return W >= 32 ? 32 : 16; }
+int fwd_x6_tile_h(int W) { return W >= 32 ? 4 : 8; }
+
+void launch_fwd_x6(const ConvFwdArgs& a, hipStream_t st) {
+    const unsigned grid = (unsigned)((int64_t)a.ntiles * (a.Cout / 64));
+    if (fwd_x6_tile_w(a.W) == 32)
+        hipLaunchKernelGGL((conv3x3_fwd_x6_kernel<4, 32, false>), dim3(grid), dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL((conv3x3_fwd_x6_kernel<8, 16, true>), dim3(grid), dim3(256), 0, st, a);
+}
+
+void launch_pack_x6(const float* w, void* wpk, int Cout, int Cin, int Cin_pad, int mode,
+                    hipStream_t st) {
+    const int N = mode == 0 ? Cout : Cin_pad, K = mode == 0 ? Cin_pad : Cout;
+    hipLaunchKernelGGL(pack_x6_kernel, dim3(stream_grid((int64_t)N * K * 9)), dim3(256), 0, st, w,
+                       static_cast<__bf16*>(wpk), Cout, Cin, N, K, mode);
+}
+
+}  // namespace ugpg

@@ -25,13 +25,13 @@ class ConvDesc(C.Structure):
     """ugpg_conv_t."""
     _fields_ = [("B", _i), ("H", _i), ("W", _i), ("src", Src * 2), ("wpk", _p), ("bias", _p),
                 ("Cout", _i), ("out", _p * 2), ("out_split", _i), ("accumulate", _i * 2),
-                ("stats", _p)]
+                ("stats", _p), ("wfmt", _i)]
 
 
 class WgradDesc(C.Structure):
     """ugpg_wgrad_t."""
     _fields_ = [("B", _i), ("H", _i), ("W", _i), ("src", Src * 2), ("dy", _p), ("Cout", _i),
-                ("dw", _p), ("Cin_real", _i), ("db", _p), ("accumulate", _i)]
+                ("dw", _p), ("Cin_real", _i), ("db", _p), ("accumulate", _i), ("math", _i)]
 
 
 # name -> (restype, argtypes); must match include/ugpg.h exactly
@@ -40,8 +40,9 @@ SIGNATURES = {
     "ugpg_last_error": (C.c_char_p, []),
     "ugpg_set_tuning": (_i, [C.c_char_p, _i]),
     "ugpg_conv3x3_fwd": (_i, [C.POINTER(ConvDesc), _p]),
-    "ugpg_conv3x3_fwd_ntiles": (_i, [_i, _i, _i, _i, _i]),
-    "ugpg_pack_conv3x3": (_i, [_p, _p, _i, _i, _i, _i, _p]),
+    "ugpg_conv3x3_fwd_ntiles": (_i, [_i, _i, _i, _i, _i, _i]),
+    "ugpg_pack_conv3x3_bytes": (_sz, [_i, _i, _i]),
+    "ugpg_pack_conv3x3": (_i, [_p, _p, _i, _i, _i, _i, _i, _p]),
     "ugpg_conv3x3_wgrad_workspace": (_sz, [C.POINTER(WgradDesc)]),
     "ugpg_conv3x3_wgrad": (_i, [C.POINTER(WgradDesc), _p, _sz, _p]),
     "ugpg_bn_finalize": (_i, [_p, _i, _i, _p, _p, _p, _p, _p, _f, _f, _p, _p, _p, _p, _p]),

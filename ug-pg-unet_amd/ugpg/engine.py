@@ -74,7 +74,7 @@ def double_conv_forward(mod, srcs, ctx: BlockCtx, save: bool):
         stats = None
         ntiles = 0
         if train:
-            ntiles = ops.conv_ntiles(B, H, W, cin, cout)
+            ntiles = ops.conv_ntiles(B, H, W, cin, cout, wpk)
             stats = ops.empty(3 * cout * ntiles, like=y)
         bias = conv.bias.detach() if conv.bias is not None else None
         ops.conv3x3_fwd(cur, wpk, bias, cout, [y], stats=stats,

@@ -7,6 +7,7 @@ Activations are NHWC fp32 ``(B, H, W, C)`` tensors.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import torch
 
@@ -79,16 +80,47 @@ NULL_SRC = Src(None, None, None, 0)
 
 
 # ------------------------------------------------------------------ conv
+WFMT_F32, WFMT_X6 = 0, 1
+_MATHS = ("x6", "f32")
+_conv_math = os.environ.get("UGPG_CONV_MATH", "x6")
+if _conv_math not in _MATHS:
+    raise ValueError(f"UGPG_CONV_MATH must be one of {_MATHS}, got {_conv_math!r}")
+
+
+def set_conv_math(math: str) -> None:
+    """'x6': split-bf16 MFMA (fp32-accurate, 2.67x the fp32 MFMA rate) wherever the
+    shape allows; 'f32': v_mfma_f32_32x32x2_f32 everywhere."""
+    global _conv_math
+    if math not in _MATHS:
+        raise ValueError(f"conv math must be one of {_MATHS}")
+    _conv_math = math
+
+
+def conv_math() -> str:
+    return _conv_math
+
+
+def conv_weight_format(n: int, k: int) -> int:
+    """Pack format for a conv GEMM with N output columns and K input channels."""
+    return WFMT_X6 if _conv_math == "x6" and n % 64 == 0 and k % 16 == 0 else WFMT_F32
+
+
 def pack_conv3x3(w, cin_pad: int, mode: int) -> torch.Tensor:
+    """Repack OIHW weights for conv3x3_fwd (mode 0) or its data gradient (mode 1).
+    The result carries its pack format in ``.ugpg_fmt``."""
     cout, cin = w.shape[0], w.shape[1]
-    out = empty(cin_pad * 9 * cout, like=w)
-    check(lib.ugpg_pack_conv3x3(_f32(w.contiguous()), ptr(out), cout, cin, cin_pad, mode, stream()),
-          "pack_conv3x3")
+    fmt = conv_weight_format(cout, cin_pad) if mode == 0 else conv_weight_format(cin_pad, cout)
+    out = torch.empty(lib.ugpg_pack_conv3x3_bytes(cout, cin_pad, fmt), dtype=torch.uint8,
+                      device=w.device)
+    check(lib.ugpg_pack_conv3x3(_f32(w.contiguous()), ptr(out), cout, cin, cin_pad, mode, fmt,
+                                stream()), "pack_conv3x3")
+    out.ugpg_fmt = fmt
     return out
 
 
-def conv_ntiles(B, H, W, cin, cout) -> int:
-    return lib.ugpg_conv3x3_fwd_ntiles(B, H, W, cin, cout)
+def conv_ntiles(B, H, W, cin, cout, wpk) -> int:
+    """BatchNorm partial-tile count of conv3x3_fwd with these packed weights."""
+    return lib.ugpg_conv3x3_fwd_ntiles(B, H, W, cin, cout, wpk.ugpg_fmt)
 
 
 class KernelTimer:
@@ -142,6 +174,7 @@ def conv3x3_fwd(srcs, wpk, bias, cout, outs, split=None, accumulate=(0, 0), stat
     d.out_split = cout if split is None else split
     d.accumulate[0], d.accumulate[1] = int(accumulate[0]), int(accumulate[1])
     d.stats = ptr(stats)
+    d.wfmt = wpk.ugpg_fmt
     _timed("conv3x3_fwd", flops,
            lambda: check(lib.ugpg_conv3x3_fwd(C.byref(d), stream()), "conv3x3_fwd"))
 
@@ -154,6 +187,7 @@ def conv3x3_wgrad(srcs, dy, dw, db, cin_real, accumulate=0, flops=None):
     d.src[1] = srcs[1].src() if len(srcs) > 1 else NULL_SRC
     d.dy, d.Cout = ptr(dy), dy.shape[-1]
     d.dw, d.Cin_real, d.db, d.accumulate = ptr(dw), cin_real, ptr(db), int(accumulate)
+    d.math = WFMT_X6 if _conv_math == "x6" else WFMT_F32
     nbytes = lib.ugpg_conv3x3_wgrad_workspace(C.byref(d))
     if nbytes == 0:
         check(-1, "conv3x3_wgrad_workspace")
