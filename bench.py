@@ -31,6 +31,8 @@ sys.path[:0] = [str(ROOT), str(ROOT / "ug-pg-unet_amd")]
 
 METRIC = "images/sec Stage-4 256×256 bs16 fwd+bwd at 1/2/4/8 MI355X; Dice vs ref"
 FP32_PEAK_TFLOPS = 157.3  # MI355X dense FP32 (matrix = vector rate), MI355X_MICROARCH.md
+BF16_PEAK_TFLOPS = 16 * FP32_PEAK_TFLOPS  # dense bf16 MFMA = 16x the f32 rate (same guide)
+X6_PRODUCTS = 6  # split-bf16: 6 bf16 MFMA products per fp32-accurate multiply-add
 UG_STEP_GFLOP = 225.2866  # per image, SURVEY.md §8d
 
 
@@ -67,6 +69,22 @@ def cpu_baseline(batch, res, steps, threads):
             "kind": "port",
             "sample": f"{steps} oracle UG steps (bs{batch} {res}^2, S4 fwd+bwd + S3 U-map + RMSprop) "
                       f"after 1 warm-up, torch CPU fp32, {threads} threads"}
+
+
+def pmc_traffic(family):
+    """HBM bytes per launch of a kernel family from the newest committed PMC summary
+    (profiles/*_pmc.json, written by tools/pmc_summary.py from separate FETCH_SIZE /
+    WRITE_SIZE passes with the gfx950 x2 read correction); None when absent."""
+    files = sorted((ROOT / "profiles").glob("*_pmc.json"), key=lambda p: p.stat().st_mtime)
+    if not files:
+        return None, None
+    rows = json.load(open(files[-1]))
+    sel = [r for k, r in rows.items() if k.split("<")[0].split("::")[-1].startswith(family + "_")
+           or k.split("<")[0].split("::")[-1] == family + "_kernel"]
+    calls = sum(r["calls"] for r in sel)
+    if not calls:
+        return None, None
+    return round(sum(r["calls"] * r["hbm_bytes"] for r in sel) / calls), f"profiles/{files[-1].name}"
 
 
 def main():
@@ -131,9 +149,14 @@ def main():
         dom = max(summ, key=lambda k: summ[k]["ms"])
         d = summ[dom]
         achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
+        x6 = ops.conv_math() == "x6"
+        peak = BF16_PEAK_TFLOPS / X6_PRODUCTS if x6 else FP32_PEAK_TFLOPS
+        traffic, src = pmc_traffic(dom)
         roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2),
-                "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                "peak": round(peak, 1), "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+                "traffic": traffic, "traffic_source": src,
+                "arithmetic": ("split-bf16 x6: fp32-accurate products from 6 bf16 MFMAs; peak = "
+                               "dense bf16 MFMA peak / 6" if x6 else "fp32 MFMA"),
                 "flops_per_launch": round(d["flops"] / d["launches"]),
                 "avg_launch_ms": round(d["ms"] / d["launches"], 4)}
 

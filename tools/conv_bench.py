@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--cfgs", default="-1", help="fp32 tile configs (-1 = heuristic)")
     ap.add_argument("--maths", default="x6,f32")
+    ap.add_argument("--pipes", default="1", help="x6 forward forms to time (x6_pipe knob)")
     ap.add_argument("--wgrad", action="store_true")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
@@ -67,11 +68,14 @@ def main():
             wpk1 = ops.pack_conv3x3(w, real_cin, 1) if real_cin % 64 == 0 else None
             nt = ops.conv_ntiles(B, H, H, cin, Cout, wpk)
             st = torch.empty(3 * Cout * nt, device=dev)
-            for c in (cfgs if m == "f32" else [-1]):
-                tag = m if c == -1 else f"{m}{c}"
+            variants = [(c, 1) for c in cfgs] if m == "f32" else \
+                [(-1, int(pp)) for pp in a.pipes.split(",")]
+            for c, pipe in variants:
+                tag = (m if c == -1 else f"{m}{c}") + (f"p{pipe}" if m == "x6" and "," in a.pipes else "")
 
-                def f(c=c, wpk=wpk, st=st):
+                def f(c=c, wpk=wpk, st=st, pipe=pipe):
                     lib.ugpg_set_tuning(b"fwd_cfg", c)
+                    lib.ugpg_set_tuning(b"x6_pipe", pipe)
                     ops.conv3x3_fwd(srcs, wpk, bias, Cout, [out], stats=st)
                 fns[f"fwd_{tag}"] = f
                 if wpk1 is not None:
@@ -79,8 +83,9 @@ def main():
                     d0 = torch.empty(B, H, H, C0, device=dev)
                     d1 = torch.empty(B, H, H, C1, device=dev) if C1 else None
 
-                    def g(c=c, wpk1=wpk1, dy=dy, d0=d0, d1=d1):
+                    def g(c=c, wpk1=wpk1, dy=dy, d0=d0, d1=d1, pipe=pipe):
                         lib.ugpg_set_tuning(b"fwd_cfg", c)
+                        lib.ugpg_set_tuning(b"x6_pipe", pipe)
                         ops.conv3x3_fwd([ops.Act(dy)], wpk1, None, real_cin,
                                         [d0, d1] if C1 else [d0], split=C0 if C1 else None)
                     fns[f"dgrad_{tag}"] = g
@@ -101,6 +106,7 @@ def main():
                 except RuntimeError as e:
                     res[k].append(float("nan"))
         lib.ugpg_set_tuning(b"fwd_cfg", -1)
+        lib.ugpg_set_tuning(b"x6_pipe", 1)
         ops.set_conv_math("x6")
         rows[name] = {k: (min(v), flops / (min(v) * 1e-3) / 1e12) for k, v in res.items()}
         print(name, " ".join(f"{k}={v[0]:.3f}ms/{v[1]:.0f}TF" for k, v in rows[name].items()),

@@ -53,6 +53,34 @@ __device__ __forceinline__ f32x4 act_apply4(f32x4 v, const float* sc, const floa
     return v;
 }
 
+// Lazy-activation coefficients of 4 channels held in registers: conv kernels load
+// them together with the data they will transform (a load at LDS-store time would
+// stall the whole block on a global round trip).
+struct Act4 {
+    f32x4 s, h;
+};
+__device__ __forceinline__ Act4 act_load4(const float* sc, const float* sh, int c) {
+    Act4 r;
+    if (sc) {
+        r.s = *reinterpret_cast<const f32x4*>(sc + c);
+        r.h = *reinterpret_cast<const f32x4*>(sh + c);
+    } else {
+        r.s = f32x4{1.f, 1.f, 1.f, 1.f};
+        r.h = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    return r;
+}
+// on == false: identity (no BatchNorm+ReLU on this operand)
+__device__ __forceinline__ f32x4 act_reg4(f32x4 v, const Act4& a, bool on) {
+    if (on) {
+        v.x = fmaxf(fmaf(v.x, a.s.x, a.h.x), 0.0f);
+        v.y = fmaxf(fmaf(v.y, a.s.y, a.h.y), 0.0f);
+        v.z = fmaxf(fmaf(v.z, a.s.z, a.h.z), 0.0f);
+        v.w = fmaxf(fmaf(v.w, a.s.w, a.h.w), 0.0f);
+    }
+    return v;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

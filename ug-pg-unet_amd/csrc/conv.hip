@@ -46,16 +46,24 @@ __global__ void __launch_bounds__(256, MINW) conv3x3_fwd_kernel(ConvFwdArgs a) {
     f32x4 ra[A_PER];
     f32x4 rb[B_PER];
     unsigned avalid = 0;
+    Act4 ract;  // coefficients of this thread's 4 channels (fixed: q = tid % (BKC/4))
+    bool aon = false;
 
     auto gload = [&](int c) {
         int cb = c * BKC;
         const float* src = a.src0;
+        const float* sc = a.sc0;
+        const float* sh = a.sh0;
         int Cs = a.C0;
         if (cb >= a.C0) {
             src = a.src1;
+            sc = a.sc1;
+            sh = a.sh1;
             Cs = a.C1;
             cb -= a.C0;
         }
+        aon = sc != nullptr;
+        ract = act_load4(sc, sh, cb + (tid % (BKC / 4)) * 4);
         avalid = 0;
 #pragma unroll
         for (int v = 0; v < A_PER; ++v) {
@@ -85,21 +93,14 @@ __global__ void __launch_bounds__(256, MINW) conv3x3_fwd_kernel(ConvFwdArgs a) {
     };
 
     auto lstore = [&](int c) {
-        int cb = c * BKC;
-        const float* sc = a.sc0;
-        const float* sh = a.sh0;
-        if (cb >= a.C0) {
-            sc = a.sc1;
-            sh = a.sh1;
-            cb -= a.C0;
-        }
+        (void)c;
 #pragma unroll
         for (int v = 0; v < A_PER; ++v) {
             const int idx = tid + v * 256;
             if (idx < A_VEC) {
                 const int hp = idx / (BKC / 4), q = idx % (BKC / 4);
                 f32x4 val = ra[v];
-                if ((avalid >> v) & 1u) val = act_apply4(val, sc, sh, cb + q * 4);
+                if ((avalid >> v) & 1u) val = act_reg4(val, ract, aon);
                 *reinterpret_cast<f32x4*>(&As[hp * AP + q * 4]) = val;
             }
         }
@@ -209,6 +210,8 @@ __global__ void __launch_bounds__(256) conv3x3_wgrad_kernel(WgradArgs a) {
         cbase = ci0 - a.C0;
     }
     const int tpi = a.tiles_x * a.tiles_y;
+    const Act4 xact = act_load4(xsc, xsh, cbase + (tid & 15) * 4);  // q = idx & 15 = tid & 15
+    const bool xon = xsc != nullptr;
 
     f32x4 rdy[DY_PER], rx[X_PER];
     unsigned xvalid = 0;
@@ -256,7 +259,7 @@ __global__ void __launch_bounds__(256) conv3x3_wgrad_kernel(WgradArgs a) {
             const int idx = tid + v * 256;
             if (idx < X_VEC) {
                 f32x4 val = rx[v];
-                if ((xvalid >> v) & 1u) val = act_apply4(val, xsc, xsh, cbase + (idx & 15) * 4);
+                if ((xvalid >> v) & 1u) val = act_reg4(val, xact, xon);
                 *reinterpret_cast<f32x4*>(&xs[idx * 4]) = val;
             }
         }
@@ -348,6 +351,9 @@ __global__ void __launch_bounds__(192) conv3x3_wgrad_c8_kernel(WgradArgs a) {
     const bool jvalid = j < 72;
     const int jt = jvalid ? j / 8 : 0, jc = j % 8;
     const int joff = ((jt / 3) * HWD + (jt % 3)) * 8 + jc;
+    // this thread's 4 staged channels are fixed: (idx & 1) == (tid & 1)
+    const Act4 xact = act_load4(a.sc0, a.sh0, (tid & 1) * 4);
+    const bool xon = a.sc0 != nullptr;
 
     f32x4 rdy[DY_PER], rx[X_PER];
     unsigned xvalid = 0;
@@ -395,7 +401,7 @@ __global__ void __launch_bounds__(192) conv3x3_wgrad_c8_kernel(WgradArgs a) {
             const int idx = tid + v * NT;
             if (idx < X_VEC) {
                 f32x4 val = rx[v];
-                if ((xvalid >> v) & 1u) val = act_apply4(val, a.sc0, a.sh0, (idx & 1) * 4);
+                if ((xvalid >> v) & 1u) val = act_reg4(val, xact, xon);
                 *reinterpret_cast<f32x4*>(&xs[idx * 4]) = val;
             }
         }
@@ -609,6 +615,14 @@ extern "C" int ugpg_set_tuning(const char* key, int value) {
         g_force_fwd_cfg = value;
         return UGPG_OK;
     }
+    if (key && std::string(key) == "x6_pipe") {
+        g_x6_pipe = value;
+        return UGPG_OK;
+    }
+    if (key && std::string(key) == "x6_probe") {  // timing diagnostics; results are wrong
+        g_x6_probe = value;
+        return UGPG_OK;
+    }
     set_error("set_tuning: unknown key '%s'", key ? key : "(null)");
     return UGPG_ERR_INVALID;
 }
@@ -646,6 +660,7 @@ extern "C" int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream) {
         return UGPG_ERR_INVALID;
     }
     ConvFwdArgs a;
+    a.probe = 0;
     a.src0 = p->src[0].data;
     a.sc0 = p->src[0].scale;
     a.sh0 = p->src[0].shift;

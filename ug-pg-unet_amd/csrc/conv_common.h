@@ -24,6 +24,7 @@ struct ConvFwdArgs {
     float* stats;
     int B, H, W, Cin, Cout;
     int tiles_x, tiles_y, ntiles;
+    int probe;  // diagnostics only (tuning knob "x6_probe"): bit0 skip prefetch, bit1 skip staging
 };
 
 // Output pixel (row*TW + col inside the tile) of GEMM row m.  PERM16 is the
@@ -160,6 +161,7 @@ struct WgradArgs {
 
 // split-bf16 path (conv_x6.hip)
 void launch_fwd_x6(const ConvFwdArgs& a, hipStream_t st);
+extern int g_x6_pipe, g_x6_probe;
 int fwd_x6_tile_w(int W);  // 32 or 16
 int fwd_x6_tile_h(int W);  // 4 or 8
 void launch_wgrad_x6(const WgradArgs& a, unsigned grid, hipStream_t st);

@@ -92,59 +92,56 @@ __global__ void __launch_bounds__(256) conv3x3_fwd_x6_kernel(ConvFwdArgs a) {
     f32x4 ra[A_PER][2];
     u32x4 rb[B_PER];
     unsigned avalid = 0;
+    Act4 ract0, ract1;
+    bool aon = false;
 
     auto gload = [&](int c) {
         int cb = c * BKC;
         const float* src = a.src0;
+        const float* sc = a.sc0;
+        const float* sh = a.sh0;
         int Cs = a.C0;
         if (cb >= a.C0) {
             src = a.src1;
+            sc = a.sc1;
+            sh = a.sh1;
             Cs = a.C1;
             cb -= a.C0;
         }
+        // this thread's channel half is fixed (hh = idx & 1 = tid & 1)
+        aon = sc != nullptr;
+        ract0 = act_load4(sc, sh, cb + (tid & 1) * 8);
+        ract1 = act_load4(sc, sh, cb + (tid & 1) * 8 + 4);
         avalid = 0;
+        // branch-free: every lane loads from a clamped (valid) address and the halo
+        // mask is applied at LDS-store time, so no loaded register is merged at a
+        // join (which makes the compiler wait for the prefetch before the MFMAs)
 #pragma unroll
         for (int v = 0; v < A_PER; ++v) {
             const int idx = tid + v * 256;
-            ra[v][0] = ra[v][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (idx < A_ITEMS) {
-                const int hp = idx >> 1, hh = idx & 1;
-                const int gy = ty0 - 1 + hp / HWD, gx = tx0 - 1 + hp % HWD;
-                if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
-                    const float* p = src + ((size_t)(b * a.H + gy) * a.W + gx) * Cs + cb + hh * 8;
-                    ra[v][0] = *reinterpret_cast<const f32x4*>(p);
-                    ra[v][1] = *reinterpret_cast<const f32x4*>(p + 4);
-                    avalid |= 1u << v;
-                }
-            }
+            const int hp = idx < A_ITEMS ? idx >> 1 : 0, hh = tid & 1;
+            const int gy = ty0 - 1 + hp / HWD, gx = tx0 - 1 + hp % HWD;
+            const bool ok = idx < A_ITEMS && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
+            const int cy = min(max(gy, 0), a.H - 1), cx = min(max(gx, 0), a.W - 1);
+            const float* p = src + ((size_t)(b * a.H + cy) * a.W + cx) * Cs + cb + hh * 8;
+            ra[v][0] = *reinterpret_cast<const f32x4*>(p);
+            ra[v][1] = *reinterpret_cast<const f32x4*>(p + 4);
+            avalid |= (ok ? 1u : 0u) << v;
         }
         const u32x4* wsrc = static_cast<const u32x4*>(a.wpk) + ((size_t)nb * nchunk + c) * B_VEC;
 #pragma unroll
-        for (int v = 0; v < B_PER; ++v) {
-            const int idx = tid + v * 256;
-            if (idx < B_VEC) rb[v] = wsrc[idx];
-        }
+        for (int v = 0; v < B_PER; ++v) rb[v] = wsrc[min(tid + v * 256, B_VEC - 1)];
     };
 
     auto lstore = [&](int c) {
-        int cb = c * BKC;
-        const float* sc = a.sc0;
-        const float* sh = a.sh0;
-        if (cb >= a.C0) {
-            sc = a.sc1;
-            sh = a.sh1;
-            cb -= a.C0;
-        }
+        (void)c;
 #pragma unroll
         for (int v = 0; v < A_PER; ++v) {
             const int idx = tid + v * 256;
             if (idx < A_ITEMS) {
                 const int hp = idx >> 1, hh = idx & 1;
-                f32x4 lo4 = ra[v][0], hi4 = ra[v][1];
-                if ((avalid >> v) & 1u) {
-                    lo4 = act_apply4(lo4, sc, sh, cb + hh * 8);
-                    hi4 = act_apply4(hi4, sc, sh, cb + hh * 8 + 4);
-                }
+                f32x4 lo4 = act_reg4(ra[v][0], ract0, aon), hi4 = act_reg4(ra[v][1], ract1, aon);
+                if (!((avalid >> v) & 1u)) lo4 = hi4 = f32x4{0.f, 0.f, 0.f, 0.f};
                 const f32x8 x = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
                 u32x4 p0, p1, p2;
                 split3(x, p0, p1, p2);
@@ -174,7 +171,7 @@ __global__ void __launch_bounds__(256) conv3x3_fwd_x6_kernel(ConvFwdArgs a) {
         const int m = tile_pixel<TW, PERM16>(wm * 64 + mt * 32 + (lane & 31));
         aoff[mt] = hl * NHP + (m / TW) * HS + (m % TW);
     }
-    const int boff = hl * 9 * BN + wn * 32 + (lane & 31);
+    const int boff = hl * 3 * BN + wn * 32 + (lane & 31);
 
     auto ldfrag = [&](int t, u32x4 (&af)[MT][3], u32x4 (&bf)[3]) {
         const int toff = (t / 3) * HS + (t % 3);
@@ -182,7 +179,7 @@ __global__ void __launch_bounds__(256) conv3x3_fwd_x6_kernel(ConvFwdArgs a) {
         for (int q = 0; q < 3; ++q) {
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt) af[mt][q] = As[q * 2 * NHP + aoff[mt] + toff];
-            bf[q] = Bs[q * 2 * 9 * BN + boff + t * BN];
+            bf[q] = Bs[(((t / 3) * 3 + q) * 2) * 3 * BN + boff + (t % 3) * BN];
         }
     };
 
@@ -190,7 +187,7 @@ __global__ void __launch_bounds__(256) conv3x3_fwd_x6_kernel(ConvFwdArgs a) {
     lstore(0);
     __syncthreads();
     for (int c = 0; c < nchunk; ++c) {
-        if (c + 1 < nchunk) gload(c + 1);
+        if (c + 1 < nchunk && !(a.probe & 1)) gload(c + 1);
         u32x4 fa[2][MT][3], fb[2][3];
         ldfrag(0, fa[0], fb[0]);
 #pragma unroll
@@ -199,11 +196,181 @@ __global__ void __launch_bounds__(256) conv3x3_fwd_x6_kernel(ConvFwdArgs a) {
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt) acc[mt][0] = mfma_x6(fa[t & 1][mt], fb[t & 1], acc[mt][0]);
         }
+        if (a.probe & 2) continue;
         __syncthreads();
         if (c + 1 < nchunk) {
             lstore(c + 1);
             __syncthreads();
         }
+    }
+
+    conv_epilogue<TH, TW, BN, WM, WN, MT, NT, PERM16>(a, acc, reinterpret_cast<float*>(smem), tile,
+                                                      b, ty0, tx0, n0, wm, wn);
+}
+
+// ---------------------------------------------------------------------------
+// Pipelined form of the same forward: the K loop runs in stages of one kernel
+// row (3 taps x 16 channels, 36 MFMAs per wave).  The weight stage (18 KB) and
+// the activation halo are double-buffered in LDS (2 x 18 KB + 2 x 19.6 KB = 76 KB,
+// two blocks per CU), so the LDS writes for stage s+1 are issued right behind
+// stage s's MFMAs and each stage ends in ONE barrier with nothing left to stage.
+// Global loads run two stages (weights) / three stages (halo) ahead in registers.
+// ---------------------------------------------------------------------------
+template <int TH, int TW, bool PERM16>
+__global__ void __launch_bounds__(256) conv3x3_fwd_x6p_kernel(ConvFwdArgs a) {
+    constexpr int BN = 64, BKC = 16, WM = 2, WN = 2, MT = 2, NT = 1;
+    static_assert(TH * TW == 128, "tile must be 128 pixels");
+    constexpr int HWD = TW + 2;
+    constexpr int HS = PERM16 ? 24 : HWD;
+    constexpr int NHALO = (TH + 2) * HWD;
+    constexpr int NHP0 = (TH + 2) * HS;
+    constexpr int NHP = NHP0 + (12 - NHP0 % 8) % 8;
+    constexpr int A_ITEMS = NHALO * 2;
+    constexpr int A_PER = (A_ITEMS + 255) / 256;
+    constexpr int A_VECS = 6 * NHP;
+    constexpr int B_STAGE = 3 * 2 * 3 * BN;  // 16-B vectors of one kernel-row weight slab
+    constexpr int B_PER = (B_STAGE + 255) / 256;
+    __shared__ __attribute__((aligned(16))) u32x4 smem[2 * A_VECS + 2 * B_STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int NB = a.Cout / BN;
+    const int nb = blockIdx.x % NB, tile = blockIdx.x / NB;
+    const int n0 = nb * BN;
+    const int tpi = a.tiles_x * a.tiles_y;
+    const int b = tile / tpi, trem = tile % tpi;
+    const int ty0 = (trem / a.tiles_x) * TH, tx0 = (trem % a.tiles_x) * TW;
+    const int nchunk = a.Cin / BKC;
+    const int nstage = 3 * nchunk;
+    const u32x4* wbase = static_cast<const u32x4*>(a.wpk) + (size_t)nb * nchunk * 3 * B_STAGE;
+
+    f32x4 ra[A_PER][2];
+    unsigned avalid = 0;
+    Act4 ract0, ract1;
+    bool aon = false;
+    u32x4 rbn[B_PER], rbf[B_PER];  // weights of stage s+1 (landed) and s+2 (in flight)
+
+    auto gload_a = [&](int c) {
+        int cb = c * BKC;
+        const float* src = a.src0;
+        const float* sc = a.sc0;
+        const float* sh = a.sh0;
+        int Cs = a.C0;
+        if (cb >= a.C0) {
+            src = a.src1;
+            sc = a.sc1;
+            sh = a.sh1;
+            Cs = a.C1;
+            cb -= a.C0;
+        }
+        // this thread's channel half is fixed (hh = idx & 1 = tid & 1)
+        aon = sc != nullptr;
+        ract0 = act_load4(sc, sh, cb + (tid & 1) * 8);
+        ract1 = act_load4(sc, sh, cb + (tid & 1) * 8 + 4);
+        avalid = 0;
+        // branch-free: every lane loads from a clamped (valid) address and the halo
+        // mask is applied at LDS-store time, so no loaded register is merged at a
+        // join (which makes the compiler wait for the prefetch before the MFMAs)
+#pragma unroll
+        for (int v = 0; v < A_PER; ++v) {
+            const int idx = tid + v * 256;
+            const int hp = idx < A_ITEMS ? idx >> 1 : 0, hh = tid & 1;
+            const int gy = ty0 - 1 + hp / HWD, gx = tx0 - 1 + hp % HWD;
+            const bool ok = idx < A_ITEMS && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
+            const int cy = min(max(gy, 0), a.H - 1), cx = min(max(gx, 0), a.W - 1);
+            const float* p = src + ((size_t)(b * a.H + cy) * a.W + cx) * Cs + cb + hh * 8;
+            ra[v][0] = *reinterpret_cast<const f32x4*>(p);
+            ra[v][1] = *reinterpret_cast<const f32x4*>(p + 4);
+            avalid |= (ok ? 1u : 0u) << v;
+        }
+    };
+    auto lstore_a = [&](int c, u32x4* As) {
+        (void)c;
+#pragma unroll
+        for (int v = 0; v < A_PER; ++v) {
+            const int idx = tid + v * 256;
+            if (idx < A_ITEMS) {
+                const int hp = idx >> 1, hh = idx & 1;
+                f32x4 lo4 = act_reg4(ra[v][0], ract0, aon), hi4 = act_reg4(ra[v][1], ract1, aon);
+                if (!((avalid >> v) & 1u)) lo4 = hi4 = f32x4{0.f, 0.f, 0.f, 0.f};
+                const f32x8 x = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
+                u32x4 p0, p1, p2;
+                split3(x, p0, p1, p2);
+                const int hl = (hp / HWD) * HS + hp % HWD;
+                As[(0 * 2 + hh) * NHP + hl] = p0;
+                As[(1 * 2 + hh) * NHP + hl] = p1;
+                As[(2 * 2 + hh) * NHP + hl] = p2;
+            }
+        }
+    };
+    auto gload_b = [&](int s, u32x4 (&rb)[B_PER]) {
+        const u32x4* src = wbase + (size_t)s * B_STAGE;
+#pragma unroll
+        for (int v = 0; v < B_PER; ++v) rb[v] = src[min(tid + v * 256, B_STAGE - 1)];
+    };
+    auto lstore_b = [&](const u32x4 (&rb)[B_PER], u32x4* Bs) {
+#pragma unroll
+        for (int v = 0; v < B_PER; ++v) {
+            const int idx = tid + v * 256;
+            if (idx < B_STAGE) Bs[idx] = rb[v];
+        }
+    };
+
+    f32x16 acc[MT][NT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[mt][0][r] = 0.f;
+
+    const int hl = lane >> 5;
+    int aoff[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        const int m = tile_pixel<TW, PERM16>(wm * 64 + mt * 32 + (lane & 31));
+        aoff[mt] = hl * NHP + (m / TW) * HS + (m % TW);
+    }
+    const int boff = hl * 3 * BN + wn * 32 + (lane & 31);
+
+    // prologue: halo of chunk 0 and weights of stage 0 in LDS, stage 1 in registers
+    gload_a(0);
+    gload_b(0, rbf);
+    if (nstage > 1) gload_b(1, rbn);
+    lstore_a(0, smem);
+    lstore_b(rbf, smem + 2 * A_VECS);
+    __syncthreads();
+
+    for (int s = 0; s < nstage; ++s) {
+        const int c = s / 3, ky = s % 3;
+        if (s + 2 < nstage) gload_b(s + 2, rbf);
+        if (ky == 0 && c + 1 < nchunk) gload_a(c + 1);
+        const u32x4* As = smem + (c & 1) * A_VECS;
+        const u32x4* Bs = smem + 2 * A_VECS + (s & 1) * B_STAGE;
+        u32x4 fa[2][MT][3], fb[2][3];
+        auto ldfrag = [&](int kx, u32x4 (&af)[MT][3], u32x4 (&bf)[3]) {
+            const int toff = ky * HS + kx;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt) af[mt][q] = As[q * 2 * NHP + aoff[mt] + toff];
+                bf[q] = Bs[q * 2 * 3 * BN + boff + kx * BN];
+            }
+        };
+        ldfrag(0, fa[0], fb[0]);
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+            if (kx + 1 < 3) ldfrag(kx + 1, fa[(kx + 1) & 1], fb[(kx + 1) & 1]);
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+                acc[mt][0] = mfma_x6(fa[kx & 1][mt], fb[kx & 1], acc[mt][0]);
+        }
+        // stage s+1's weights into the other buffer (last read in stage s-1)
+        if (s + 1 < nstage) {
+            lstore_b(rbn, smem + 2 * A_VECS + ((s + 1) & 1) * B_STAGE);
+#pragma unroll
+            for (int v = 0; v < B_PER; ++v) rbn[v] = rbf[v];
+        }
+        if (ky == 2 && c + 1 < nchunk) lstore_a(c + 1, smem + ((c + 1) & 1) * A_VECS);
+        __syncthreads();
     }
 
     conv_epilogue<TH, TW, BN, WM, WN, MT, NT, PERM16>(a, acc, reinterpret_cast<float*>(smem), tile,
@@ -277,6 +444,8 @@ __global__ void __launch_bounds__(256, 2) conv3x3_wgrad_x6_kernel(WgradArgs a) {
         cbase = ci0 - a.C0;
     }
     const int tpi = a.tiles_x * a.tiles_y;
+    const Act4 xact = act_load4(xsc, xsh, cbase + (tid & 15) * 4);  // q = idx & 15 = tid & 15
+    const bool xon = xsc != nullptr;
 
     f32x4 rdy[DY_PER], rx[X_PER];
     unsigned xvalid = 0;
@@ -333,7 +502,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3_wgrad_x6_kernel(WgradArgs a) {
             const int idx = tid + v * 256;
             if (idx < X_Q) {
                 f32x4 val = rx[v];
-                if ((xvalid >> v) & 1u) val = act_apply4(val, xsc, xsh, cbase + (idx & 15) * 4);
+                if ((xvalid >> v) & 1u) val = act_reg4(val, xact, xon);
                 put(xs, idx >> 4, idx & 15, val);
             }
         }
@@ -404,24 +573,28 @@ void launch_wgrad_x6(const WgradArgs& a, unsigned grid, hipStream_t st) {
 
 // Weight pack for the split path.  mode 0 (forward): GEMM N = Cout, K channels =
 // Cin_pad; mode 1 (data gradient): N = Cin_pad, K channels = Cout, taps rotated
-// by 180 degrees.  Layout [N/64][K/16][piece][half][tap][64][8] bf16: the slab of
-// one (column block, chunk) is contiguous and equals the kernel's B LDS image.
+// by 180 degrees.  Layout [N/64][K/16][ky 3][piece 3][half 2][kx 3][64][8] bf16:
+// the slab of one (column block, chunk, kernel row) is contiguous (18 KB) and
+// equals one LDS weight stage of the kernels below.
 __global__ void pack_x6_kernel(const float* w, __bf16* wpk, int Cout, int Cin, int N, int K,
                                int mode) {
     const int nchunk = K / 16;
     const int64_t total = (int64_t)N * K * 9;
-    const int64_t plane = 9 * 64 * 8;  // one (piece, half) sub-slab
+    const int64_t plane = 3 * 64 * 8;  // one (ky, piece, half) sub-slab: kx x co x 8
     for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
          e += (int64_t)gridDim.x * blockDim.x) {
         const int j = (int)(e & 7);
         int64_t r = e >> 3;
         const int co = (int)(r % 64);
         r /= 64;
-        const int t = (int)(r % 9);
-        r /= 9;
+        const int kx = (int)(r % 3);
+        r /= 3;
         const int h = (int)(r % 2);
         r /= 2;
+        const int ky = (int)(r % 3);
+        r /= 3;
         const int chunk = (int)(r % nchunk), nb = (int)(r / nchunk);
+        const int t = ky * 3 + kx;
         const int n = nb * 64 + co, k = chunk * 16 + h * 8 + j;
         float v;
         if (mode == 0) v = k < Cin ? w[((size_t)n * Cin + k) * 9 + t] : 0.f;
@@ -430,8 +603,8 @@ __global__ void pack_x6_kernel(const float* w, __bf16* wpk, int Cout, int Cin, i
         const float r1 = v - (float)p0;
         const __bf16 p1 = (__bf16)r1;
         const __bf16 p2 = (__bf16)(r1 - (float)p1);
-        const size_t base = ((size_t)(nb * nchunk + chunk) * 3 * 2) * plane;
-        const size_t off = ((size_t)t * 64 + co) * 8 + j;
+        const size_t base = ((size_t)((nb * nchunk + chunk) * 3 + ky) * 3 * 2) * plane;
+        const size_t off = ((size_t)kx * 64 + co) * 8 + j;
         wpk[base + (0 * 2 + h) * plane + off] = p0;
         wpk[base + (1 * 2 + h) * plane + off] = p1;
         wpk[base + (2 * 2 + h) * plane + off] = p2;
@@ -441,12 +614,23 @@ __global__ void pack_x6_kernel(const float* w, __bf16* wpk, int Cout, int Cin, i
 int fwd_x6_tile_w(int W) { return W >= 32 ? 32 : 16; }
 int fwd_x6_tile_h(int W) { return W >= 32 ? 4 : 8; }
 
-void launch_fwd_x6(const ConvFwdArgs& a, hipStream_t st) {
+int g_x6_pipe = 1;
+int g_x6_probe = 0;  // tuning knob "x6_pipe": 1 = pipelined forward (default), 0 = single-stage
+
+void launch_fwd_x6(const ConvFwdArgs& a_in, hipStream_t st) {
+    ConvFwdArgs a = a_in;
+    a.probe = g_x6_probe;
     const unsigned grid = (unsigned)((int64_t)a.ntiles * (a.Cout / 64));
-    if (fwd_x6_tile_w(a.W) == 32)
+    const bool wide = fwd_x6_tile_w(a.W) == 32;
+    // (the 16-wide tile's padded halo makes its double-buffered form 84 KB = 1 block/CU,
+    // so narrow images keep the single-stage kernel)
+    if (g_x6_pipe && wide) {
+        hipLaunchKernelGGL((conv3x3_fwd_x6p_kernel<4, 32, false>), dim3(grid), dim3(256), 0, st, a);
+    } else if (wide) {
         hipLaunchKernelGGL((conv3x3_fwd_x6_kernel<4, 32, false>), dim3(grid), dim3(256), 0, st, a);
-    else
+    } else {
         hipLaunchKernelGGL((conv3x3_fwd_x6_kernel<8, 16, true>), dim3(grid), dim3(256), 0, st, a);
+    }
 }
 
 void launch_pack_x6(const float* w, void* wpk, int Cout, int Cin, int Cin_pad, int mode,

@@ -87,6 +87,12 @@ if _conv_math not in _MATHS:
     raise ValueError(f"UGPG_CONV_MATH must be one of {_MATHS}, got {_conv_math!r}")
 
 
+for _knob in ("x6_pipe", "fwd_cfg"):  # benchmarking knobs from the environment
+    _v = os.environ.get("UGPG_" + _knob.upper())
+    if _v is not None:
+        check(lib.ugpg_set_tuning(_knob.encode(), int(_v)), "set_tuning")
+
+
 def set_conv_math(math: str) -> None:
     """'x6': split-bf16 MFMA (fp32-accurate, 2.67x the fp32 MFMA rate) wherever the
     shape allows; 'f32': v_mfma_f32_32x32x2_f32 everywhere."""
