@@ -614,8 +614,12 @@ __global__ void pack_x6_kernel(const float* w, __bf16* wpk, int Cout, int Cin, i
 int fwd_x6_tile_w(int W) { return W >= 32 ? 32 : 16; }
 int fwd_x6_tile_h(int W) { return W >= 32 ? 4 : 8; }
 
-int g_x6_pipe = 1;
-int g_x6_probe = 0;  // tuning knob "x6_pipe": 1 = pipelined forward (default), 0 = single-stage
+// tuning knob "x6_pipe": 0 = single-stage (default), 1 = kernel-row pipelined.  Whole-step
+// A/B on MI355X (bench.py, 20 steps x 2 runs each): 653 vs 645 img/s -- the extra
+// barriers and the per-stage register hand-off cost more than the staging overlap
+// buys at two blocks per CU.
+int g_x6_pipe = 0;
+int g_x6_probe = 0;  // "x6_probe": timing diagnostics (see ugpg_set_tuning)
 
 void launch_fwd_x6(const ConvFwdArgs& a_in, hipStream_t st) {
     ConvFwdArgs a = a_in;
