@@ -87,7 +87,8 @@ typedef struct {
 
 /* Replaces aten::convolution forward (cuDNN/oneDNN) for DoubleConv's 3x3 convs. */
 int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream);
-/* number of BatchNorm partial tiles the forward writes (size stats as 3*Cout*ntiles) */
+/* number of BatchNorm partial slots the forward writes (size stats as 3*Cout*ntiles);
+ * depends on the forward kernel form (tuning knob "x6_pipe") */
 int ugpg_conv3x3_fwd_ntiles(int B, int H, int W, int Cin, int Cout, int wfmt);
 
 /* Weight repack from OIHW fp32 [Cout][Cin][3][3].

@@ -57,13 +57,22 @@ CONV_CASES = [
 BIG = {5, 6, 7}
 
 
-@pytest.fixture(params=["x6", "f32"])
+# x6 forward/dgrad kernel forms (tuning knob "x6_pipe"): 1 = persistent double-buffered
+# warp-specialized (default), 0 = single-stage
+X6_FORMS = {"x6": 1, "x6s": 0}
+
+
+@pytest.fixture(params=["x6", "x6s", "f32"])
 def math(request):
-    """Both conv arithmetic forms: split-bf16 (default) and fp32 MFMA."""
+    """Both conv arithmetic forms: split-bf16 (default, every forward kernel form)
+    and fp32 MFMA."""
     from ugpg import ops
+    from ugpg._C import lib
     old = ops.conv_math()
-    ops.set_conv_math(request.param)
+    ops.set_conv_math("f32" if request.param == "f32" else "x6")
+    lib.ugpg_set_tuning(b"x6_pipe", X6_FORMS.get(request.param, 1))
     yield request.param
+    lib.ugpg_set_tuning(b"x6_pipe", 1)
     ops.set_conv_math(old)
 
 
@@ -92,7 +101,7 @@ def test_conv3x3_fwd_stats(dev, case, math):
         srcs.append(ops.Act(nhwc(x1).to(dev), g(sc1), g(sh1)))
     wpk = ops.pack_conv3x3(w.to(dev), cin, 0)
     out = torch.empty(B, H, W, Cout, device=dev)
-    assert wpk.ugpg_fmt == (ops.WFMT_X6 if math == "x6" and cin % 16 == 0 else ops.WFMT_F32)
+    assert wpk.ugpg_fmt == (ops.WFMT_X6 if math != "f32" and cin % 16 == 0 else ops.WFMT_F32)
     nt = ops.conv_ntiles(B, H, W, cin, Cout, wpk)
     stats = torch.empty(3 * Cout * nt, device=dev)
     ops.conv3x3_fwd(srcs, wpk, b.to(dev), Cout, [out], stats=stats)

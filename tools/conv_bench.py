@@ -46,11 +46,15 @@ def main():
     ap.add_argument("--maths", default="x6,f32")
     ap.add_argument("--pipes", default="1", help="x6 forward forms to time (x6_pipe knob)")
     ap.add_argument("--wgrad", action="store_true")
+    ap.add_argument("--layers", default="", help="comma-separated layer names (default: all)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     cfgs = [int(c) for c in a.cfgs.split(",")]
     rows = {}
+    sel = set(a.layers.split(",")) if a.layers else None
     for name, H, C0, C1, Cout in LAYERS:
+        if sel and name not in sel:
+            continue
         cin = C0 + C1
         real_cin = 3 if cin == 8 else cin
         srcs = [ops.Act(torch.randn(B, H, H, C0, device=dev),

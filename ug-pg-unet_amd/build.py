@@ -47,42 +47,50 @@ def _newest_header() -> float:
 PER_FILE = {"ops.hip": ["-ffp-contract=off"]}
 
 
-def _compile(src: Path, force: bool) -> Path:
-    obj = BUILD / (src.stem + ".o")
+def _compile(src: Path, force: bool, bdir: Path = BUILD, defines=()) -> Path:
+    obj = bdir / (src.stem + ".o")
     if not force and obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime, _newest_header()):
         return obj
-    cmd = [_hipcc(), *FLAGS, *PER_FILE.get(src.name, []), "-c", str(src), "-o", str(obj)]
+    cmd = [_hipcc(), *FLAGS, *PER_FILE.get(src.name, []), *[f"-D{d}" for d in defines], "-c",
+           str(src), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr}")
     return obj
 
 
-def build(force: bool = False, verbose: bool = True) -> Path:
-    BUILD.mkdir(exist_ok=True)
+def build(force: bool = False, verbose: bool = True, defines=(), out: Path | None = None) -> Path:
+    """Build libugpg.so; `defines`/`out` build an experimental variant (its own object
+    directory) for A/B timing via UGPG_LIB."""
+    lib = Path(out) if out else LIB
+    bdir = BUILD if not defines else BUILD / ("v_" + "_".join(d.replace("=", "") for d in defines))
+    bdir.mkdir(parents=True, exist_ok=True)
     srcs = _sources()
     jobs = min(len(srcs), int(os.environ.get("MAX_JOBS", "8")))
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        objs = list(ex.map(lambda s: _compile(s, force), srcs))
+        objs = list(ex.map(lambda s: _compile(s, force, bdir, defines), srcs))
     newest = max(o.stat().st_mtime for o in objs)
-    if force or not LIB.exists() or LIB.stat().st_mtime < newest:
-        tmp = LIB.with_suffix(".so.tmp")
+    LIB_ = lib
+    if force or not LIB_.exists() or LIB_.stat().st_mtime < newest:
+        tmp = LIB_.with_suffix(".so.tmp")
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr}")
-        os.replace(tmp, LIB)
+        os.replace(tmp, LIB_)
     if verbose:
-        print(f"built {LIB} ({LIB.stat().st_size / 1e6:.1f} MB)")
-    return LIB
+        print(f"built {LIB_} ({LIB_.stat().st_size / 1e6:.1f} MB)")
+    return LIB_
 
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
+    ap.add_argument("-D", dest="defines", action="append", default=[], help="experimental define")
+    ap.add_argument("--out", default=None, help="output .so (experimental variants)")
     a = ap.parse_args()
     try:
-        build(force=a.force)
+        build(force=a.force, defines=tuple(a.defines), out=a.out)
     except RuntimeError as e:
         print(e, file=sys.stderr)
         sys.exit(1)

@@ -630,7 +630,7 @@ extern "C" int ugpg_set_tuning(const char* key, int value) {
 extern "C" int ugpg_conv3x3_fwd_ntiles(int B, int H, int W, int Cin, int Cout, int wfmt) {
     (void)Cin;
     if (wfmt == UGPG_WFMT_X6)
-        return (int)(B * cdiv(H, fwd_x6_tile_h(W)) * cdiv(W, fwd_x6_tile_w(W)));
+        return fwd_x6_stat_slots((int)(B * cdiv(H, fwd_x6_tile_h(W)) * cdiv(W, fwd_x6_tile_w(W))), W);
     const int cfg = pick_fwd_cfg(B, H, W, Cout, Cout);
     return (int)(B * cdiv(H, kFwd[cfg].th) * cdiv(W, kFwd[cfg].tw));
 }

@@ -164,6 +164,7 @@ void launch_fwd_x6(const ConvFwdArgs& a, hipStream_t st);
 extern int g_x6_pipe, g_x6_probe;
 int fwd_x6_tile_w(int W);  // 32 or 16
 int fwd_x6_tile_h(int W);  // 4 or 8
+int fwd_x6_stat_slots(int ntiles, int W);  // BatchNorm partial slots the forward writes
 void launch_wgrad_x6(const WgradArgs& a, unsigned grid, hipStream_t st);
 constexpr int WGX6_TH = 2, WGX6_TW = 16;  // pixel tile of the split-bf16 wgrad
 void launch_pack_x6(const float* w, void* wpk, int Cout, int Cin, int Cin_pad, int mode,

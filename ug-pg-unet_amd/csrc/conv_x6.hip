@@ -26,6 +26,9 @@
 // Both fragment reads are single ds_read_b128 per (piece, tile) and conflict-free:
 // a 16-lane read group touches 16 distinct 16-B bank slots (32-wide tile: one
 // image row; 16-wide tile: permuted rows, see tile_pixel<16, true>, with HS=24).
+#include <algorithm>
+#include <type_traits>
+
 #include "conv_common.h"
 
 namespace ugpg {
@@ -43,6 +46,26 @@ __device__ __forceinline__ void split3(f32x8 v, u32x4& p0, u32x4& p1, u32x4& p2)
     p0 = __builtin_bit_cast(u32x4, h);
     p1 = __builtin_bit_cast(u32x4, m);
     p2 = __builtin_bit_cast(u32x4, l);
+}
+
+// identity lazy-activation coefficients (for sources stored already activated)
+__device__ const float g_act_ones[1024] = {
+#define UGPG_ONE8 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f
+#define UGPG_ONE64 UGPG_ONE8, UGPG_ONE8, UGPG_ONE8, UGPG_ONE8, UGPG_ONE8, UGPG_ONE8, UGPG_ONE8, UGPG_ONE8
+    UGPG_ONE64, UGPG_ONE64, UGPG_ONE64, UGPG_ONE64, UGPG_ONE64, UGPG_ONE64, UGPG_ONE64, UGPG_ONE64,
+    UGPG_ONE64, UGPG_ONE64, UGPG_ONE64, UGPG_ONE64, UGPG_ONE64, UGPG_ONE64, UGPG_ONE64, UGPG_ONE64};
+#undef UGPG_ONE64
+#undef UGPG_ONE8
+__device__ const float g_act_zeros[1024] = {0.f};
+
+// max(scale*v + shift, floor): the lazy BatchNorm+ReLU with floor 0, the identity
+// with scale 1, shift 0, floor -inf (no branch on whether the source has one)
+__device__ __forceinline__ f32x4 act_floor4(f32x4 v, const Act4& a, float lo) {
+    v.x = fmaxf(fmaf(v.x, a.s.x, a.h.x), lo);
+    v.y = fmaxf(fmaf(v.y, a.s.y, a.h.y), lo);
+    v.z = fmaxf(fmaf(v.z, a.s.z, a.h.z), lo);
+    v.w = fmaxf(fmaf(v.w, a.s.w, a.h.w), lo);
+    return v;
 }
 
 __device__ __forceinline__ f32x16 mfma16(u32x4 a, u32x4 b, f32x16 c) {
@@ -209,172 +232,320 @@ __global__ void __launch_bounds__(256) conv3x3_fwd_x6_kernel(ConvFwdArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Pipelined form of the same forward: the K loop runs in stages of one kernel
-// row (3 taps x 16 channels, 36 MFMAs per wave).  The weight stage (18 KB) and
-// the activation halo are double-buffered in LDS (2 x 18 KB + 2 x 19.6 KB = 76 KB,
-// two blocks per CU), so the LDS writes for stage s+1 are issued right behind
-// stage s's MFMAs and each stage ends in ONE barrier with nothing left to stage.
-// Global loads run two stages (weights) / three stages (halo) ahead in registers.
+// Persistent, warp-specialized form of the same forward for images >= 32 wide
+// ("x6r").  One 8-wave workgroup per CU; a work item is an 8 x 32 = 256-pixel tile
+// x 64 output channels (twice the pixels of conv3x3_fwd_x6_kernel, so each weight
+// byte staged through the CU feeds twice the MFMAs -- the per-CU L2->LDS weight
+// stream is what bounds the single-stage kernel).  Waves 0-3 only read fragments
+// and issue MFMAs (2 pixel halves x 2 column halves, each 128 px x 32 co = four
+// 32x32 accumulators); waves 4-7 only stage.  The K loop runs per 16-channel
+// chunk ("step") in three phases, one per kernel row ky: the halo is double-
+// buffered per step (2 x 33 KB) and the weights go through a ring of four
+// kernel-row slots (4 x 18 KB), so the loaders write row r of step k+1 while
+// row r of step k is being computed, with one barrier per phase.  Items are
+// walked per XCD as contiguous ranges (column blocks of one tile share the halo
+// in one L2).  Epilogue per wave, no barriers: BatchNorm partials per (tile,
+// pixel half), i.e. 2 stat slots per tile.
 // ---------------------------------------------------------------------------
-template <int TH, int TW, bool PERM16>
-__global__ void __launch_bounds__(256) conv3x3_fwd_x6p_kernel(ConvFwdArgs a) {
-    constexpr int BN = 64, BKC = 16, WM = 2, WN = 2, MT = 2, NT = 1;
-    static_assert(TH * TW == 128, "tile must be 128 pixels");
-    constexpr int HWD = TW + 2;
-    constexpr int HS = PERM16 ? 24 : HWD;
-    constexpr int NHALO = (TH + 2) * HWD;
-    constexpr int NHP0 = (TH + 2) * HS;
-    constexpr int NHP = NHP0 + (12 - NHP0 % 8) % 8;
-    constexpr int A_ITEMS = NHALO * 2;
-    constexpr int A_PER = (A_ITEMS + 255) / 256;
+// 16-byte global load the compiler does not track: the caller waits for it with an
+// explicit counted s_waitcnt vmcnt (vm_wait), which is followed by a scheduling
+// fence.  The loader waves use it so that their loads stay in flight across
+// barriers and loop iterations (hipcc's own waitcnt placement drains all loads at
+// loop headers).
+__device__ __forceinline__ f32x4 gld16(const void* p) {
+    f32x4 r;
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p));
+    return r;
+}
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+// LDS writes complete, then a workgroup barrier that does not wait for global loads
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// per-wave epilogue: bias, (dual-destination, accumulate-capable) store, and the
+// wave's BatchNorm partial (count, sum, M2) over its MT*32 pixels x 32 channels into
+// slot 2*tile + wm (stat slots = 2 * ntiles)
+template <int TH, int TW, int MT>
+__device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&acc)[MT], int tile,
+                                                 int b, int ty0, int tx0, int n0, int wm, int wn) {
+    const int lane = threadIdx.x & 63;
+    const int vh = min(TH, a.H - ty0), vw = min(TW, a.W - tx0);
+    float* out;
+    int ostride, ocol0, oacc;
+    if (n0 < a.split) {
+        out = a.out0;
+        ostride = a.split;
+        ocol0 = n0;
+        oacc = a.acc0;
+    } else {
+        out = a.out1;
+        ostride = a.Cout - a.split;
+        ocol0 = n0 - a.split;
+        oacc = a.acc1;
+    }
+    const int nl = wn * 32 + (lane & 31);
+    const float bv = a.bias ? a.bias[n0 + nl] : 0.f;
+    float psum = 0.f;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = wm * MT * 32 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            const int py = m / TW, px = m % TW;
+            const float v = acc[mt][r] + bv;
+            acc[mt][r] = v;
+            if (py < vh && px < vw) {
+                const size_t o = ((size_t)(b * a.H + ty0 + py) * a.W + tx0 + px) * ostride + ocol0 + nl;
+                out[o] = oacc ? out[o] + v : v;
+                psum += v;
+            }
+        }
+    if (a.stats == nullptr) return;
+    constexpr int WROWS = MT * 32 / TW;  // image rows of one wave's pixels
+    const int rows = min(max(vh - wm * WROWS, 0), WROWS);
+    const float cnt = (float)(rows * vw);
+    const float s = psum + __shfl_xor(psum, 32, 64);
+    const float mu = cnt > 0.f ? s / cnt : 0.f;
+    float q = 0.f;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = wm * MT * 32 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            if (m / TW < vh && m % TW < vw) {
+                const float d = acc[mt][r] - mu;
+                q = fmaf(d, d, q);
+            }
+        }
+    q += __shfl_xor(q, 32, 64);
+    if (lane < 32) {
+        const size_t n = n0 + nl, S = 2 * (size_t)a.ntiles, slot = 2 * (size_t)tile + wm;
+        a.stats[(0 * (size_t)a.Cout + n) * S + slot] = cnt;
+        a.stats[(1 * (size_t)a.Cout + n) * S + slot] = s;
+        a.stats[(2 * (size_t)a.Cout + n) * S + slot] = q;
+    }
+}
+
+__global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) {
+    constexpr int TH = 8, TW = 32, BN = 64, BKC = 16, MT = 4;
+    constexpr int HWD = TW + 2, HS = HWD;
+    constexpr int NHALO = (TH + 2) * HWD;                   // 340 halo pixels
+    constexpr int NHP = NHALO + 1 + (11 - NHALO % 8) % 8;   // 348: spare slot NHALO, = 4 (mod 8)
+    constexpr int A_ITEMS = NHALO * 2;                      // (pixel, channel half)
+    constexpr int A_PER = (A_ITEMS + 255) / 256;            // 3
     constexpr int A_VECS = 6 * NHP;
-    constexpr int B_STAGE = 3 * 2 * 3 * BN;  // 16-B vectors of one kernel-row weight slab
-    constexpr int B_PER = (B_STAGE + 255) / 256;
-    __shared__ __attribute__((aligned(16))) u32x4 smem[2 * A_VECS + 2 * B_STAGE];
+    constexpr int R_VEC = 3 * 2 * 3 * BN;                   // one kernel row of weights: 1152
+    constexpr int R_PER = (R_VEC + 255) / 256;              // 5 (the last one half-used)
+    constexpr int R_STR = R_VEC;                            // ring slot pitch
+    constexpr int NSLOT = 4;
+    __shared__ __attribute__((aligned(16))) u32x4 smem[2 * A_VECS + NSLOT * R_STR + 1];
+    u32x4* const Bring = smem + 2 * A_VECS;
+    u32x4* const dummy = smem + 2 * A_VECS + NSLOT * R_STR;  // writes of idle lanes
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave / WN, wn = wave % WN;
+    const bool loader = wave >= 4;
     const int NB = a.Cout / BN;
-    const int nb = blockIdx.x % NB, tile = blockIdx.x / NB;
-    const int n0 = nb * BN;
-    const int tpi = a.tiles_x * a.tiles_y;
-    const int b = tile / tpi, trem = tile % tpi;
-    const int ty0 = (trem / a.tiles_x) * TH, tx0 = (trem % a.tiles_x) * TW;
+    const int nitems = a.ntiles * NB;
+    const int nslots = gridDim.x >> 3;
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    const int iq = nitems >> 3, ir = nitems & 7;
+    const int ibeg = xcd * iq + min(xcd, ir);
+    const int iend = ibeg + iq + (xcd < ir ? 1 : 0);
+    const int item0 = ibeg + slot;
+    if (item0 >= iend) return;  // uniform per workgroup
     const int nchunk = a.Cin / BKC;
-    const int nstage = 3 * nchunk;
-    const u32x4* wbase = static_cast<const u32x4*>(a.wpk) + (size_t)nb * nchunk * 3 * B_STAGE;
+    const int total = (iend - item0 + nslots - 1) / nslots * nchunk;  // steps of this workgroup
+    const int last = total - 1;
+    const int tpi = a.tiles_x * a.tiles_y;
 
-    f32x4 ra[A_PER][2];
-    unsigned avalid = 0;
-    Act4 ract0, ract1;
-    bool aon = false;
-    u32x4 rbn[B_PER], rbf[B_PER];  // weights of stage s+1 (landed) and s+2 (in flight)
-
-    auto gload_a = [&](int c) {
-        int cb = c * BKC;
-        const float* src = a.src0;
-        const float* sc = a.sc0;
-        const float* sh = a.sh0;
-        int Cs = a.C0;
-        if (cb >= a.C0) {
-            src = a.src1;
-            sc = a.sc1;
-            sh = a.sh1;
-            Cs = a.C1;
-            cb -= a.C0;
-        }
-        // this thread's channel half is fixed (hh = idx & 1 = tid & 1)
-        aon = sc != nullptr;
-        ract0 = act_load4(sc, sh, cb + (tid & 1) * 8);
-        ract1 = act_load4(sc, sh, cb + (tid & 1) * 8 + 4);
-        avalid = 0;
-        // branch-free: every lane loads from a clamped (valid) address and the halo
-        // mask is applied at LDS-store time, so no loaded register is merged at a
-        // join (which makes the compiler wait for the prefetch before the MFMAs)
-#pragma unroll
-        for (int v = 0; v < A_PER; ++v) {
-            const int idx = tid + v * 256;
-            const int hp = idx < A_ITEMS ? idx >> 1 : 0, hh = tid & 1;
-            const int gy = ty0 - 1 + hp / HWD, gx = tx0 - 1 + hp % HWD;
-            const bool ok = idx < A_ITEMS && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
-            const int cy = min(max(gy, 0), a.H - 1), cx = min(max(gx, 0), a.W - 1);
-            const float* p = src + ((size_t)(b * a.H + cy) * a.W + cx) * Cs + cb + hh * 8;
-            ra[v][0] = *reinterpret_cast<const f32x4*>(p);
-            ra[v][1] = *reinterpret_cast<const f32x4*>(p + 4);
-            avalid |= (ok ? 1u : 0u) << v;
-        }
+    struct Pos {
+        int b, ty0, tx0, nb, tile;
     };
-    auto lstore_a = [&](int c, u32x4* As) {
-        (void)c;
+    auto pos_of = [&](int it) {
+        Pos p;
+        p.nb = it % NB;
+        p.tile = it / NB;
+        p.b = p.tile / tpi;
+        const int trem = p.tile % tpi;
+        p.ty0 = (trem / a.tiles_x) * TH;
+        p.tx0 = (trem % a.tiles_x) * TW;
+        return p;
+    };
+
+    if (loader) {
+        // ------------------------------------------------------------ loader waves
+        // per step k:  phase 0: write halo(k+1) and weight row 0 of k+1, load row 1 of
+        // k+1 and halo(k+2);  phase 1: write row 1, load row 2;  phase 2: write row 2,
+        // load row 0 of k+2.  Row r of step j goes to ring slot (3j + r) % 4.
+        const int lt = tid - 256;
+        f32x4 ra[A_PER][2];
+        unsigned avalid = 0;
+        Act4 r0, r1;
+        float lo = 0.f;
+        u32x4 rb[R_PER];
+        auto load_halo = [&](int k) {
+            k = min(k, last);
+            const int c = k % nchunk;
+            const Pos p = pos_of(item0 + (k / nchunk) * nslots);
+            const int cb0 = c * BKC;
+            const bool second = cb0 >= a.C0;
+            const float* src = second ? a.src1 : a.src0;
+            const float* sc = second ? a.sc1 : a.sc0;
+            const float* sh = second ? a.sh1 : a.sh0;
+            const int Cs = second ? a.C1 : a.C0;
+            const int cb = second ? cb0 - a.C0 : cb0;
+            const bool aon = sc != nullptr;
+            const float* scp = aon ? sc : g_act_ones;  // identity coefficients without activation
+            const float* shp = aon ? sh : g_act_zeros;
+            lo = aon ? 0.f : -INFINITY;
+            const int cc = cb + (lt & 1) * 8;
+            r0.s = gld16(scp + cc);
+            r0.h = gld16(shp + cc);
+            r1.s = gld16(scp + cc + 4);
+            r1.h = gld16(shp + cc + 4);
+            avalid = 0;
 #pragma unroll
-        for (int v = 0; v < A_PER; ++v) {
-            const int idx = tid + v * 256;
-            if (idx < A_ITEMS) {
+            for (int v = 0; v < A_PER; ++v) {
+                const int idx = lt + v * 256;
+                const int hp = idx < A_ITEMS ? idx >> 1 : 0, hh = lt & 1;
+                const int gy = p.ty0 - 1 + hp / HWD, gx = p.tx0 - 1 + hp % HWD;
+                const bool ok = idx < A_ITEMS && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
+                const int cy = min(max(gy, 0), a.H - 1), cx = min(max(gx, 0), a.W - 1);
+                const float* q = src + ((size_t)(p.b * a.H + cy) * a.W + cx) * Cs + cb + hh * 8;
+                ra[v][0] = gld16(q);
+                ra[v][1] = gld16(q + 4);
+                avalid |= (ok ? 1u : 0u) << v;
+            }
+        };
+        constexpr int HALO_LOADS = 4 + 2 * A_PER;
+        auto store_halo = [&](int k) {
+            u32x4* As = smem + (k & 1) * A_VECS;
+#pragma unroll
+            for (int v = 0; v < A_PER; ++v) {
+                const int idx = lt + v * 256;
                 const int hp = idx >> 1, hh = idx & 1;
-                f32x4 lo4 = act_reg4(ra[v][0], ract0, aon), hi4 = act_reg4(ra[v][1], ract1, aon);
-                if (!((avalid >> v) & 1u)) lo4 = hi4 = f32x4{0.f, 0.f, 0.f, 0.f};
-                const f32x8 x = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
+                const f32x4 lo4 = act_floor4(ra[v][0], r0, lo), hi4 = act_floor4(ra[v][1], r1, lo);
+                const bool ok = (avalid >> v) & 1u;
+                const f32x8 x = {ok ? lo4.x : 0.f, ok ? lo4.y : 0.f, ok ? lo4.z : 0.f,
+                                 ok ? lo4.w : 0.f, ok ? hi4.x : 0.f, ok ? hi4.y : 0.f,
+                                 ok ? hi4.z : 0.f, ok ? hi4.w : 0.f};
                 u32x4 p0, p1, p2;
                 split3(x, p0, p1, p2);
-                const int hl = (hp / HWD) * HS + hp % HWD;
+                const int hl = idx < A_ITEMS ? (hp / HWD) * HS + hp % HWD : NHALO;
                 As[(0 * 2 + hh) * NHP + hl] = p0;
                 As[(1 * 2 + hh) * NHP + hl] = p1;
                 As[(2 * 2 + hh) * NHP + hl] = p2;
             }
-        }
-    };
-    auto gload_b = [&](int s, u32x4 (&rb)[B_PER]) {
-        const u32x4* src = wbase + (size_t)s * B_STAGE;
+        };
+        auto load_row = [&](int k, int ky) {
+            k = min(k, last);
+            const int c = k % nchunk;
+            const int nb = (item0 + (k / nchunk) * nslots) % NB;
+            const u32x4* ws =
+                static_cast<const u32x4*>(a.wpk) + (((size_t)nb * nchunk + c) * 3 + ky) * R_VEC;
 #pragma unroll
-        for (int v = 0; v < B_PER; ++v) rb[v] = src[min(tid + v * 256, B_STAGE - 1)];
-    };
-    auto lstore_b = [&](const u32x4 (&rb)[B_PER], u32x4* Bs) {
+            for (int v = 0; v < R_PER; ++v)
+                rb[v] = __builtin_bit_cast(u32x4, gld16(ws + min(lt + v * 256, R_VEC - 1)));
+        };
+        auto store_row = [&](int k, int ky) {
+            u32x4* Bs = Bring + ((3 * k + ky) % NSLOT) * R_STR;
 #pragma unroll
-        for (int v = 0; v < B_PER; ++v) {
-            const int idx = tid + v * 256;
-            if (idx < B_STAGE) Bs[idx] = rb[v];
+            for (int v = 0; v < R_PER; ++v) {
+                const int idx = lt + v * 256;
+                *(idx < R_VEC ? Bs + idx : dummy) = rb[v];
+            }
+        };
+        // prologue: step 0 complete in LDS (halo buffer 0, rows in slots 0-2)
+        load_halo(0);
+        vm_wait<0>();
+        store_halo(0);
+#pragma unroll 1
+        for (int ky = 0; ky < 3; ++ky) {
+            load_row(0, ky);
+            vm_wait<0>();
+            store_row(0, ky);
         }
-    };
+        load_row(1, 0);
+        load_halo(1);
+        lds_barrier();
+        for (int k = 0; k < total; ++k) {
+            // phase 0
+            vm_wait<0>();
+            store_halo(k + 1);
+            store_row(k + 1, 0);
+            load_row(k + 1, 1);
+            load_halo(k + 2);
+            lds_barrier();
+            // phase 1
+            vm_wait<HALO_LOADS>();
+            store_row(k + 1, 1);
+            load_row(k + 1, 2);
+            lds_barrier();
+            // phase 2
+            vm_wait<0>();
+            store_row(k + 1, 2);
+            load_row(k + 2, 0);
+            lds_barrier();
+        }
+        vm_wait<0>();  // no load outlives the workgroup
+        return;
+    }
 
-    f32x16 acc[MT][NT];
+    // ---------------------------------------------------------------- compute waves
+    const int wm = wave >> 1, wn = wave & 1;
+    f32x16 acc[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[mt][0][r] = 0.f;
-
+        for (int r = 0; r < 16; ++r) acc[mt][r] = 0.f;
     const int hl = lane >> 5;
-    int aoff[MT];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-        const int m = tile_pixel<TW, PERM16>(wm * 64 + mt * 32 + (lane & 31));
-        aoff[mt] = hl * NHP + (m / TW) * HS + (m % TW);
-    }
+    const int aoff = hl * NHP + (wm * MT) * HS + (lane & 31);  // + mt*HS + ky*HS + kx
     const int boff = hl * 3 * BN + wn * 32 + (lane & 31);
-
-    // prologue: halo of chunk 0 and weights of stage 0 in LDS, stage 1 in registers
-    gload_a(0);
-    gload_b(0, rbf);
-    if (nstage > 1) gload_b(1, rbn);
-    lstore_a(0, smem);
-    lstore_b(rbf, smem + 2 * A_VECS);
-    __syncthreads();
-
-    for (int s = 0; s < nstage; ++s) {
-        const int c = s / 3, ky = s % 3;
-        if (s + 2 < nstage) gload_b(s + 2, rbf);
-        if (ky == 0 && c + 1 < nchunk) gload_a(c + 1);
-        const u32x4* As = smem + (c & 1) * A_VECS;
-        const u32x4* Bs = smem + 2 * A_VECS + (s & 1) * B_STAGE;
-        u32x4 fa[2][MT][3], fb[2][3];
-        auto ldfrag = [&](int kx, u32x4 (&af)[MT][3], u32x4 (&bf)[3]) {
-            const int toff = ky * HS + kx;
+    auto ldfrag = [&](const u32x4* As, const u32x4* Bs, int ky, int kx, u32x4 (&af)[MT][3],
+                      u32x4 (&bf)[3]) {
 #pragma unroll
-            for (int q = 0; q < 3; ++q) {
+        for (int q = 0; q < 3; ++q) {
 #pragma unroll
-                for (int mt = 0; mt < MT; ++mt) af[mt][q] = As[q * 2 * NHP + aoff[mt] + toff];
-                bf[q] = Bs[q * 2 * 3 * BN + boff + kx * BN];
+            for (int mt = 0; mt < MT; ++mt) af[mt][q] = As[q * 2 * NHP + aoff + (mt + ky) * HS + kx];
+            bf[q] = Bs[q * 2 * 3 * BN + boff + kx * BN];
+        }
+    };
+    lds_barrier();  // step 0 staged
+    int cc = 0, item = item0;
+    Pos cp = pos_of(item0);
+    for (int k = 0; k < total; ++k) {
+        const u32x4* Ac = smem + (k & 1) * A_VECS;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+            const u32x4* Bc = Bring + ((3 * k + ky) % NSLOT) * R_STR;
+            u32x4 fa[2][MT][3], fb[2][3];
+            ldfrag(Ac, Bc, ky, 0, fa[0], fb[0]);
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+                if (kx + 1 < 3) ldfrag(Ac, Bc, ky, kx + 1, fa[(kx + 1) & 1], fb[(kx + 1) & 1]);
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma_x6(fa[kx & 1][mt], fb[kx & 1], acc[mt]);
             }
-        };
-        ldfrag(0, fa[0], fb[0]);
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-            if (kx + 1 < 3) ldfrag(kx + 1, fa[(kx + 1) & 1], fb[(kx + 1) & 1]);
+            lds_barrier();
+        }
+        if (++cc == nchunk) {
+            x6_epilogue_wave<TH, TW, MT>(a, acc, cp.tile, cp.b, cp.ty0, cp.tx0, cp.nb * BN, wm, wn);
+            cc = 0;
+            item += nslots;
+            if (item < iend) cp = pos_of(item);
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt)
-                acc[mt][0] = mfma_x6(fa[kx & 1][mt], fb[kx & 1], acc[mt][0]);
-        }
-        // stage s+1's weights into the other buffer (last read in stage s-1)
-        if (s + 1 < nstage) {
-            lstore_b(rbn, smem + 2 * A_VECS + ((s + 1) & 1) * B_STAGE);
 #pragma unroll
-            for (int v = 0; v < B_PER; ++v) rbn[v] = rbf[v];
+                for (int r = 0; r < 16; ++r) acc[mt][r] = 0.f;
         }
-        if (ky == 2 && c + 1 < nchunk) lstore_a(c + 1, smem + ((c + 1) & 1) * A_VECS);
-        __syncthreads();
     }
-
-    conv_epilogue<TH, TW, BN, WM, WN, MT, NT, PERM16>(a, acc, reinterpret_cast<float*>(smem), tile,
-                                                      b, ty0, tx0, n0, wm, wn);
 }
 
 // ---------------------------------------------------------------------------
@@ -611,26 +782,48 @@ __global__ void pack_x6_kernel(const float* w, __bf16* wpk, int Cout, int Cin, i
     }
 }
 
+int g_x6_pipe = 1;   // tuning knob "x6_pipe" (see launch_fwd_x6)
+static bool use_x6r(int W) { return g_x6_pipe && W >= 32; }
 int fwd_x6_tile_w(int W) { return W >= 32 ? 32 : 16; }
-int fwd_x6_tile_h(int W) { return W >= 32 ? 4 : 8; }
+int fwd_x6_tile_h(int W) { return use_x6r(W) ? 8 : (W >= 32 ? 4 : 8); }
+int fwd_x6_stat_slots(int ntiles, int W) { return use_x6r(W) ? 2 * ntiles : ntiles; }
 
-// tuning knob "x6_pipe": 0 = single-stage (default), 1 = kernel-row pipelined.  Whole-step
-// A/B on MI355X (bench.py, 20 steps x 2 runs each): 653 vs 645 img/s -- the extra
-// barriers and the per-stage register hand-off cost more than the staging overlap
-// buys at two blocks per CU.
-int g_x6_pipe = 0;
+// tuning knob "x6_pipe": 1 = conv3x3_fwd_x6r_kernel for images >= 32 wide (default),
+// 0 = conv3x3_fwd_x6_kernel everywhere
 int g_x6_probe = 0;  // "x6_probe": timing diagnostics (see ugpg_set_tuning)
+
+// compute units of the stream's device (cached per device)
+static int cu_count(hipStream_t st) {
+    static int cache[64] = {0};
+    int dev = 0;
+    if (hipStreamGetDevice(st, &dev) != hipSuccess || dev < 0 || dev >= 64) {
+        (void)hipGetLastError();
+        if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    }
+    if (!cache[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            n <= 0)
+            n = 256;
+        cache[dev] = n;
+    }
+    return cache[dev];
+}
 
 void launch_fwd_x6(const ConvFwdArgs& a_in, hipStream_t st) {
     ConvFwdArgs a = a_in;
     a.probe = g_x6_probe;
-    const unsigned grid = (unsigned)((int64_t)a.ntiles * (a.Cout / 64));
-    const bool wide = fwd_x6_tile_w(a.W) == 32;
-    // (the 16-wide tile's padded halo makes its double-buffered form 84 KB = 1 block/CU,
-    // so narrow images keep the single-stage kernel)
-    if (g_x6_pipe && wide) {
-        hipLaunchKernelGGL((conv3x3_fwd_x6p_kernel<4, 32, false>), dim3(grid), dim3(256), 0, st, a);
-    } else if (wide) {
+    const int64_t items = (int64_t)a.ntiles * (a.Cout / 64);
+    if (use_x6r(a.W)) {
+        // persistent: one workgroup per CU (a multiple of 8: blockIdx % 8 = XCD), each
+        // walking a strided share of its XCD's contiguous item range
+        int64_t g = std::min<int64_t>(cu_count(st), (items + 7) / 8 * 8);
+        g = std::max<int64_t>(8, g / 8 * 8);
+        hipLaunchKernelGGL(conv3x3_fwd_x6r_kernel, dim3((unsigned)g), dim3(512), 0, st, a);
+        return;
+    }
+    const unsigned grid = (unsigned)items;
+    if (fwd_x6_tile_w(a.W) == 32) {
         hipLaunchKernelGGL((conv3x3_fwd_x6_kernel<4, 32, false>), dim3(grid), dim3(256), 0, st, a);
     } else {
         hipLaunchKernelGGL((conv3x3_fwd_x6_kernel<8, 16, true>), dim3(grid), dim3(256), 0, st, a);
