@@ -262,6 +262,13 @@ __device__ __forceinline__ void vm_wait() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
     __builtin_amdgcn_sched_barrier(0);
 }
+// workgroup barrier for waves that write no LDS: their fragment reads for the next
+// phase (a different ring slot than the one the loaders overwrite next) stay in flight
+__device__ __forceinline__ void read_barrier() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
 // LDS writes complete, then a workgroup barrier that does not wait for global loads
 __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -517,23 +524,35 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
             bf[q] = Bs[q * 2 * 3 * BN + boff + kx * BN];
         }
     };
+    // Every weight row a phase reads was completed a full phase earlier (the ring runs
+    // one step ahead), so the fragments of the next phase's first tap are read BEFORE
+    // the phase's barrier: the barriers only order the loaders' overwrites and expose
+    // no LDS latency inside a step.
     lds_barrier();  // step 0 staged
     int cc = 0, item = item0;
     Pos cp = pos_of(item0);
     for (int k = 0; k < total; ++k) {
         const u32x4* Ac = smem + (k & 1) * A_VECS;
+        u32x4 fa[2][MT][3], fb[2][3];
+        ldfrag(Ac, Bring + ((3 * k) % NSLOT) * R_STR, 0, 0, fa[0], fb[0]);
 #pragma unroll
-        for (int ky = 0; ky < 3; ++ky) {
-            const u32x4* Bc = Bring + ((3 * k + ky) % NSLOT) * R_STR;
-            u32x4 fa[2][MT][3], fb[2][3];
-            ldfrag(Ac, Bc, ky, 0, fa[0], fb[0]);
-#pragma unroll
-            for (int kx = 0; kx < 3; ++kx) {
-                if (kx + 1 < 3) ldfrag(Ac, Bc, ky, kx + 1, fa[(kx + 1) & 1], fb[(kx + 1) & 1]);
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma_x6(fa[kx & 1][mt], fb[kx & 1], acc[mt]);
+        for (int t = 0; t < 9; ++t) {
+            if (t + 1 < 9) {
+                const int ky1 = (t + 1) / 3, kx1 = (t + 1) % 3;
+                ldfrag(Ac, Bring + ((3 * k + ky1) % NSLOT) * R_STR, ky1, kx1, fa[(t + 1) & 1],
+                       fb[(t + 1) & 1]);
             }
-            lds_barrier();
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma_x6(fa[t & 1][mt], fb[t & 1], acc[mt]);
+            // the next tap's 15 fragment reads go out one per MFMA gap from the start
+            // of this tap's 24 MFMAs (fresh registers, landed long before their use)
+#pragma unroll
+            for (int i = 0; i < 24; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                     // MFMA
+                if (t + 1 < 9 && i < 15) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+            }
+            __builtin_amdgcn_sched_barrier(0);  // taps do not mix
+            if (t % 3 == 2) read_barrier();
         }
         if (++cc == nchunk) {
             x6_epilogue_wave<TH, TW, MT>(a, acc, cp.tile, cp.b, cp.ty0, cp.tx0, cp.nb * BN, wm, wn);
@@ -547,7 +566,6 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
         }
     }
 }
-
 // ---------------------------------------------------------------------------
 // Split-bf16 weight gradient: dW[co][ci][t] = sum_p dy[p][co] * act(x)[p+t][ci].
 // Same block decomposition and partial layout as conv3x3_wgrad_kernel (64 co x
