@@ -57,8 +57,8 @@ CONV_CASES = [
 BIG = {5, 6, 7}
 
 
-# x6 forward/dgrad kernel forms (tuning knob "x6_pipe"): 1 = persistent double-buffered
-# warp-specialized (default), 0 = single-stage
+# x6 kernel forms (tuning knobs "x6_pipe" for forward/dgrad, "x6_wgrad"): 1 = persistent
+# warp-specialized (default), 0 = one workgroup per tile/item
 X6_FORMS = {"x6": 1, "x6s": 0}
 
 
@@ -71,8 +71,10 @@ def math(request):
     old = ops.conv_math()
     ops.set_conv_math("f32" if request.param == "f32" else "x6")
     lib.ugpg_set_tuning(b"x6_pipe", X6_FORMS.get(request.param, 1))
+    lib.ugpg_set_tuning(b"x6_wgrad", X6_FORMS.get(request.param, 1))
     yield request.param
     lib.ugpg_set_tuning(b"x6_pipe", 1)
+    lib.ugpg_set_tuning(b"x6_wgrad", 1)
     ops.set_conv_math(old)
 
 

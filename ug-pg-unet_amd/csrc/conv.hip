@@ -619,6 +619,10 @@ extern "C" int ugpg_set_tuning(const char* key, int value) {
         g_x6_pipe = value;
         return UGPG_OK;
     }
+    if (key && std::string(key) == "x6_wgrad") {
+        g_x6_wgrad = value;
+        return UGPG_OK;
+    }
     if (key && std::string(key) == "x6_probe") {  // timing diagnostics; results are wrong
         g_x6_probe = value;
         return UGPG_OK;
@@ -769,7 +773,14 @@ static WgradKind wgrad_kind(const ugpg_wgrad_t* p, int C0, int C1) {
 
 static WgradPlan wgrad_plan_for(const ugpg_wgrad_t* p, WgradKind k, int Cin) {
     if (k == WG_C8) return wgrad_plan_c8(p->B, p->H, p->W, p->Cout);
-    if (k == WG_X6) return wgrad_plan(p->B, p->H, p->W, Cin, p->Cout, WGX6_TH, WGX6_TW);
+    if (k == WG_X6) {
+        WgradPlan w = wgrad_plan(p->B, p->H, p->W, Cin, p->Cout, g_x6_wgrad ? WGX6W_TH : WGX6_TH,
+                                 WGX6_TW);
+        // persistent kernel: about one item per CU, planned for the MI355X's 256 CUs
+        // (a fixed count keeps the split, hence the summation order, device-independent)
+        if (g_x6_wgrad) wgrad_x6w_plan(w.ntiles, p->Cout, Cin, 256, w.nsplit, w.tps);
+        return w;
+    }
     return wgrad_plan(p->B, p->H, p->W, Cin, p->Cout);
 }
 

@@ -48,6 +48,24 @@ __device__ __forceinline__ void split3(f32x8 v, u32x4& p0, u32x4& p1, u32x4& p2)
     p2 = __builtin_bit_cast(u32x4, l);
 }
 
+// compute units of the stream's device (cached per device)
+static int cu_count(hipStream_t st) {
+    static int cache[64] = {0};
+    int dev = 0;
+    if (hipStreamGetDevice(st, &dev) != hipSuccess || dev < 0 || dev >= 64) {
+        (void)hipGetLastError();
+        if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    }
+    if (!cache[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            n <= 0)
+            n = 256;
+        cache[dev] = n;
+    }
+    return cache[dev];
+}
+
 // identity lazy-activation coefficients (for sources stored already activated)
 __device__ const float g_act_ones[1024] = {
 #define UGPG_ONE8 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f
@@ -755,7 +773,261 @@ __global__ void __launch_bounds__(256, 2) conv3x3_wgrad_x6_kernel(WgradArgs a) {
         }
 }
 
+// ---------------------------------------------------------------------------
+// Persistent, warp-specialized form of the split-bf16 weight gradient ("x6w").
+// Same LDS records, transposed fragment reads and MFMA decomposition as
+// conv3x3_wgrad_x6_kernel, but one 8-wave workgroup per CU walks a contiguous
+// per-XCD range of items (64-co block, 64-ci block, pixel split); waves 0-3 only
+// read fragments and issue MFMAs, waves 4-7 stage: during step k (one 2 x 16
+// pixel tile) they write tile k+1 into the idle half of a double-buffered LDS
+// image from registers loaded during step k-1, then issue the loads of tile k+2
+// (untracked loads + counted vmcnt, so they stay in flight across the barrier).
+// ---------------------------------------------------------------------------
+template <int TH, int TW>
+__global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) {
+    static_assert(TW == 16, "one 16-pixel row per MFMA k-step");
+    constexpr int P = TH * TW, HWD = TW + 2, NHALO = (TH + 2) * HWD;
+    constexpr int DY_Q = P * 16, X_Q = NHALO * 16;  // float4 quads per tile
+    constexpr int DY_PER = (DY_Q + 255) / 256, X_PER = (X_Q + 255) / 256;
+    constexpr int RECS = P + NHALO;                  // records per buffer
+    constexpr int LOADS = DY_PER + X_PER + 2;        // loader VMEM instructions per step
+    __shared__ __attribute__((aligned(16))) char smem[(2 * RECS + 1) * WX_REC];
+    char* const dummy = smem + 2 * RECS * WX_REC;    // record for idle lanes' writes
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const bool loader = wave >= 4;
+    const int NCO = a.Cout / 64, NCI = a.Cin / 64;
+    const int nitems = NCO * NCI * a.nsplit;
+    const int nslots = gridDim.x >> 3;
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    const int iq = nitems >> 3, ir = nitems & 7;
+    const int ibeg = xcd * iq + min(xcd, ir);
+    const int iend = ibeg + iq + (xcd < ir ? 1 : 0);
+    const int item0 = ibeg + slot;
+    if (item0 >= iend) return;  // uniform per workgroup
+    const int tpi = a.tiles_x * a.tiles_y;
+
+    // flat step sequence: the tiles of item0, then of item0 + nslots, ...
+    struct Cur {
+        int item, tile, tend;
+    };
+    auto item_range = [&](int it, Cur& c) {
+        const int split = it / (NCO * NCI);
+        c.item = it;
+        c.tile = split * a.tps;
+        c.tend = min(a.ntiles, c.tile + a.tps);
+    };
+    auto advance = [&](Cur& c) {  // stays on the last step past the end
+        if (c.tile + 1 < c.tend) {
+            ++c.tile;
+        } else if (c.item + nslots < iend) {
+            item_range(c.item + nslots, c);
+        }
+    };
+    int total = 0;
+    for (int it = item0; it < iend; it += nslots) {
+        Cur c;
+        item_range(it, c);
+        total += max(c.tend - c.tile, 0);
+    }
+    if (total == 0) return;
+
+    if (loader) {
+        // ------------------------------------------------------------ loader waves
+        const int lt = tid - 256;
+        f32x4 rdy[DY_PER], rx[X_PER];
+        Act4 xa;
+        float xlo = 0.f;
+        unsigned dvalid = 0, xvalid = 0;
+        auto gload = [&](const Cur& c) {
+            const int nb = c.item % NCO, cb = (c.item / NCO) % NCI;
+            const int co0 = nb * 64, ci0 = cb * 64;
+            const bool second = ci0 >= a.C0;
+            const float* xsrc = second ? a.src1 : a.src0;
+            const float* xsc = second ? a.sc1 : a.sc0;
+            const float* xsh = second ? a.sh1 : a.sh0;
+            const int Cs = second ? a.C1 : a.C0, cbase = second ? ci0 - a.C0 : ci0;
+            const bool xon = xsc != nullptr;
+            xlo = xon ? 0.f : -INFINITY;
+            const int cq = cbase + (lt & 15) * 4;  // q = idx & 15 = lt & 15
+            xa.s = gld16((xon ? xsc : g_act_ones) + cq);
+            xa.h = gld16((xon ? xsh : g_act_zeros) + cq);
+            const int b = c.tile / tpi, trem = c.tile % tpi;
+            const int ty0 = (trem / a.tiles_x) * TH, tx0 = (trem % a.tiles_x) * TW;
+            dvalid = 0;
+#pragma unroll
+            for (int v = 0; v < DY_PER; ++v) {
+                const int idx = lt + v * 256;
+                const int p = idx >> 4, q = idx & 15;
+                const int gy = ty0 + p / TW, gx = tx0 + p % TW;
+                const bool ok = gy < a.H && gx < a.W;
+                const int cy = min(gy, a.H - 1), cx = min(gx, a.W - 1);
+                rdy[v] = gld16(a.dy + ((size_t)(b * a.H + cy) * a.W + cx) * a.Cout + co0 + q * 4);
+                dvalid |= (ok ? 1u : 0u) << v;
+            }
+            xvalid = 0;
+#pragma unroll
+            for (int v = 0; v < X_PER; ++v) {
+                const int idx = lt + v * 256;
+                const int hp = idx < X_Q ? idx >> 4 : 0, q = idx & 15;
+                const int gy = ty0 - 1 + hp / HWD, gx = tx0 - 1 + hp % HWD;
+                const bool ok = idx < X_Q && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
+                const int cy = min(max(gy, 0), a.H - 1), cx = min(max(gx, 0), a.W - 1);
+                rx[v] = gld16(xsrc + ((size_t)(b * a.H + cy) * a.W + cx) * Cs + cbase + q * 4);
+                xvalid |= (ok ? 1u : 0u) << v;
+            }
+        };
+        // record layout: [piece][64 ch] bf16 at byte piece*128 + ch*2
+        auto put = [&](char* rec, int q, f32x4 v) {
+            u32x2 p0, p1, p2;
+            split3_4(v, p0, p1, p2);
+            char* r = rec + q * 8;
+            *reinterpret_cast<u32x2*>(r) = p0;
+            *reinterpret_cast<u32x2*>(r + 128) = p1;
+            *reinterpret_cast<u32x2*>(r + 256) = p2;
+        };
+        auto lstore = [&](int buf) {
+            char* dys = smem + buf * RECS * WX_REC;
+            char* xs = dys + P * WX_REC;
+#pragma unroll
+            for (int v = 0; v < DY_PER; ++v) {
+                const int idx = lt + v * 256;
+                const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+                put(dys + (idx >> 4) * WX_REC, idx & 15, ((dvalid >> v) & 1u) ? rdy[v] : z);
+            }
+#pragma unroll
+            for (int v = 0; v < X_PER; ++v) {
+                const int idx = lt + v * 256;
+                const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+                const f32x4 val = ((xvalid >> v) & 1u) ? act_floor4(rx[v], xa, xlo) : z;
+                put(idx < X_Q ? xs + (idx >> 4) * WX_REC : dummy, idx & 15, val);
+            }
+        };
+        Cur lc;
+        item_range(item0, lc);
+        gload(lc);
+        vm_wait<0>();
+        lstore(0);
+        advance(lc);
+        gload(lc);  // step 1
+        lds_barrier();
+        for (int k = 0; k < total; ++k) {
+            vm_wait<0>();
+            lstore((k + 1) & 1);  // step k+1
+            advance(lc);
+            gload(lc);            // step k+2, in flight across the barrier
+            lds_barrier();
+        }
+        vm_wait<0>();  // no load outlives the workgroup
+        return;
+    }
+
+    // ---------------------------------------------------------------- compute waves
+    const int wm = wave >> 1, wn = wave & 1;
+    f32x16 acc[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+    // transposed-read addresses: 16-lane group g = lane>>4 (h = g>>1 pixel half,
+    // g&1 channel half), lane li supplies row (pixel) li>>2, channels 4(li&3)..+3.
+    const int li = lane & 15, g = lane >> 4, hh = g >> 1;
+    const int pix_in = 8 * hh + (li >> 2);
+    const int ch_a = wm * 32 + 16 * (g & 1) + 4 * (li & 3);
+    const int ch_b = wn * 32 + 16 * (g & 1) + 4 * (li & 3);
+    Cur cc;
+    item_range(item0, cc);
+    lds_barrier();  // step 0 staged
+    for (int k = 0; k < total; ++k) {
+        const char* dys = smem + (k & 1) * RECS * WX_REC;
+        const char* abase = dys + pix_in * WX_REC + ch_a * 2;
+        const char* bbase = dys + P * WX_REC + pix_in * WX_REC + ch_b * 2;
+        auto lda = [&](int ks, u32x4 (&af)[3]) {
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const char* pa = abase + ks * TW * WX_REC + q * 128;
+                const u32x2 lo = ds_read_tr(pa), hi = ds_read_tr(pa + 4 * WX_REC);
+                af[q] = u32x4{lo.x, lo.y, hi.x, hi.y};
+            }
+        };
+        auto ldb = [&](int ks, int t, u32x4 (&bf)[3]) {
+            const char* pb = bbase + ((ks + t / 3) * HWD + (t % 3)) * WX_REC;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const u32x2 lo = ds_read_tr(pb + q * 128), hi = ds_read_tr(pb + q * 128 + 4 * WX_REC);
+                bf[q] = u32x4{lo.x, lo.y, hi.x, hi.y};
+            }
+        };
+        // 2 rows x 9 taps as one sequence: the next tap's fragments (and the next row's
+        // dy fragments) are read during the current tap's MFMAs
+        u32x4 afr[2][3], bfr[2][3];
+        lda(0, afr[0]);
+        ldb(0, 0, bfr[0]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < 9 * TH; ++u) {
+            const int ks = u / 9, t = u % 9;
+            if (u + 1 < 9 * TH) {
+                if ((u + 1) % 9 == 0) lda((u + 1) / 9, afr[((u + 1) / 9) & 1]);
+                ldb((u + 1) / 9, (u + 1) % 9, bfr[(u + 1) & 1]);
+            }
+            acc[t] = mfma_x6(afr[ks & 1], bfr[u & 1], acc[t]);
+            // next fragments two (four at a row change) per MFMA gap in the first half
+            // of the tap, so they land before the next tap's first MFMAs
+            const bool more = u + 1 < 9 * TH, row = (u + 1) % 9 == 0;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                if (more && i < 3) {
+                    if (row) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+                    else __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        read_barrier();
+        const bool item_end = cc.tile + 1 >= cc.tend;
+        if (item_end) {
+            const int nb = cc.item % NCO, rest = cc.item / NCO;
+            const int cb = rest % NCI, split = rest / NCI;
+            const int ci = cb * 64 + wn * 32 + (lane & 31);
+#pragma unroll
+            for (int t = 0; t < 9; ++t)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int co = nb * 64 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                    a.part[((size_t)(split * 9 + t) * a.Cout + co) * a.Cin + ci] = acc[t][r];
+                    acc[t][r] = 0.f;
+                }
+        }
+        advance(cc);
+    }
+}
+
+// Persistent wgrad plan: about one item per CU (items = co blocks x ci blocks x splits)
+void wgrad_x6w_plan(int ntiles, int Cout, int Cin, int cus, int& nsplit, int& tps) {
+    const int64_t base = (int64_t)(Cout / 64) * (Cin / 64);
+    int64_t ns = cdiv(cus, base);
+    const int64_t per = (int64_t)9 * Cout * Cin * 4;  // fp32 partial slab per split
+    int64_t cap = (192ll << 20) / per;
+    if (cap < 1) cap = 1;
+    if (ns > cap) ns = cap;
+    if (ns > ntiles) ns = ntiles;
+    if (ns < 1) ns = 1;
+    tps = (int)cdiv(ntiles, ns);
+    nsplit = (int)cdiv(ntiles, tps);
+}
+
+int g_x6_wgrad = 1;  // tuning knob "x6_wgrad": 1 = persistent x6w kernel, 0 = one block per item
+
 void launch_wgrad_x6(const WgradArgs& a, unsigned grid, hipStream_t st) {
+    if (g_x6_wgrad) {
+        const int64_t items = (int64_t)(a.Cout / 64) * (a.Cin / 64) * a.nsplit;
+        int64_t g = std::min<int64_t>(cu_count(st), (items + 7) / 8 * 8);
+        g = std::max<int64_t>(8, g / 8 * 8);
+        hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW>), dim3((unsigned)g), dim3(512), 0, st, a);
+        return;
+    }
     hipLaunchKernelGGL((conv3x3_wgrad_x6_kernel<WGX6_TH, WGX6_TW>), dim3(grid), dim3(256), 0, st,
                        a);
 }
@@ -809,24 +1081,6 @@ int fwd_x6_stat_slots(int ntiles, int W) { return use_x6r(W) ? 2 * ntiles : ntil
 // tuning knob "x6_pipe": 1 = conv3x3_fwd_x6r_kernel for images >= 32 wide (default),
 // 0 = conv3x3_fwd_x6_kernel everywhere
 int g_x6_probe = 0;  // "x6_probe": timing diagnostics (see ugpg_set_tuning)
-
-// compute units of the stream's device (cached per device)
-static int cu_count(hipStream_t st) {
-    static int cache[64] = {0};
-    int dev = 0;
-    if (hipStreamGetDevice(st, &dev) != hipSuccess || dev < 0 || dev >= 64) {
-        (void)hipGetLastError();
-        if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    }
-    if (!cache[dev]) {
-        int n = 0;
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            n <= 0)
-            n = 256;
-        cache[dev] = n;
-    }
-    return cache[dev];
-}
 
 void launch_fwd_x6(const ConvFwdArgs& a_in, hipStream_t st) {
     ConvFwdArgs a = a_in;

@@ -87,7 +87,7 @@ if _conv_math not in _MATHS:
     raise ValueError(f"UGPG_CONV_MATH must be one of {_MATHS}, got {_conv_math!r}")
 
 
-for _knob in ("x6_pipe", "fwd_cfg"):  # benchmarking knobs from the environment
+for _knob in ("x6_pipe", "x6_wgrad", "fwd_cfg"):  # benchmarking knobs from the environment
     _v = os.environ.get("UGPG_" + _knob.upper())
     if _v is not None:
         check(lib.ugpg_set_tuning(_knob.encode(), int(_v)), "set_tuning")
