@@ -216,6 +216,19 @@ int ugpg_weighted_mean_bwd(const float* umap, int B, int C, int HW, int Cu, floa
 size_t ugpg_seg_metrics_workspace(int B);
 int ugpg_seg_metrics(const float* logits, const float* target, int B, int HW, float* out,
                      void* ws, size_t ws_bytes, void* stream);
+/* ---- inference / evaluation (MoNuSegImprove/test_monuseg.py:164-297) ----------
+ * Replaces MoNuSegTester.calculate_metrics (:264-297, numpy on float32 arrays) and the
+ * sigmoid / threshold / mean of predict_image (:188-199) for a batch of logits
+ * (B,1,H,W) against ground-truth masks (B,1,H,W): pred = sigmoid(x) > 0.5;
+ * out[8*b + 0..7] = iou, dice, accuracy, precision, recall, specificity (float32,
+ * eps 1e-8, the reference's operation order), confidence = mean sigmoid, tp count. */
+size_t ugpg_seg_eval_workspace(int B, int HW);
+int ugpg_seg_eval(const float* logits, const float* gt, int B, int HW, float* out, void* ws,
+                  size_t ws_bytes, void* stream);
+/* mask (B,1,Ho,Wo) = F.interpolate((sigmoid(x) > 0.5).float(), (Ho,Wo), mode='nearest')
+ * (test_monuseg.py:190-195) */
+int ugpg_predict_mask(const float* logits, int B, int H, int W, float* mask, int Ho, int Wo,
+                      void* stream);
 /* mean and unbiased std of n floats: out = [mean, std] (torch.mean/torch.std) */
 size_t ugpg_mean_std_workspace(int64_t n);
 int ugpg_mean_std(const float* x, int64_t n, float* out, void* ws, size_t ws_bytes,

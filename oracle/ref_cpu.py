@@ -17,6 +17,10 @@ Reference anchors (file:line in tridang04022004/UG-PG-UNet):
   weighted loss       UG_unet.py:61-94
   trainer step/metrics uncertainty_guided_trainer.py:81-256
   Herlev model/step   Herlev/train_herlev.py:29-121, 216-296
+  eval metrics/masks  MoNuSegImprove/test_monuseg.py:164-297 (parity unpinned: that
+                      module imports cv2 at top level, absent here, so it is restated
+                      from its source; its torch calls -- sigmoid, >0.5, nearest
+                      interpolate -- are the ATen CPU ops themselves)
 
 Parity: pinned against the imported reference (goldens under tests/golden/).
 """
@@ -328,3 +332,47 @@ def herlev_ug_loss(logits, target, prev_logits, alpha, num_classes, class_weight
         w = w.unsqueeze(0)
     final = torch.mean(F.cross_entropy(logits, target, reduction="none") * w.detach())
     return final, base, w
+
+
+# ---------------------------------------------------------------------------
+# Inference / evaluation (MoNuSegImprove/test_monuseg.py)
+# ---------------------------------------------------------------------------
+def predict_mask(logits, size):
+    """test_monuseg.py:188-195: (sigmoid > 0.5).float() then nearest resize to `size`."""
+    probs = torch.sigmoid(logits)
+    pred = (probs > 0.5).float()
+    return F.interpolate(pred, size=size, mode="nearest"), probs
+
+
+def calculate_metrics(pred_mask, gt_mask):
+    """test_monuseg.py:264-297, numpy on float32 arrays (NEP 50: python scalars weak)."""
+    import numpy as np
+    pred_flat = np.asarray(pred_mask, dtype=np.float32).flatten()
+    gt_flat = np.asarray(gt_mask, dtype=np.float32).flatten()
+    intersection = np.sum(pred_flat * gt_flat)
+    tp = intersection
+    fp = np.sum(pred_flat) - tp
+    fn = np.sum(gt_flat) - tp
+    tn = len(pred_flat) - tp - fp - fn
+    eps = 1e-8
+    return {
+        "iou": (tp + eps) / (tp + fp + fn + eps),
+        "dice": (2 * tp + eps) / (2 * tp + fp + fn + eps),
+        "accuracy": (tp + tn + eps) / (tp + tn + fp + fn + eps),
+        "precision": (tp + eps) / (tp + fp + eps),
+        "recall": (tp + eps) / (tp + fn + eps),
+        "specificity": (tn + eps) / (tn + fp + eps),
+    }
+
+
+def evaluate_logits(logits, gt):
+    """Per-sample calculate_metrics of (sigmoid(logits) > 0.5) vs gt plus the mean
+    probability (test_monuseg.py:199, 244-252) -> list of dicts."""
+    probs = torch.sigmoid(logits)
+    pred = (probs > 0.5).float()
+    out = []
+    for b in range(logits.shape[0]):
+        m = calculate_metrics(pred[b].numpy(), gt[b].float().numpy())
+        m["confidence"] = probs[b].mean().item()
+        out.append(m)
+    return out

@@ -148,3 +148,37 @@ def test_shard_helper():
     assert torch.equal(torch.cat(parts), x)
     with pytest.raises(ValueError):
         shard(x, 0, 3)
+
+
+def test_eval_metrics_host_api_matches_oracle():
+    """ugpg.evaluation.calculate_metrics keeps test_monuseg.py:264-297's numpy float32
+    arithmetic (the oracle restatement) exactly, including the empty-mask eps paths."""
+    import numpy as np
+    from ugpg.evaluation import calculate_metrics
+    rng = np.random.default_rng(0)
+    cases = [(rng.random(4096) > 0.5, rng.random(4096) > 0.7),
+             (np.zeros(100), rng.random(100) > 0.5), (rng.random(100) > 0.5, np.zeros(100)),
+             (np.zeros(64), np.zeros(64)), (np.ones(64), np.ones(64))]
+    for pred, gt in cases:
+        got = calculate_metrics(pred.astype(np.float32), gt.astype(np.float32))
+        want = O.calculate_metrics(pred, gt)
+        for k, v in want.items():
+            assert got[k] == v and type(got[k]) is type(v), k
+
+
+def test_tester_checkpoint_formats(tmp_path):
+    """MoNuSegTester.load_model (test_monuseg.py:120-162): checkpoint dict with 'stage',
+    raw state_dict (stage 4), anything else rejected; weights-only loading."""
+    import ugpg
+    from tests._parity import det_state
+    s2 = det_state(2, 3, 1)
+    torch.save({"model_state_dict": s2, "stage": 2, "val_dice": 0.5}, tmp_path / "a.pth")
+    t = ugpg.MoNuSegTester(str(tmp_path / "a.pth"), device="cpu")
+    assert t.stage == 2 and isinstance(t.model, ugpg.PGUNet2) and not t.model.training
+    s4 = det_state(4, 3, 1)
+    torch.save(s4, tmp_path / "b.pth")
+    t = ugpg.MoNuSegTester(str(tmp_path / "b.pth"), device="cpu")
+    assert t.stage == 4 and isinstance(t.model, ugpg.PGUNet4)
+    torch.save([1, 2, 3], tmp_path / "c.pth")
+    with pytest.raises(RuntimeError, match="Unrecognized checkpoint"):
+        ugpg.MoNuSegTester(str(tmp_path / "c.pth"), device="cpu")

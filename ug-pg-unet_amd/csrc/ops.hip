@@ -580,6 +580,84 @@ __global__ void __launch_bounds__(256) seg_metrics_finalize_kernel(const float* 
     }
 }
 
+// ------------------------------------------------------------- inference / evaluation
+// MoNuSegTester.calculate_metrics / predict_image (MoNuSegImprove/test_monuseg.py:164-297):
+// per-sample counts of pred = sigmoid(x) > 0.5 against a ground-truth mask, then the six
+// metrics in float32 exactly as numpy evaluates them on float32 arrays (eps 1e-8).
+__global__ void __launch_bounds__(256) seg_eval_part_kernel(const float* x, const float* t, int HW,
+                                                            int nbps, double* part) {
+    const int b = blockIdx.y;
+    double stp = 0, sp = 0, st = 0, ss = 0;
+    const int per = (HW + nbps - 1) / nbps;
+    const int p0 = blockIdx.x * per, p1 = min(HW, p0 + per);
+    for (int p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
+        const size_t i = (size_t)b * HW + p;
+        const float pr = sigmoidf_(x[i]);
+        const float pm = pr > 0.5f ? 1.0f : 0.0f;
+        const float tv = t[i];
+        stp += (double)(pm * tv);
+        sp += pm;
+        st += tv;
+        ss += pr;
+    }
+    stp = wave_sum_d(stp);
+    sp = wave_sum_d(sp);
+    st = wave_sum_d(st);
+    ss = wave_sum_d(ss);
+    __shared__ double red[4][4];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) {
+        red[wave][0] = stp;
+        red[wave][1] = sp;
+        red[wave][2] = st;
+        red[wave][3] = ss;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        const double v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
+                         red[3][threadIdx.x];
+        part[((size_t)b * nbps + blockIdx.x) * 4 + threadIdx.x] = v;
+    }
+}
+
+__global__ void seg_eval_finalize_kernel(const double* part, int B, int nbps, int HW, float* out) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    double c[4] = {0, 0, 0, 0};
+    for (int k = 0; k < nbps; ++k)
+        for (int q = 0; q < 4; ++q) c[q] += part[((size_t)b * nbps + k) * 4 + q];
+    // float32 arithmetic in the reference's order (numpy on float32 arrays; python
+    // scalars are weak under NEP 50, so eps and len() enter as float32)
+    const float eps = 1e-8f;
+    const float tp = (float)c[0], sp = (float)c[1], st = (float)c[2];
+    const float fp = sp - tp, fn = st - tp;
+    const float tn = (((float)HW - tp) - fp) - fn;
+    float* o = out + (size_t)b * 8;
+    o[0] = (tp + eps) / (((tp + fp) + fn) + eps);
+    o[1] = (2.0f * tp + eps) / (((2.0f * tp + fp) + fn) + eps);
+    o[2] = ((tp + tn) + eps) / ((((tp + tn) + fp) + fn) + eps);
+    o[3] = (tp + eps) / ((tp + fp) + eps);
+    o[4] = (tp + eps) / ((tp + fn) + eps);
+    o[5] = (tn + eps) / ((tn + fp) + eps);
+    o[6] = (float)(c[3] / (double)HW);  // confidence = mean probability
+    o[7] = tp;
+}
+
+// mask = nearest-resize(sigmoid(x) > 0.5) to (Ho, Wo)  (test_monuseg.py:188-195)
+__global__ void predict_mask_kernel(const float* x, int B, int H, int W, float* mask, int Ho,
+                                    int Wo) {
+    const int64_t total = (int64_t)B * Ho * Wo;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int ox = (int)(i % Wo);
+        const int64_t r = i / Wo;
+        const int oy = (int)(r % Ho);
+        const int64_t b = r / Ho;
+        const float v = x[((size_t)b * H + nearest_src(oy, H, Ho)) * W + nearest_src(ox, W, Wo)];
+        mask[i] = sigmoidf_(v) > 0.5f ? 1.0f : 0.0f;
+    }
+}
+
 __global__ void __launch_bounds__(256) mean_std_part_kernel(const float* x, int64_t n,
                                                             int64_t per, double* part) {
     const int64_t p0 = blockIdx.x * per, p1 = min(n, p0 + per);
@@ -1001,6 +1079,36 @@ extern "C" int ugpg_seg_metrics(const float* x, const float* t, int B, int HW, f
     hipLaunchKernelGGL(seg_metrics_finalize_kernel, dim3(1), dim3(256), 0, st,
                        static_cast<const float*>(ws), B, nbps, (int64_t)B * HW, out);
     return check_launch("seg_metrics_finalize");
+}
+
+extern "C" size_t ugpg_seg_eval_workspace(int B, int HW) {
+    return (size_t)B * metrics_nbps(HW) * 4 * sizeof(double);
+}
+
+extern "C" int ugpg_seg_eval(const float* x, const float* t, int B, int HW, float* out, void* ws,
+                             size_t ws_bytes, void* stream) {
+    UGPG_REQUIRE(x && t && out && B > 0 && HW > 0, "seg_eval");
+    const int nbps = metrics_nbps(HW);
+    const size_t need = ugpg_seg_eval_workspace(B, HW);
+    if (!ws || ws_bytes < need) {
+        set_error("seg_eval: workspace %zu < %zu", ws_bytes, need);
+        return UGPG_ERR_WORKSPACE;
+    }
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(seg_eval_part_kernel, dim3(nbps, B), dim3(256), 0, st, x, t, HW, nbps,
+                       static_cast<double*>(ws));
+    if (int e = check_launch("seg_eval")) return e;
+    hipLaunchKernelGGL(seg_eval_finalize_kernel, dim3((unsigned)cdiv(B, 64)), dim3(64), 0, st,
+                       static_cast<const double*>(ws), B, nbps, HW, out);
+    return check_launch("seg_eval_finalize");
+}
+
+extern "C" int ugpg_predict_mask(const float* x, int B, int H, int W, float* mask, int Ho, int Wo,
+                                 void* stream) {
+    UGPG_REQUIRE(x && mask && B > 0 && H > 0 && W > 0 && Ho > 0 && Wo > 0, "predict_mask");
+    hipLaunchKernelGGL(predict_mask_kernel, dim3(stream_grid((int64_t)B * Ho * Wo)), dim3(256), 0,
+                       as_stream(stream), x, B, H, W, mask, Ho, Wo);
+    return check_launch("predict_mask");
 }
 
 extern "C" size_t ugpg_mean_std_workspace(int64_t n) {

@@ -69,6 +69,9 @@ SIGNATURES = {
     "ugpg_weighted_mean_bwd": (_i, [_p, _i, _i, _i, _i, _f, _p, _p, _p]),
     "ugpg_seg_metrics_workspace": (_sz, [_i]),
     "ugpg_seg_metrics": (_i, [_p, _p, _i, _i, _p, _p, _sz, _p]),
+    "ugpg_seg_eval_workspace": (_sz, [_i, _i]),
+    "ugpg_seg_eval": (_i, [_p, _p, _i, _i, _p, _p, _sz, _p]),
+    "ugpg_predict_mask": (_i, [_p, _i, _i, _i, _p, _i, _i, _p]),
     "ugpg_mean_std_workspace": (_sz, [_i64]),
     "ugpg_mean_std": (_i, [_p, _i64, _p, _p, _sz, _p]),
     "ugpg_rmsprop_step": (_i, [_p, _p, _p, _i64, _f, _f, _f, _f, _f, _p]),

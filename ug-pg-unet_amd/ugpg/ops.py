@@ -390,6 +390,35 @@ def seg_metrics(logits, target, out=None):
     return out
 
 
+EVAL_KEYS = ("iou", "dice", "accuracy", "precision", "recall", "specificity", "confidence", "tp")
+
+
+def seg_eval(logits, gt):
+    """Per-sample evaluation metrics of single-channel logits (B,1,H,W) against masks
+    (B,1,H,W) -> device tensor (B, 8) with columns EVAL_KEYS (test_monuseg.py:264-297)."""
+    B = logits.shape[0]
+    hw = logits.numel() // B
+    if gt.numel() != logits.numel():
+        raise ValueError(f"seg_eval: mask {tuple(gt.shape)} does not match logits {tuple(logits.shape)}")
+    out = empty((B, 8), like=logits)
+    ws = workspace(lib.ugpg_seg_eval_workspace(B, hw), logits.device)
+    check(lib.ugpg_seg_eval(_f32(logits.contiguous()), _f32(gt.contiguous()), B, hw, ptr(out),
+                            ptr(ws), ws.numel(), stream()), "seg_eval")
+    return out
+
+
+def predict_mask(logits, size):
+    """(sigmoid(x) > 0.5) nearest-resized to `size` = (Ho, Wo) -> (B,1,Ho,Wo) float."""
+    B, C, H, W = logits.shape
+    if C != 1:
+        raise ValueError("predict_mask: single-channel logits expected")
+    Ho, Wo = size
+    out = empty((B, 1, Ho, Wo), like=logits)
+    check(lib.ugpg_predict_mask(_f32(logits.contiguous()), B, H, W, ptr(out), Ho, Wo, stream()),
+          "predict_mask")
+    return out
+
+
 def mean_std(x, out=None):
     x = x.contiguous()
     out = empty(2, like=x) if out is None else out
