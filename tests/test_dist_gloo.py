@@ -88,3 +88,53 @@ def test_dp_allreduce_flat_buffer():
 
 def test_dp_allreduce_per_tensor_fallback():
     _run(flat=False)
+
+
+def _reducer_worker(rank, port, outdir):
+    """Feed OverlapReducer the way the ugpg backward does: per-parameter views of one
+    flat buffer, completed block by block from the end of the layout to the start."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "ug-pg-unet_amd")]
+    import torch.distributed as dist
+    from ugpg.dist import OverlapReducer, allreduce_gradients, overlapped_allreduce, overlap_reducer
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    sizes = [7, 300, 1, 4096, 33, 5000, 12, 900, 2]      # uneven parameter sizes
+    gen = torch.Generator().manual_seed(10 + rank)
+    flat = torch.randn(sum(sizes), generator=gen)
+    want = flat.clone()
+    dist.all_reduce(want)
+    views, off = [], 0
+    for n in sizes:
+        views.append(flat[off:off + n])
+        off += n
+    assert overlap_reducer() is None                     # opt-in only
+    with overlapped_allreduce():
+        red = overlap_reducer()
+        assert isinstance(red, OverlapReducer)
+        red.bucket = 1000                                # force several buckets
+        red.begin(flat, views)
+        blocks = [[8, 7], [6], [5, 4, 3], [2, 1], [0]]   # backward order: last params first
+        issued = []
+        for blk in blocks:
+            red.done([views[i] for i in blk])
+            issued.append(red.hi)
+        red.flush()
+    params = [torch.nn.Parameter(torch.zeros(n)) for n in sizes]
+    for p, v in zip(params, views):
+        p.grad = v
+    scale = allreduce_gradients(params)
+    assert scale == 1.0 / WORLD
+    # buckets went out during the "backward" (not only at flush), highest offsets first
+    assert issued == sorted(issued, reverse=True) and issued[-1] < sum(sizes), issued
+    torch.save((flat, want), os.path.join(outdir, f"r{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_overlap_reducer_buckets_sum_like_one_allreduce():
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_reducer_worker, args=(_free_port(), d), nprocs=WORLD, join=True)
+        for r in range(WORLD):
+            got, want = torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True)
+            assert torch.allclose(got, want, rtol=1e-6, atol=1e-6)

@@ -189,3 +189,34 @@ def test_rmsprop_step_matches_oracle(dev):
         err = (named[k].detach().cpu() - P[k]).abs().max().item()
         assert err <= 1e-6 * max(1.0, P[k].abs().max().item()), (k, err)
         assert int(opt.state[named[k]]["step"]) == 2
+
+
+def test_backward_reports_gradients_back_to_front(dev, monkeypatch):
+    """The data-parallel OverlapReducer relies on the backward finishing the flat
+    gradient buffer from its end to its start: every gradient view is reported once,
+    and each report's views all lie below the previous report's (block granularity)."""
+    import ugpg
+    from ugpg import functional
+
+    class Recorder:
+        def begin(self, flat, views):
+            self.base = flat.storage_offset()
+            self.n = len(views)
+            self.calls = []
+
+        def done(self, views):
+            self.calls.append(sorted(v.storage_offset() - self.base for v in views if v is not None))
+
+        def flush(self):
+            self.flushed = True
+
+    rec = Recorder()
+    monkeypatch.setattr(functional, "overlap_reducer", lambda: rec)
+    m = ugpg.PGUNet4(3, 1).to(dev).train()
+    x = torch.randn(2, 3, 64, 64, device=dev)
+    m(x).sum().backward()
+    offs = [o for c in rec.calls for o in c]
+    assert rec.flushed and len(offs) == len(set(offs)) == rec.n == len(list(m.parameters()))
+    for prev, cur in zip(rec.calls, rec.calls[1:]):
+        if cur:
+            assert max(cur) < min(prev), (prev, cur)

@@ -1,5 +1,11 @@
-"""Data parallelism: one process per GPU, minibatch sharded across ranks, one
-RCCL all-reduce of the flat gradient buffer per step.
+"""Data parallelism: one process per GPU, minibatch sharded across ranks, RCCL
+all-reduce of the flat gradient buffer per step.
+
+The all-reduce is bucketed and overlapped with the backward: the network's flat
+gradient buffer is laid out in forward (state_dict) order and the backward
+produces it back to front, so as soon as every gradient above an offset is final
+the bucket below the previous watermark is handed to RCCL (async, on its own
+stream) while the remaining backward kernels run (OverlapReducer).
 
 BatchNorm stays local to each rank (each rank's forward equals the reference's
 bs-16 forward on its shard); gradients are summed and the 1/world_size average
@@ -46,14 +52,119 @@ def shard(batch: torch.Tensor, rank: int, world_size: int) -> torch.Tensor:
     return batch[rank * per:(rank + 1) * per]
 
 
+class OverlapReducer:
+    """Bucketed SUM all-reduce of one flat gradient buffer, issued during the backward.
+
+    begin(flat, views): a new backward starts; `views` are the per-parameter gradient
+    views of `flat` (any order).  done(views): these gradients are final.  Whenever all
+    gradients at offsets >= w are final (the watermark w), the elements between w and
+    the last issued bucket are issued in buckets of `bucket_bytes` (async).  flush()
+    issues the rest; wait() makes the current stream wait for every bucket and returns
+    the 1/world_size scale.  Buckets are issued in the same order on every rank (the
+    backward is identical), as collectives require."""
+
+    def __init__(self, bucket_bytes: int = 16 << 20):
+        self.bucket = max(1, bucket_bytes // 4)
+        self.flat = None
+        self.works = []
+
+    def begin(self, flat, views):
+        base = flat.storage_offset()
+        self.flat = flat
+        self.ranges = sorted(((v.storage_offset() - base, v.numel()) for v in views if v is not None),
+                             reverse=True)
+        self.final = set()
+        self.k = 0                    # ranges[:k] (highest offsets first) are final
+        self.hi = flat.numel()        # [hi, end) already issued
+        self.works = []
+
+    def _issue(self, lo, hi):
+        while hi > lo:
+            a = max(lo, hi - self.bucket)
+            self.works.append(dist.all_reduce(self.flat[a:hi], async_op=True))
+            hi = a
+        return lo
+
+    def done(self, views):
+        if self.flat is None:
+            return
+        base = self.flat.storage_offset()
+        for v in views:
+            if v is not None:
+                self.final.add(v.storage_offset() - base)
+        while self.k < len(self.ranges) and self.ranges[self.k][0] in self.final:
+            self.k += 1
+        mark = self.ranges[self.k - 1][0] if self.k else self.flat.numel()
+        if self.hi - mark >= self.bucket:
+            # issue whole buckets only; the remainder waits for more gradients
+            lo = self.hi - (self.hi - mark) // self.bucket * self.bucket
+            self.hi = self._issue(lo, self.hi)
+
+    def flush(self):
+        if self.flat is not None and self.hi > 0:
+            self.hi = self._issue(0, self.hi)
+
+    def pending_for(self, grads) -> bool:
+        return self.flat is not None and bool(grads) and \
+            grads[0].untyped_storage().data_ptr() == self.flat.untyped_storage().data_ptr()
+
+    def wait(self) -> float:
+        for w in self.works:
+            w.wait()
+        self.works = []
+        self.flat = None
+        return 1.0 / world()[1]
+
+
+_REDUCER: OverlapReducer | None = None
+_OVERLAP = False
+
+
+def enable_overlap(flag: bool = True) -> None:
+    """Opt in to overlapped gradient all-reduce: every ugpg backward then feeds the
+    process-wide OverlapReducer (gradients are summed over ranks during the backward)
+    and the caller must finish the step with allreduce_gradients (the trainers do)."""
+    global _OVERLAP
+    _OVERLAP = bool(flag)
+
+
+class overlapped_allreduce:
+    """Context manager: backwards run inside it feed the OverlapReducer (see
+    enable_overlap); finish with allreduce_gradients after the block."""
+
+    def __enter__(self):
+        self.prev = _OVERLAP
+        enable_overlap(True)
+        return self
+
+    def __exit__(self, *exc):
+        enable_overlap(self.prev)
+        return False
+
+
+def overlap_reducer() -> OverlapReducer | None:
+    """The reducer the ugpg backward feeds: None unless enabled, data-parallel, and not
+    disabled with UGPG_DP_OVERLAP=0."""
+    global _REDUCER
+    if not _OVERLAP or world()[1] <= 1 or os.environ.get("UGPG_DP_OVERLAP", "1") == "0":
+        return None
+    if _REDUCER is None:
+        _REDUCER = OverlapReducer(int(os.environ.get("UGPG_DP_BUCKET_MB", "16")) << 20)
+    return _REDUCER
+
+
 def allreduce_gradients(params, bucket_bytes: int = 64 << 20):
-    """Sum gradients over ranks.  One call when the grads form a single flat run
-    (the normal ugpg layout), otherwise per-tensor calls.  Returns the scale
-    (1/world_size) the optimizer must apply."""
+    """Sum gradients over ranks.  If the backward already issued them through the
+    OverlapReducer, only wait for those buckets; else one call when the grads form
+    a single flat run (the normal ugpg layout), otherwise per-tensor calls.
+    Returns the scale (1/world_size) the optimizer must apply."""
     _, ws = world()
     grads = [p.grad for p in params if p.grad is not None]
     if ws <= 1 or not grads:
         return 1.0
+    red = _REDUCER
+    if red is not None and red.pending_for(grads):
+        return red.wait()
     run = contiguous_run(grads)
     if run is not None:
         base, _, n = run

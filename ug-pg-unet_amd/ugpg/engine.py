@@ -207,10 +207,13 @@ class UNetGraph:
         return logits, state
 
     # -------------------------------------------------------------- backward
-    def backward(self, state, grads, dlogits=None, dout_act=None, need_dx=False):
+    def backward(self, state, grads, dlogits=None, dout_act=None, need_dx=False, on_done=None):
         """dlogits: NCHW gradient of the combined head output, or dout_act: NHWC
         gradient w.r.t. the last block's activation (encoder-only graphs).
-        grads: {param: destination tensor or None}.  Returns dx (NCHW) or None."""
+        grads: {param: destination tensor or None}.  on_done(views) is called with the
+        gradient views of each block (and of the heads) once they are final (the
+        data-parallel reducer overlaps its all-reduce with the rest of the backward).
+        Returns dx (NCHW) or None."""
         outs, ctxs = state["outs"], state["ctxs"]
         nb = len(self.blocks)
         da = [None] * nb
@@ -227,6 +230,8 @@ class UNetGraph:
                 dw_flat = dw.view(w.shape) if dw is not None else torch.empty_like(w)
                 db = grads.get(conv.bias)
                 ops.head_bwd(a, w, dh.contiguous(), dw_flat, db, da[hd.block], acc)
+            if on_done is not None:
+                on_done([grads.get(p) for hd in self.heads for p in hd.mod.parameters()])
         else:
             da[nb - 1] = dout_act
         dx0 = None
@@ -263,6 +268,8 @@ class UNetGraph:
                 if not acc_l:
                     da[low] = torch.empty_like(outs[low].y)
                 ops.bilinear_nhwc_bwd(du, h, w, da[low], acc_l)
+            if on_done is not None:
+                on_done([grads.get(p) for p in blk.mod.parameters()])
             da[bi] = None
             ctxs[bi] = None
         if dx0 is not None:

@@ -13,6 +13,7 @@ import torch
 from torch.autograd.function import once_differentiable
 
 from . import ops
+from .dist import overlap_reducer
 
 
 def _check_device(x, params):
@@ -38,6 +39,14 @@ def _grad_views(params, needs):
     return views
 
 
+def _flat_of(views):
+    """The 1-D flat buffer behind the gradient views of _grad_views."""
+    v = next(t for t in views if t is not None)
+    st = v.untyped_storage()
+    return torch.empty(0, dtype=torch.float32, device=v.device).set_(
+        st, 0, (st.nbytes() // 4,), (1,))
+
+
 class _LogitsFn(torch.autograd.Function):
     """x (NCHW) -> combined deep-supervision logits (NCHW)."""
 
@@ -53,7 +62,13 @@ class _LogitsFn(torch.autograd.Function):
         need = ctx.needs_input_grad
         views = _grad_views(ctx.params, need[2:])
         grads = {p: v for p, v in zip(ctx.params, views) if v is not None}
-        dx = ctx.graph.backward(ctx.state, grads, dlogits=dlogits.contiguous(), need_dx=need[1])
+        red = overlap_reducer()
+        if red is not None and grads:
+            red.begin(_flat_of(views), list(grads.values()))
+        dx = ctx.graph.backward(ctx.state, grads, dlogits=dlogits.contiguous(), need_dx=need[1],
+                                on_done=red.done if red is not None and grads else None)
+        if red is not None and grads:
+            red.flush()
         ctx.state = None
         return (None, dx, *views)
 

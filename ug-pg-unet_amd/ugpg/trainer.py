@@ -19,7 +19,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
-from .dist import allreduce_gradients, world
+from .dist import allreduce_gradients, overlapped_allreduce, world
 from .loss import UncertaintyGuidedLoss, weighted_loss_tensors
 from .optim import RMSprop
 from .unet import PGUNet1, PGUNet2, PGUNet3, PGUNet4, transfer_state
@@ -129,7 +129,8 @@ class UncertaintyGuidedProgressiveTrainer:
         mbuf = torch.zeros(8, dtype=torch.float32, device=data.device)
         self.optimizer.zero_grad()
         output, umap, final, _ = self._forward_device(data, target, stage, mbuf)
-        final.backward()
+        with overlapped_allreduce():  # data-parallel: buckets go to RCCL during the backward
+            final.backward()
         self.optimizer.grad_scale = allreduce_gradients(
             [p for g in self.optimizer.param_groups for p in g["params"]])
         self.optimizer.step()
