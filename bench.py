@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--conv-math", choices=("x6", "bf16", "f32"), default="x6",
+                    help="conv arithmetic: x6 = fp32-accurate split-bf16 (configs[1], default); "
+                         "bf16 = bf16 operands, fp32 accumulation (configs[2] arithmetic)")
     return ap.parse_args()
 
 
@@ -95,6 +98,7 @@ def main():
     from ugpg import ops
     from ugpg.dist import broadcast_parameters, init_from_env, max_over_ranks
 
+    ops.set_conv_math(args.conv_math)
     rank, world = init_from_env("nccl")
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
@@ -149,26 +153,33 @@ def main():
         dom = max(summ, key=lambda k: summ[k]["ms"])
         d = summ[dom]
         achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
-        x6 = ops.conv_math() == "x6"
-        peak = BF16_PEAK_TFLOPS / X6_PRODUCTS if x6 else FP32_PEAK_TFLOPS
-        traffic, src = pmc_traffic(dom)
+        math = ops.conv_math()
+        peak = {"x6": BF16_PEAK_TFLOPS / X6_PRODUCTS, "bf16": BF16_PEAK_TFLOPS}.get(
+            math, FP32_PEAK_TFLOPS)
+        traffic, src = pmc_traffic(dom) if math == "x6" else (None, None)
         roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2),
                 "peak": round(peak, 1), "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                 "traffic": traffic, "traffic_source": src,
-                "arithmetic": ("split-bf16 x6: fp32-accurate products from 6 bf16 MFMAs; peak = "
-                               "dense bf16 MFMA peak / 6" if x6 else "fp32 MFMA"),
+                "arithmetic": {"x6": "split-bf16 x6: fp32-accurate products from 6 bf16 MFMAs; "
+                                     "peak = dense bf16 MFMA peak / 6",
+                               "bf16": "bf16 operands, fp32 accumulation: dense bf16 MFMA peak"
+                               }.get(math, "fp32 MFMA"),
                 "flops_per_launch": round(d["flops"] / d["launches"]),
                 "avg_launch_ms": round(d["ms"] / d["launches"], 4)}
 
     result = {
         "metric": METRIC, "value": round(value, 3), "unit": "images/sec", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "bf16" if args.conv_math == "bf16" else "fp32",
         "data": "synthetic (x~N(0,1), masks~Bernoulli(0.5); random-init weights)",
         "config": {"workload": "Stage-4 uncertainty-guided train step: PGUNet4 fwd+bwd 256^2 + "
                                "PGUNet3 eval fwd 128^2 (U-map) + weighted BCE + RMSprop",
                    "per_gpu_batch": B, "global_batch": B * world, "resolution": R,
-                   "parallelism": f"dp{world}", "baseline_config": "BASELINE.json configs[1]"},
+                   "parallelism": f"dp{world}",
+                   "baseline_config": ("BASELINE.json configs[2] arithmetic (bf16 conv operands, "
+                                       "fp32 accumulation and storage)" if args.conv_math == "bf16"
+                                       else "BASELINE.json configs[1]")},
         "step_roofline": {"gflop_per_image": UG_STEP_GFLOP,
                           "achieved_tflops_per_gpu": round(value / world * UG_STEP_GFLOP / 1e3, 2),
                           "frac_of_fp32_peak": round(value / world * UG_STEP_GFLOP / 1e3 / FP32_PEAK_TFLOPS, 4)},

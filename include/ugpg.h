@@ -61,6 +61,10 @@ typedef struct {
  *                  6 v_mfma_f32_32x32x16_bf16 products per k-step with fp32
  *                  accumulation (product error < 2^-25 relative, below one fp32
  *                  rounding); needs K channels % 16 == 0 and N % 64 == 0.
+ *   UGPG_WFMT_BF16: bf16 arithmetic (BASELINE.json configs[2]) -- operands rounded
+ *                  to bf16 (round to nearest even), one v_mfma_f32_32x32x16_bf16
+ *                  product per k-step, fp32 accumulation and fp32 storage (what
+ *                  torch.autocast(bfloat16) does to a conv); same shape rules.
  * Input = channel-concat of src[0] and src[1] (src[1].data may be NULL):
  * this is the concat-free `torch.cat([x2, x1], dim=1)` of Up (UG_unet_parts.py:80).
  * Cin = src[0].C + src[1].C must be a multiple of 8 (pad the image to 8 channels).
@@ -79,11 +83,12 @@ typedef struct {
     int out_split;
     int accumulate[2];
     float* stats;
-    int wfmt;              /* UGPG_WFMT_F32 or UGPG_WFMT_X6 */
+    int wfmt;              /* UGPG_WFMT_F32, UGPG_WFMT_X6 or UGPG_WFMT_BF16 */
 } ugpg_conv_t;
 
 #define UGPG_WFMT_F32 0
 #define UGPG_WFMT_X6 1
+#define UGPG_WFMT_BF16 2
 
 /* Replaces aten::convolution forward (cuDNN/oneDNN) for DoubleConv's 3x3 convs. */
 int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream);
@@ -117,8 +122,9 @@ typedef struct {
     int Cin_real;
     float* db;             /* [Cout] or NULL */
     int accumulate;
-    int math;              /* UGPG_WFMT_X6: split-bf16 MFMA where the shape allows
-                              (db == NULL, 64-channel sources); else fp32 MFMA */
+    int math;              /* UGPG_WFMT_X6 (split-bf16) or UGPG_WFMT_BF16 (bf16) MFMA
+                              where the shape allows (db == NULL, 64-channel
+                              sources); else fp32 MFMA */
 } ugpg_wgrad_t;
 size_t ugpg_conv3x3_wgrad_workspace(const ugpg_wgrad_t* p);
 int ugpg_conv3x3_wgrad(const ugpg_wgrad_t* p, void* ws, size_t ws_bytes, void* stream);

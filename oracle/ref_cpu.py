@@ -105,9 +105,46 @@ def _bn(P, pre, x, training):
                         training, BN_MOMENTUM, BN_EPS)
 
 
+def _bq(t):
+    """Round to bf16 (nearest even) and back."""
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
+class _Bf16Conv3x3(torch.autograd.Function):
+    """A 3x3 / pad-1 conv in the build's bf16 arithmetic (BASELINE config 3 -- not a
+    reference behaviour; the reference is fp32-only): forward conv(bf16(x), bf16(w)),
+    data gradient conv_T(bf16(dy), bf16(w)), weight gradient of bf16(dy) and bf16(x),
+    all accumulated in fp32 (bf16 x bf16 products are exact in fp32)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        xq, wq = _bq(x), _bq(w)
+        ctx.save_for_backward(xq, wq)
+        return F.conv2d(xq, wq, b, padding=1)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xq, wq = ctx.saved_tensors
+        dyq = _bq(dy)
+        dx = torch.nn.grad.conv2d_input(xq.shape, wq, dyq, padding=1)
+        dw = torch.nn.grad.conv2d_weight(xq, wq.shape, dyq, padding=1)
+        return dx, dw, dy.sum(dim=(0, 2, 3))
+
+
+# conv arithmetic of double_conv: "f32" (the reference) or "bf16" (the build's
+# config-3 arithmetic, applied where the build runs it: 16-channel-multiple inputs)
+CONV_MATH = "f32"
+
+
+def conv3x3(x, w, b):
+    if CONV_MATH == "bf16" and x.shape[1] % 16 == 0:
+        return _Bf16Conv3x3.apply(x, w, b)
+    return F.conv2d(x, w, b, padding=1)
+
+
 def double_conv(P, prefix, x, training):
     for conv_i, bn_i in ((0, 1), (3, 4)):
-        x = F.conv2d(x, P[f"{prefix}.{conv_i}.weight"], P[f"{prefix}.{conv_i}.bias"], padding=1)
+        x = conv3x3(x, P[f"{prefix}.{conv_i}.weight"], P[f"{prefix}.{conv_i}.bias"])
         x = F.relu(_bn(P, f"{prefix}.{bn_i}", x, training), inplace=True)
     return x
 

@@ -220,3 +220,62 @@ def test_backward_reports_gradients_back_to_front(dev, monkeypatch):
     for prev, cur in zip(rec.calls, rec.calls[1:]):
         if cur:
             assert max(cur) < min(prev), (prev, cur)
+
+
+@pytest.mark.parametrize("res", [64, 256])
+def test_bf16_train_step(dev, res):
+    """bf16 arithmetic (BASELINE config 3): every 3x3 conv with bf16-rounded operands
+    (forward x, W; data gradient dy, W; weight gradient dy, x), fp32 accumulation and
+    storage.  Each conv is exact to that arithmetic (test_gpu_ops.py, math "bf16");
+    through the network, a few-ulp fp32 difference upstream (fmaf-folded BatchNorm
+    vs the oracle's (y-mean)*invstd*w+b, summation order) moves values across bf16
+    rounding boundaries, and train-mode BatchNorm's backward (g - mean(g) -
+    xhat*mean(g*xhat)) amplifies that noise, so the network is compared with
+    tolerances: vs the oracle in the same arithmetic (CONV_MATH = "bf16") logits
+    within 2 % of their range, loss 0.5 %, per-tensor gradient cosine median > 0.95
+    and min > 0.9; vs the fp32 reference loss within 1 %, Dice within 0.01."""
+    import torch.nn as nn
+    from ugpg import ops
+    from ugpg.loss import UncertaintyGuidedLoss
+    state = det_state(4, 3, 1)
+    x = G.randn(1, (2, 3, res, res), "x")
+    t = G.bernoulli(2, (2, 1, res, res), 0.5, "t")
+    logits32, final32, _, _, _ = oracle_run(4, state, x, t)
+    O.CONV_MATH = "bf16"
+    try:
+        logits16, final16, _, g16, _ = oracle_run(4, state, x, t)
+    finally:
+        O.CONV_MATH = "f32"
+    old = ops.conv_math()
+    ops.set_conv_math("bf16")
+    try:
+        m = build(4, 1, state, dev)
+        out = m(x.to(dev))
+        crit = nn.BCEWithLogitsLoss(pos_weight=torch.tensor([5.0], device=dev), reduction="none")
+        final, _ = UncertaintyGuidedLoss(dev).apply_uncertainty_weighted_loss(crit, out, t.to(dev))
+        final.backward()
+        torch.cuda.synchronize()
+    finally:
+        ops.set_conv_math(old)
+    o = out.detach().cpu()
+    err16 = (o - logits16).abs().max().item() / (logits16.max() - logits16.min()).item()
+    err32 = (o - logits32).abs().max().item() / (logits32.max() - logits32.min()).item()
+    coss = {}
+    for k, p in zip(param_keys(state), m.parameters()):
+        if is_prebn_bias(k):
+            continue
+        a, b = p.grad.detach().cpu().double().flatten(), g16[k].double().flatten()
+        coss[k] = (a @ b / (a.norm() * b.norm() + 1e-30)).item()
+    worst = min(coss, key=coss.get)
+    d = O.dice(O.predictions(o), t).item()
+    d32 = O.dice(O.predictions(logits32), t).item()
+    med = float(np.median(list(coss.values())))
+    print(f"bf16 res {res}: logits vs bf16 oracle {err16:.2e}, vs fp32 {err32:.2e}; loss "
+          f"{final.item():.6f} vs {final16.item():.6f} (bf16 oracle) {final32.item():.6f} (fp32); "
+          f"grad cosine vs bf16 oracle median {med:.4f} min {coss[worst]:.4f} ({worst}); "
+          f"dice {d:.4f} vs fp32 {d32:.4f}")
+    assert err16 < 2e-2, err16
+    assert abs(final.item() - final16.item()) <= 5e-3 * abs(final16.item())
+    assert med > 0.95 and coss[worst] > 0.9, (med, worst, coss[worst])
+    assert abs(final.item() - final32.item()) <= 1e-2 * abs(final32.item())
+    assert abs(d - d32) <= 1e-2, (d, d32)

@@ -31,10 +31,19 @@ def close(a, b, tol, what=""):
     assert err <= tol * scale, f"{what}: max|diff| {err:.3e} > {tol:.1e} * {scale:.3e}"
 
 
+def bq(t, on=True):
+    """The operand as the bf16 arithmetic sees it: rounded to bf16 (nearest even)."""
+    return t.to(torch.bfloat16).to(t.dtype) if on else t
+
+
 def act_ref(y, scale, shift):
+    """relu(scale*y + shift) rounded once to fp32, as the kernels' fmaf computes it
+    (a twice-rounded reference can sit one fp32 ulp off, which the bf16 arithmetic
+    turns into a whole bf16 rounding step)."""
     if scale is None:
         return y
-    return torch.relu(y * scale.view(1, -1, 1, 1) + shift.view(1, -1, 1, 1))
+    a = y.double() * scale.double().view(1, -1, 1, 1) + shift.double().view(1, -1, 1, 1)
+    return torch.relu(a.float())
 
 
 CONV_CASES = [
@@ -62,14 +71,14 @@ BIG = {5, 6, 7}
 X6_FORMS = {"x6": 1, "x6s": 0}
 
 
-@pytest.fixture(params=["x6", "x6s", "f32"])
+@pytest.fixture(params=["x6", "x6s", "f32", "bf16"])
 def math(request):
-    """Both conv arithmetic forms: split-bf16 (default, every forward kernel form)
-    and fp32 MFMA."""
+    """Every conv arithmetic form: split-bf16 (default, every kernel form), fp32
+    MFMA, and bf16 (BASELINE config 3: operands rounded to bf16, fp32 accumulation)."""
     from ugpg import ops
     from ugpg._C import lib
     old = ops.conv_math()
-    ops.set_conv_math("f32" if request.param == "f32" else "x6")
+    ops.set_conv_math({"f32": "f32", "bf16": "bf16"}.get(request.param, "x6"))
     lib.ugpg_set_tuning(b"x6_pipe", X6_FORMS.get(request.param, 1))
     lib.ugpg_set_tuning(b"x6_wgrad", X6_FORMS.get(request.param, 1))
     yield request.param
@@ -95,7 +104,8 @@ def test_conv3x3_fwd_stats(dev, case, math):
     inp = act_ref(x0, sc0, sh0)
     if C1:
         inp = torch.cat([inp, act_ref(x1, sc1, sh1) if affine else x1], 1)
-    ref = F.conv2d(inp.double(), w.double(), b.double(), padding=1)
+    half = math == "bf16" and cin % 16 == 0  # runs in bf16 arithmetic
+    ref = F.conv2d(bq(inp, half).double(), bq(w, half).double(), b.double(), padding=1)
 
     g = lambda t: None if t is None else t.to(dev)
     srcs = [ops.Act(nhwc(x0).to(dev), g(sc0), g(sh0))]
@@ -103,7 +113,8 @@ def test_conv3x3_fwd_stats(dev, case, math):
         srcs.append(ops.Act(nhwc(x1).to(dev), g(sc1), g(sh1)))
     wpk = ops.pack_conv3x3(w.to(dev), cin, 0)
     out = torch.empty(B, H, W, Cout, device=dev)
-    assert wpk.ugpg_fmt == (ops.WFMT_X6 if math != "f32" and cin % 16 == 0 else ops.WFMT_F32)
+    fmt = {"f32": ops.WFMT_F32, "bf16": ops.WFMT_BF16}.get(math, ops.WFMT_X6)
+    assert wpk.ugpg_fmt == (fmt if cin % 16 == 0 else ops.WFMT_F32)
     nt = ops.conv_ntiles(B, H, W, cin, Cout, wpk)
     stats = torch.empty(3 * Cout * nt, device=dev)
     ops.conv3x3_fwd(srcs, wpk, b.to(dev), Cout, [out], stats=stats)
@@ -142,6 +153,12 @@ def test_conv3x3_dgrad_wgrad(dev, case, math):
     bd = torch.zeros(Cout, dtype=torch.float64, requires_grad=True)
     y = F.conv2d(xin, wd, bd, padding=1)
     y.backward(dy.double())
+    # bf16 arithmetic: the same gradients of bf16-rounded operands (dgrad: dy, W;
+    # wgrad: dy, act(x)), accumulated exactly
+    half = math == "bf16"
+    xq = bq(xin.detach(), half).clone().requires_grad_(True)
+    wq = bq(wd.detach(), half).clone().requires_grad_(True)
+    F.conv2d(xq, wq, None, padding=1).backward(bq(dy.double(), half))
     # dgrad (only for real input channels that are multiples of 64)
     if cin_real % 64 == 0:
         wpk = ops.pack_conv3x3(w.to(dev), cin_real, 1)
@@ -150,12 +167,12 @@ def test_conv3x3_dgrad_wgrad(dev, case, math):
             d1 = torch.full((B, H, W, C1), 0.5, device=dev)
             ops.conv3x3_fwd([ops.Act(nhwc(dy).to(dev))], wpk, None, cin_real, [d0, d1], split=C0,
                             accumulate=(0, 1))
-            close(nchw(d0.cpu()), xin.grad[:, :C0], 2e-5, "dgrad src0")
-            close(nchw(d1.cpu()) - 0.5, xin.grad[:, C0:], 2e-5, "dgrad src1 (accumulate)")
+            close(nchw(d0.cpu()), xq.grad[:, :C0], 2e-5, "dgrad src0")
+            close(nchw(d1.cpu()) - 0.5, xq.grad[:, C0:], 2e-5, "dgrad src1 (accumulate)")
         else:
             dx = torch.empty(B, H, W, cin_real, device=dev)
             ops.conv3x3_fwd([ops.Act(nhwc(dy).to(dev))], wpk, None, cin_real, [dx])
-            close(nchw(dx.cpu()), xin.grad, 2e-5, "dgrad")
+            close(nchw(dx.cpu()), xq.grad, 2e-5, "dgrad")
     # wgrad on the activated (lazy) source
     g = lambda t: None if t is None else t.to(dev)
     xs = nhwc(x).to(dev)
@@ -173,7 +190,8 @@ def test_conv3x3_dgrad_wgrad(dev, case, math):
     # layer, the split-bf16 kernel for 64-channel sources under math "x6"
     dw2 = torch.empty(Cout, cin_real, 3, 3, device=dev)
     ops.conv3x3_wgrad(srcs, nhwc(dy).to(dev), dw2, None, cin_real)
-    close(dw2.cpu(), wd.grad, 2e-5, f"wgrad without db ({math})")
+    split = cin_real % 64 == 0 and C0 % 64 == 0  # the split-bf16 / bf16 wgrad kernel
+    close(dw2.cpu(), wq.grad if split else wd.grad, 2e-5, f"wgrad without db ({math})")
 
 
 @pytest.mark.parametrize("shape", [(4, 64, 64, 64, 64), (2, 32, 32, 512, 512), (2, 16, 16, 256, 128)])

@@ -633,7 +633,7 @@ extern "C" int ugpg_set_tuning(const char* key, int value) {
 
 extern "C" int ugpg_conv3x3_fwd_ntiles(int B, int H, int W, int Cin, int Cout, int wfmt) {
     (void)Cin;
-    if (wfmt == UGPG_WFMT_X6)
+    if (wfmt == UGPG_WFMT_X6 || wfmt == UGPG_WFMT_BF16)
         return fwd_x6_stat_slots((int)(B * cdiv(H, fwd_x6_tile_h(W)) * cdiv(W, fwd_x6_tile_w(W))), W);
     const int cfg = pick_fwd_cfg(B, H, W, Cout, Cout);
     return (int)(B * cdiv(H, kFwd[cfg].th) * cdiv(W, kFwd[cfg].tw));
@@ -655,11 +655,12 @@ extern "C" int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream) {
         set_error("conv3x3_fwd: bad out_split %d (Cout %d)", p->out_split, p->Cout);
         return UGPG_ERR_INVALID;
     }
-    if (p->wfmt != UGPG_WFMT_F32 && p->wfmt != UGPG_WFMT_X6) {
+    const bool split = p->wfmt == UGPG_WFMT_X6 || p->wfmt == UGPG_WFMT_BF16;
+    if (p->wfmt != UGPG_WFMT_F32 && !split) {
         set_error("conv3x3_fwd: unknown weight format %d", p->wfmt);
         return UGPG_ERR_INVALID;
     }
-    if (p->wfmt == UGPG_WFMT_X6 && (C0 % 16 || C1 % 16)) {
+    if (split && (C0 % 16 || C1 % 16)) {
         set_error("conv3x3_fwd: split-bf16 path needs 16-channel sources (C0=%d C1=%d)", C0, C1);
         return UGPG_ERR_INVALID;
     }
@@ -687,11 +688,11 @@ extern "C" int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream) {
     a.Cin = Cin;
     a.Cout = p->Cout;
     hipStream_t st = as_stream(stream);
-    if (p->wfmt == UGPG_WFMT_X6) {
+    if (split) {
         a.tiles_x = (int)cdiv(p->W, fwd_x6_tile_w(p->W));
         a.tiles_y = (int)cdiv(p->H, fwd_x6_tile_h(p->W));
         a.ntiles = p->B * a.tiles_x * a.tiles_y;
-        launch_fwd_x6(a, st);
+        launch_fwd_x6(a, p->wfmt == UGPG_WFMT_X6 ? 3 : 1, st);
         return check_launch("conv3x3_fwd_x6");
     }
     const int cfg = pick_fwd_cfg(p->B, p->H, p->W, p->Cout, p->out_split);
@@ -723,25 +724,26 @@ extern "C" int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream) {
 
 extern "C" size_t ugpg_pack_conv3x3_bytes(int Cout, int Cin_pad, int wfmt) {
     const size_t n = (size_t)Cin_pad * 9 * Cout;
-    return wfmt == UGPG_WFMT_X6 ? n * 3 * 2 : n * 4;
+    return wfmt == UGPG_WFMT_X6 ? n * 3 * 2 : wfmt == UGPG_WFMT_BF16 ? n * 2 : n * 4;
 }
 
 extern "C" int ugpg_pack_conv3x3(const float* w, void* wpk, int Cout, int Cin, int Cin_pad,
                                  int mode, int wfmt, void* stream) {
     if (!w || !wpk || Cin_pad < Cin || Cin_pad % 8 || (mode == 1 && Cout % 8) || mode < 0 ||
-        mode > 1 || (wfmt != UGPG_WFMT_F32 && wfmt != UGPG_WFMT_X6)) {
+        mode > 1 || (wfmt != UGPG_WFMT_F32 && wfmt != UGPG_WFMT_X6 && wfmt != UGPG_WFMT_BF16)) {
         set_error("pack_conv3x3: bad arguments (Cout=%d Cin=%d Cin_pad=%d mode=%d wfmt=%d)", Cout,
                   Cin, Cin_pad, mode, wfmt);
         return UGPG_ERR_INVALID;
     }
-    if (wfmt == UGPG_WFMT_X6) {
+    if (wfmt == UGPG_WFMT_X6 || wfmt == UGPG_WFMT_BF16) {
         const int N = mode == 0 ? Cout : Cin_pad, K = mode == 0 ? Cin_pad : Cout;
         if (N % 64 || K % 16) {
             set_error("pack_conv3x3: split-bf16 format needs N %% 64 == 0 and K %% 16 == 0 "
                       "(N=%d K=%d)", N, K);
             return UGPG_ERR_INVALID;
         }
-        launch_pack_x6(w, wpk, Cout, Cin, Cin_pad, mode, as_stream(stream));
+        launch_pack_x6(w, wpk, Cout, Cin, Cin_pad, mode, wfmt == UGPG_WFMT_X6 ? 3 : 1,
+                       as_stream(stream));
         return check_launch("pack_conv3x3_x6");
     }
     const int64_t total = (int64_t)Cin_pad * 9 * Cout;
@@ -767,18 +769,22 @@ enum WgradKind { WG_GENERIC, WG_C8, WG_X6 };
 
 static WgradKind wgrad_kind(const ugpg_wgrad_t* p, int C0, int C1) {
     if (wgrad_use_c8(C0, C1, p->db)) return WG_C8;
-    if (p->math == UGPG_WFMT_X6 && !p->db && C0 % 64 == 0 && C1 % 64 == 0) return WG_X6;
+    if ((p->math == UGPG_WFMT_X6 || p->math == UGPG_WFMT_BF16) && !p->db && C0 % 64 == 0 &&
+        C1 % 64 == 0)
+        return WG_X6;
     return WG_GENERIC;
 }
 
 static WgradPlan wgrad_plan_for(const ugpg_wgrad_t* p, WgradKind k, int Cin) {
     if (k == WG_C8) return wgrad_plan_c8(p->B, p->H, p->W, p->Cout);
     if (k == WG_X6) {
-        WgradPlan w = wgrad_plan(p->B, p->H, p->W, Cin, p->Cout, g_x6_wgrad ? WGX6W_TH : WGX6_TH,
+        // bf16 (1 piece) always runs the persistent kernel
+        const bool persist = g_x6_wgrad || p->math == UGPG_WFMT_BF16;
+        WgradPlan w = wgrad_plan(p->B, p->H, p->W, Cin, p->Cout, persist ? WGX6W_TH : WGX6_TH,
                                  WGX6_TW);
         // persistent kernel: about one item per CU, planned for the MI355X's 256 CUs
         // (a fixed count keeps the split, hence the summation order, device-independent)
-        if (g_x6_wgrad) wgrad_x6w_plan(w.ntiles, p->Cout, Cin, 256, w.nsplit, w.tps);
+        if (persist) wgrad_x6w_plan(w.ntiles, p->Cout, Cin, 256, w.nsplit, w.tps);
         return w;
     }
     return wgrad_plan(p->B, p->H, p->W, Cin, p->Cout);
@@ -828,7 +834,8 @@ extern "C" int ugpg_conv3x3_wgrad(const ugpg_wgrad_t* p, void* ws, size_t ws_byt
     a.tps = w.tps;
     hipStream_t st = as_stream(stream);
     if (kind == WG_X6) {
-        launch_wgrad_x6(a, (unsigned)((p->Cout / 64) * (Cin / 64) * w.nsplit), st);
+        launch_wgrad_x6(a, (unsigned)((p->Cout / 64) * (Cin / 64) * w.nsplit),
+                        p->math == UGPG_WFMT_BF16 ? 1 : 3, st);
     } else if (kind == WG_C8) {
         const unsigned grid = (unsigned)((p->Cout / 64) * w.nsplit);
         hipLaunchKernelGGL((conv3x3_wgrad_c8_kernel<WG8_TH, WG8_TW>), dim3(grid), dim3(192), 0, st,

@@ -160,18 +160,18 @@ struct WgradArgs {
 };
 
 // split-bf16 path (conv_x6.hip)
-void launch_fwd_x6(const ConvFwdArgs& a, hipStream_t st);
+void launch_fwd_x6(const ConvFwdArgs& a, int np, hipStream_t st);  // np: bf16 pieces (3 or 1)
 extern int g_x6_pipe, g_x6_probe;
 int fwd_x6_tile_w(int W);  // 32 or 16
 int fwd_x6_tile_h(int W);  // 4 or 8
 int fwd_x6_stat_slots(int ntiles, int W);  // BatchNorm partial slots the forward writes
-void launch_wgrad_x6(const WgradArgs& a, unsigned grid, hipStream_t st);
+void launch_wgrad_x6(const WgradArgs& a, unsigned grid, int np, hipStream_t st);
 extern int g_x6_wgrad;  // tuning knob "x6_wgrad"
 // split plan of the persistent split-bf16 wgrad (deterministic: planned for `cus` CUs)
 void wgrad_x6w_plan(int ntiles, int Cout, int Cin, int cus, int& nsplit, int& tps);
 constexpr int WGX6_TH = 2, WGX6_TW = 16;  // pixel tile of the split-bf16 wgrad
 constexpr int WGX6W_TH = 4;                // rows of its persistent form's tile (x 16)
-void launch_pack_x6(const float* w, void* wpk, int Cout, int Cin, int Cin_pad, int mode,
+void launch_pack_x6(const float* w, void* wpk, int Cout, int Cin, int Cin_pad, int mode, int np,
                     hipStream_t st);
 
 }  // namespace ugpg

@@ -91,18 +91,35 @@ __device__ __forceinline__ f32x16 mfma16(u32x4 a, u32x4 b, f32x16 c) {
                                                    __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
 }
 
-// acc += a*b to fp32 accuracy from the pieces (smallest terms first)
-__device__ __forceinline__ f32x16 mfma_x6(const u32x4 (&a)[3], const u32x4 (&b)[3], f32x16 c) {
-    c = mfma16(a[2], b[0], c);
-    c = mfma16(a[1], b[1], c);
-    c = mfma16(a[0], b[2], c);
-    c = mfma16(a[1], b[0], c);
-    c = mfma16(a[0], b[1], c);
+// acc += a*b from the pieces: NP = 3 -> fp32 accuracy (the six products of order
+// <= 2, smallest terms first); NP = 1 -> one bf16 product (the "bf16" arithmetic of
+// BASELINE config 3: operands rounded to bf16, fp32 accumulation)
+template <int NP>
+__device__ __forceinline__ f32x16 mfma_xn(const u32x4 (&a)[NP], const u32x4 (&b)[NP], f32x16 c) {
+    if constexpr (NP == 3) {
+        c = mfma16(a[2], b[0], c);
+        c = mfma16(a[1], b[1], c);
+        c = mfma16(a[0], b[2], c);
+        c = mfma16(a[1], b[0], c);
+        c = mfma16(a[0], b[1], c);
+    }
     c = mfma16(a[0], b[0], c);
     return c;
 }
+__device__ __forceinline__ f32x16 mfma_x6(const u32x4 (&a)[3], const u32x4 (&b)[3], f32x16 c) {
+    return mfma_xn<3>(a, b, c);
+}
+// the first NP pieces of x (NP = 1: bf16(x), round to nearest even)
+template <int NP>
+__device__ __forceinline__ void split_n(f32x8 v, u32x4 (&p)[NP]) {
+    if constexpr (NP == 3) {
+        split3(v, p[0], p[1], p[2]);
+    } else {
+        p[0] = __builtin_bit_cast(u32x4, __builtin_convertvector(v, bf16x8));
+    }
+}
 
-template <int TH, int TW, bool PERM16>
+template <int TH, int TW, bool PERM16, int NP>
 __global__ void __launch_bounds__(256) conv3x3_fwd_x6_kernel(ConvFwdArgs a) {
     constexpr int BN = 64, BKC = 16, WM = 2, WN = 2, MT = 2, NT = 1;
     static_assert(TH * TW == 128, "tile must be 128 pixels");
@@ -113,9 +130,9 @@ __global__ void __launch_bounds__(256) conv3x3_fwd_x6_kernel(ConvFwdArgs a) {
     constexpr int NHP = NHP0 + (12 - NHP0 % 8) % 8;  // = 4 (mod 8): h planes 64 B apart mod 128
     constexpr int A_ITEMS = NHALO * 2;           // (pixel, channel half) items
     constexpr int A_PER = (A_ITEMS + 255) / 256;
-    constexpr int B_VEC = 6 * 9 * BN;            // 16-B vectors of the weight slab
+    constexpr int B_VEC = 2 * NP * 9 * BN;       // 16-B vectors of the weight slab
     constexpr int B_PER = (B_VEC + 255) / 256;
-    constexpr int A_VECS = 6 * NHP;
+    constexpr int A_VECS = 2 * NP * NHP;
     __shared__ __attribute__((aligned(16))) u32x4 smem[A_VECS + B_VEC];
     u32x4* As = smem;
     u32x4* Bs = smem + A_VECS;
@@ -184,12 +201,11 @@ __global__ void __launch_bounds__(256) conv3x3_fwd_x6_kernel(ConvFwdArgs a) {
                 f32x4 lo4 = act_reg4(ra[v][0], ract0, aon), hi4 = act_reg4(ra[v][1], ract1, aon);
                 if (!((avalid >> v) & 1u)) lo4 = hi4 = f32x4{0.f, 0.f, 0.f, 0.f};
                 const f32x8 x = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
-                u32x4 p0, p1, p2;
-                split3(x, p0, p1, p2);
+                u32x4 pc[NP];
+                split_n<NP>(x, pc);
                 const int hl = (hp / HWD) * HS + hp % HWD;
-                As[(0 * 2 + hh) * NHP + hl] = p0;
-                As[(1 * 2 + hh) * NHP + hl] = p1;
-                As[(2 * 2 + hh) * NHP + hl] = p2;
+#pragma unroll
+                for (int q = 0; q < NP; ++q) As[(q * 2 + hh) * NHP + hl] = pc[q];
             }
         }
 #pragma unroll
@@ -214,13 +230,13 @@ __global__ void __launch_bounds__(256) conv3x3_fwd_x6_kernel(ConvFwdArgs a) {
     }
     const int boff = hl * 3 * BN + wn * 32 + (lane & 31);
 
-    auto ldfrag = [&](int t, u32x4 (&af)[MT][3], u32x4 (&bf)[3]) {
+    auto ldfrag = [&](int t, u32x4 (&af)[MT][NP], u32x4 (&bf)[NP]) {
         const int toff = (t / 3) * HS + (t % 3);
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
+        for (int q = 0; q < NP; ++q) {
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt) af[mt][q] = As[q * 2 * NHP + aoff[mt] + toff];
-            bf[q] = Bs[(((t / 3) * 3 + q) * 2) * 3 * BN + boff + (t % 3) * BN];
+            bf[q] = Bs[(((t / 3) * NP + q) * 2) * 3 * BN + boff + (t % 3) * BN];
         }
     };
 
@@ -229,13 +245,13 @@ __global__ void __launch_bounds__(256) conv3x3_fwd_x6_kernel(ConvFwdArgs a) {
     __syncthreads();
     for (int c = 0; c < nchunk; ++c) {
         if (c + 1 < nchunk && !(a.probe & 1)) gload(c + 1);
-        u32x4 fa[2][MT][3], fb[2][3];
+        u32x4 fa[2][MT][NP], fb[2][NP];
         ldfrag(0, fa[0], fb[0]);
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
             if (t + 1 < 9) ldfrag(t + 1, fa[(t + 1) & 1], fb[(t + 1) & 1]);
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt) acc[mt][0] = mfma_x6(fa[t & 1][mt], fb[t & 1], acc[mt][0]);
+            for (int mt = 0; mt < MT; ++mt) acc[mt][0] = mfma_xn<NP>(fa[t & 1][mt], fb[t & 1], acc[mt][0]);
         }
         if (a.probe & 2) continue;
         __syncthreads();
@@ -358,6 +374,7 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
     }
 }
 
+template <int NP>
 __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) {
     constexpr int TH = 8, TW = 32, BN = 64, BKC = 16, MT = 4;
     constexpr int HWD = TW + 2, HS = HWD;
@@ -365,9 +382,9 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
     constexpr int NHP = NHALO + 1 + (11 - NHALO % 8) % 8;   // 348: spare slot NHALO, = 4 (mod 8)
     constexpr int A_ITEMS = NHALO * 2;                      // (pixel, channel half)
     constexpr int A_PER = (A_ITEMS + 255) / 256;            // 3
-    constexpr int A_VECS = 6 * NHP;
-    constexpr int R_VEC = 3 * 2 * 3 * BN;                   // one kernel row of weights: 1152
-    constexpr int R_PER = (R_VEC + 255) / 256;              // 5 (the last one half-used)
+    constexpr int A_VECS = 2 * NP * NHP;
+    constexpr int R_VEC = NP * 2 * 3 * BN;                  // one kernel row of weights
+    constexpr int R_PER = (R_VEC + 255) / 256;
     constexpr int R_STR = R_VEC;                            // ring slot pitch
     constexpr int NSLOT = 4;
     __shared__ __attribute__((aligned(16))) u32x4 smem[2 * A_VECS + NSLOT * R_STR + 1];
@@ -461,12 +478,11 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
                 const f32x8 x = {ok ? lo4.x : 0.f, ok ? lo4.y : 0.f, ok ? lo4.z : 0.f,
                                  ok ? lo4.w : 0.f, ok ? hi4.x : 0.f, ok ? hi4.y : 0.f,
                                  ok ? hi4.z : 0.f, ok ? hi4.w : 0.f};
-                u32x4 p0, p1, p2;
-                split3(x, p0, p1, p2);
+                u32x4 pc[NP];
+                split_n<NP>(x, pc);
                 const int hl = idx < A_ITEMS ? (hp / HWD) * HS + hp % HWD : NHALO;
-                As[(0 * 2 + hh) * NHP + hl] = p0;
-                As[(1 * 2 + hh) * NHP + hl] = p1;
-                As[(2 * 2 + hh) * NHP + hl] = p2;
+#pragma unroll
+                for (int q = 0; q < NP; ++q) As[(q * 2 + hh) * NHP + hl] = pc[q];
             }
         };
         auto load_row = [&](int k, int ky) {
@@ -533,10 +549,10 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
     const int hl = lane >> 5;
     const int aoff = hl * NHP + (wm * MT) * HS + (lane & 31);  // + mt*HS + ky*HS + kx
     const int boff = hl * 3 * BN + wn * 32 + (lane & 31);
-    auto ldfrag = [&](const u32x4* As, const u32x4* Bs, int ky, int kx, u32x4 (&af)[MT][3],
-                      u32x4 (&bf)[3]) {
+    auto ldfrag = [&](const u32x4* As, const u32x4* Bs, int ky, int kx, u32x4 (&af)[MT][NP],
+                      u32x4 (&bf)[NP]) {
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
+        for (int q = 0; q < NP; ++q) {
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt) af[mt][q] = As[q * 2 * NHP + aoff + (mt + ky) * HS + kx];
             bf[q] = Bs[q * 2 * 3 * BN + boff + kx * BN];
@@ -551,7 +567,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
     Pos cp = pos_of(item0);
     for (int k = 0; k < total; ++k) {
         const u32x4* Ac = smem + (k & 1) * A_VECS;
-        u32x4 fa[2][MT][3], fb[2][3];
+        u32x4 fa[2][MT][NP], fb[2][NP];
         ldfrag(Ac, Bring + ((3 * k) % NSLOT) * R_STR, 0, 0, fa[0], fb[0]);
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
@@ -561,13 +577,17 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
                        fb[(t + 1) & 1]);
             }
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma_x6(fa[t & 1][mt], fb[t & 1], acc[mt]);
-            // the next tap's 15 fragment reads go out one per MFMA gap from the start
-            // of this tap's 24 MFMAs (fresh registers, landed long before their use)
+            for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma_xn<NP>(fa[t & 1][mt], fb[t & 1], acc[mt]);
+            // the next tap's fragment reads go out one per MFMA gap from the start of
+            // this tap's MFMAs (fresh registers, landed long before their use)
+            constexpr int NM = MT * (NP == 3 ? 6 : 1), NR = (MT + 1) * NP;
 #pragma unroll
-            for (int i = 0; i < 24; ++i) {
+            for (int i = 0; i < NM; ++i) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                     // MFMA
-                if (t + 1 < 9 && i < 15) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+                if (t + 1 < 9 && i < NR) {
+                    if constexpr (NR <= NM) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    else __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                }
             }
             __builtin_amdgcn_sched_barrier(0);  // taps do not mix
             if (t % 3 == 2) read_barrier();
@@ -609,6 +629,15 @@ __device__ __forceinline__ void split3_4(f32x4 v, u32x2& p0, u32x2& p1, u32x2& p
     p0 = __builtin_bit_cast(u32x2, h);
     p1 = __builtin_bit_cast(u32x2, m);
     p2 = __builtin_bit_cast(u32x2, l);
+}
+
+template <int NP>
+__device__ __forceinline__ void split_n4(f32x4 v, u32x2 (&p)[NP]) {
+    if constexpr (NP == 3) {
+        split3_4(v, p[0], p[1], p[2]);
+    } else {
+        p[0] = __builtin_bit_cast(u32x2, __builtin_convertvector(v, bf16x4));
+    }
 }
 
 __device__ __forceinline__ u32x2 ds_read_tr(const char* lds_byte_addr) {
@@ -783,16 +812,22 @@ __global__ void __launch_bounds__(256, 2) conv3x3_wgrad_x6_kernel(WgradArgs a) {
 // image from registers loaded during step k-1, then issue the loads of tile k+2
 // (untracked loads + counted vmcnt, so they stay in flight across the barrier).
 // ---------------------------------------------------------------------------
-template <int TH, int TW>
+// record pitch of the wgrad LDS images: NP pieces x 64 ch x 2 B, padded so that 4
+// consecutive records x 32 channels cover 64 distinct banks (pitch = 48 dwords mod 64)
+template <int NP>
+constexpr int wrec() { return NP == 3 ? WX_REC : 192; }
+
+template <int TH, int TW, int NP>
 __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) {
+    constexpr int REC = wrec<NP>();
     static_assert(TW == 16, "one 16-pixel row per MFMA k-step");
     constexpr int P = TH * TW, HWD = TW + 2, NHALO = (TH + 2) * HWD;
     constexpr int DY_Q = P * 16, X_Q = NHALO * 16;  // float4 quads per tile
     constexpr int DY_PER = (DY_Q + 255) / 256, X_PER = (X_Q + 255) / 256;
     constexpr int RECS = P + NHALO;                  // records per buffer
     constexpr int LOADS = DY_PER + X_PER + 2;        // loader VMEM instructions per step
-    __shared__ __attribute__((aligned(16))) char smem[(2 * RECS + 1) * WX_REC];
-    char* const dummy = smem + 2 * RECS * WX_REC;    // record for idle lanes' writes
+    __shared__ __attribute__((aligned(16))) char smem[(2 * RECS + 1) * REC];
+    char* const dummy = smem + 2 * RECS * REC;    // record for idle lanes' writes
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const bool loader = wave >= 4;
@@ -879,28 +914,27 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
         };
         // record layout: [piece][64 ch] bf16 at byte piece*128 + ch*2
         auto put = [&](char* rec, int q, f32x4 v) {
-            u32x2 p0, p1, p2;
-            split3_4(v, p0, p1, p2);
+            u32x2 pc[NP];
+            split_n4<NP>(v, pc);
             char* r = rec + q * 8;
-            *reinterpret_cast<u32x2*>(r) = p0;
-            *reinterpret_cast<u32x2*>(r + 128) = p1;
-            *reinterpret_cast<u32x2*>(r + 256) = p2;
+#pragma unroll
+            for (int k = 0; k < NP; ++k) *reinterpret_cast<u32x2*>(r + 128 * k) = pc[k];
         };
         auto lstore = [&](int buf) {
-            char* dys = smem + buf * RECS * WX_REC;
-            char* xs = dys + P * WX_REC;
+            char* dys = smem + buf * RECS * REC;
+            char* xs = dys + P * REC;
 #pragma unroll
             for (int v = 0; v < DY_PER; ++v) {
                 const int idx = lt + v * 256;
                 const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-                put(dys + (idx >> 4) * WX_REC, idx & 15, ((dvalid >> v) & 1u) ? rdy[v] : z);
+                put(dys + (idx >> 4) * REC, idx & 15, ((dvalid >> v) & 1u) ? rdy[v] : z);
             }
 #pragma unroll
             for (int v = 0; v < X_PER; ++v) {
                 const int idx = lt + v * 256;
                 const f32x4 z = {0.f, 0.f, 0.f, 0.f};
                 const f32x4 val = ((xvalid >> v) & 1u) ? act_floor4(rx[v], xa, xlo) : z;
-                put(idx < X_Q ? xs + (idx >> 4) * WX_REC : dummy, idx & 15, val);
+                put(idx < X_Q ? xs + (idx >> 4) * REC : dummy, idx & 15, val);
             }
         };
         Cur lc;
@@ -939,28 +973,28 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
     item_range(item0, cc);
     lds_barrier();  // step 0 staged
     for (int k = 0; k < total; ++k) {
-        const char* dys = smem + (k & 1) * RECS * WX_REC;
-        const char* abase = dys + pix_in * WX_REC + ch_a * 2;
-        const char* bbase = dys + P * WX_REC + pix_in * WX_REC + ch_b * 2;
-        auto lda = [&](int ks, u32x4 (&af)[3]) {
+        const char* dys = smem + (k & 1) * RECS * REC;
+        const char* abase = dys + pix_in * REC + ch_a * 2;
+        const char* bbase = dys + P * REC + pix_in * REC + ch_b * 2;
+        auto lda = [&](int ks, u32x4 (&af)[NP]) {
 #pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                const char* pa = abase + ks * TW * WX_REC + q * 128;
-                const u32x2 lo = ds_read_tr(pa), hi = ds_read_tr(pa + 4 * WX_REC);
+            for (int q = 0; q < NP; ++q) {
+                const char* pa = abase + ks * TW * REC + q * 128;
+                const u32x2 lo = ds_read_tr(pa), hi = ds_read_tr(pa + 4 * REC);
                 af[q] = u32x4{lo.x, lo.y, hi.x, hi.y};
             }
         };
-        auto ldb = [&](int ks, int t, u32x4 (&bf)[3]) {
-            const char* pb = bbase + ((ks + t / 3) * HWD + (t % 3)) * WX_REC;
+        auto ldb = [&](int ks, int t, u32x4 (&bf)[NP]) {
+            const char* pb = bbase + ((ks + t / 3) * HWD + (t % 3)) * REC;
 #pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                const u32x2 lo = ds_read_tr(pb + q * 128), hi = ds_read_tr(pb + q * 128 + 4 * WX_REC);
+            for (int q = 0; q < NP; ++q) {
+                const u32x2 lo = ds_read_tr(pb + q * 128), hi = ds_read_tr(pb + q * 128 + 4 * REC);
                 bf[q] = u32x4{lo.x, lo.y, hi.x, hi.y};
             }
         };
         // 2 rows x 9 taps as one sequence: the next tap's fragments (and the next row's
         // dy fragments) are read during the current tap's MFMAs
-        u32x4 afr[2][3], bfr[2][3];
+        u32x4 afr[2][NP], bfr[2][NP];
         lda(0, afr[0]);
         ldb(0, 0, bfr[0]);
         __builtin_amdgcn_sched_barrier(0);
@@ -971,14 +1005,22 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
                 if ((u + 1) % 9 == 0) lda((u + 1) / 9, afr[((u + 1) / 9) & 1]);
                 ldb((u + 1) / 9, (u + 1) % 9, bfr[(u + 1) & 1]);
             }
-            acc[t] = mfma_x6(afr[ks & 1], bfr[u & 1], acc[t]);
-            // next fragments two (four at a row change) per MFMA gap in the first half
-            // of the tap, so they land before the next tap's first MFMAs
+            acc[t] = mfma_xn<NP>(afr[ks & 1], bfr[u & 1], acc[t]);
+            // next fragments (2 reads per piece, twice that at a row change) spread over
+            // the first half of the tap's MFMA gaps, so they land before the next tap
             const bool more = u + 1 < 9 * TH, row = (u + 1) % 9 == 0;
+            if constexpr (NP == 3) {
 #pragma unroll
-            for (int i = 0; i < 6; ++i) {
+                for (int i = 0; i < 6; ++i) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    if (more && i < 3) {
+                        if (row) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+                        else __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                    }
+                }
+            } else {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                if (more && i < 3) {
+                if (more) {
                     if (row) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
                     else __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
                 }
@@ -1020,12 +1062,15 @@ void wgrad_x6w_plan(int ntiles, int Cout, int Cin, int cus, int& nsplit, int& tp
 
 int g_x6_wgrad = 1;  // tuning knob "x6_wgrad": 1 = persistent x6w kernel, 0 = one block per item
 
-void launch_wgrad_x6(const WgradArgs& a, unsigned grid, hipStream_t st) {
-    if (g_x6_wgrad) {
+void launch_wgrad_x6(const WgradArgs& a, unsigned grid, int np, hipStream_t st) {
+    if (g_x6_wgrad || np == 1) {  // (the per-item kernel has no single-piece form)
         const int64_t items = (int64_t)(a.Cout / 64) * (a.Cin / 64) * a.nsplit;
         int64_t g = std::min<int64_t>(cu_count(st), (items + 7) / 8 * 8);
         g = std::max<int64_t>(8, g / 8 * 8);
-        hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW>), dim3((unsigned)g), dim3(512), 0, st, a);
+        if (np == 3)
+            hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW, 3>), dim3((unsigned)g), dim3(512), 0, st, a);
+        else
+            hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW, 1>), dim3((unsigned)g), dim3(512), 0, st, a);
         return;
     }
     hipLaunchKernelGGL((conv3x3_wgrad_x6_kernel<WGX6_TH, WGX6_TW>), dim3(grid), dim3(256), 0, st,
@@ -1038,7 +1083,7 @@ void launch_wgrad_x6(const WgradArgs& a, unsigned grid, hipStream_t st) {
 // the slab of one (column block, chunk, kernel row) is contiguous (18 KB) and
 // equals one LDS weight stage of the kernels below.
 __global__ void pack_x6_kernel(const float* w, __bf16* wpk, int Cout, int Cin, int N, int K,
-                               int mode) {
+                               int mode, int np) {
     const int nchunk = K / 16;
     const int64_t total = (int64_t)N * K * 9;
     const int64_t plane = 3 * 64 * 8;  // one (ky, piece, half) sub-slab: kx x co x 8
@@ -1064,11 +1109,13 @@ __global__ void pack_x6_kernel(const float* w, __bf16* wpk, int Cout, int Cin, i
         const float r1 = v - (float)p0;
         const __bf16 p1 = (__bf16)r1;
         const __bf16 p2 = (__bf16)(r1 - (float)p1);
-        const size_t base = ((size_t)((nb * nchunk + chunk) * 3 + ky) * 3 * 2) * plane;
+        const size_t base = ((size_t)((nb * nchunk + chunk) * 3 + ky) * np * 2) * plane;
         const size_t off = ((size_t)kx * 64 + co) * 8 + j;
         wpk[base + (0 * 2 + h) * plane + off] = p0;
-        wpk[base + (1 * 2 + h) * plane + off] = p1;
-        wpk[base + (2 * 2 + h) * plane + off] = p2;
+        if (np == 3) {
+            wpk[base + (1 * 2 + h) * plane + off] = p1;
+            wpk[base + (2 * 2 + h) * plane + off] = p2;
+        }
     }
 }
 
@@ -1082,7 +1129,7 @@ int fwd_x6_stat_slots(int ntiles, int W) { return use_x6r(W) ? 2 * ntiles : ntil
 // 0 = conv3x3_fwd_x6_kernel everywhere
 int g_x6_probe = 0;  // "x6_probe": timing diagnostics (see ugpg_set_tuning)
 
-void launch_fwd_x6(const ConvFwdArgs& a_in, hipStream_t st) {
+void launch_fwd_x6(const ConvFwdArgs& a_in, int np, hipStream_t st) {
     ConvFwdArgs a = a_in;
     a.probe = g_x6_probe;
     const int64_t items = (int64_t)a.ntiles * (a.Cout / 64);
@@ -1091,22 +1138,32 @@ void launch_fwd_x6(const ConvFwdArgs& a_in, hipStream_t st) {
         // walking a strided share of its XCD's contiguous item range
         int64_t g = std::min<int64_t>(cu_count(st), (items + 7) / 8 * 8);
         g = std::max<int64_t>(8, g / 8 * 8);
-        hipLaunchKernelGGL(conv3x3_fwd_x6r_kernel, dim3((unsigned)g), dim3(512), 0, st, a);
+        if (np == 3)
+            hipLaunchKernelGGL(conv3x3_fwd_x6r_kernel<3>, dim3((unsigned)g), dim3(512), 0, st, a);
+        else
+            hipLaunchKernelGGL(conv3x3_fwd_x6r_kernel<1>, dim3((unsigned)g), dim3(512), 0, st, a);
         return;
     }
     const unsigned grid = (unsigned)items;
-    if (fwd_x6_tile_w(a.W) == 32) {
-        hipLaunchKernelGGL((conv3x3_fwd_x6_kernel<4, 32, false>), dim3(grid), dim3(256), 0, st, a);
+    const bool wide = fwd_x6_tile_w(a.W) == 32;
+    if (np == 3) {
+        if (wide)
+            hipLaunchKernelGGL((conv3x3_fwd_x6_kernel<4, 32, false, 3>), dim3(grid), dim3(256), 0, st, a);
+        else
+            hipLaunchKernelGGL((conv3x3_fwd_x6_kernel<8, 16, true, 3>), dim3(grid), dim3(256), 0, st, a);
     } else {
-        hipLaunchKernelGGL((conv3x3_fwd_x6_kernel<8, 16, true>), dim3(grid), dim3(256), 0, st, a);
+        if (wide)
+            hipLaunchKernelGGL((conv3x3_fwd_x6_kernel<4, 32, false, 1>), dim3(grid), dim3(256), 0, st, a);
+        else
+            hipLaunchKernelGGL((conv3x3_fwd_x6_kernel<8, 16, true, 1>), dim3(grid), dim3(256), 0, st, a);
     }
 }
 
-void launch_pack_x6(const float* w, void* wpk, int Cout, int Cin, int Cin_pad, int mode,
+void launch_pack_x6(const float* w, void* wpk, int Cout, int Cin, int Cin_pad, int mode, int np,
                     hipStream_t st) {
     const int N = mode == 0 ? Cout : Cin_pad, K = mode == 0 ? Cin_pad : Cout;
     hipLaunchKernelGGL(pack_x6_kernel, dim3(stream_grid((int64_t)N * K * 9)), dim3(256), 0, st, w,
-                       static_cast<__bf16*>(wpk), Cout, Cin, N, K, mode);
+                       static_cast<__bf16*>(wpk), Cout, Cin, N, K, mode, np);
 }
 
 }  // namespace ugpg

@@ -80,8 +80,9 @@ NULL_SRC = Src(None, None, None, 0)
 
 
 # ------------------------------------------------------------------ conv
-WFMT_F32, WFMT_X6 = 0, 1
-_MATHS = ("x6", "f32")
+WFMT_F32, WFMT_X6, WFMT_BF16 = 0, 1, 2
+_MATHS = ("x6", "f32", "bf16")
+_MATH_FMT = {"x6": WFMT_X6, "bf16": WFMT_BF16, "f32": WFMT_F32}
 _conv_math = os.environ.get("UGPG_CONV_MATH", "x6")
 if _conv_math not in _MATHS:
     raise ValueError(f"UGPG_CONV_MATH must be one of {_MATHS}, got {_conv_math!r}")
@@ -95,7 +96,9 @@ for _knob in ("x6_pipe", "x6_wgrad", "fwd_cfg"):  # benchmarking knobs from the 
 
 def set_conv_math(math: str) -> None:
     """'x6': split-bf16 MFMA (fp32-accurate, 2.67x the fp32 MFMA rate) wherever the
-    shape allows; 'f32': v_mfma_f32_32x32x2_f32 everywhere."""
+    shape allows; 'f32': v_mfma_f32_32x32x2_f32 everywhere; 'bf16': bf16 arithmetic
+    (operands rounded to bf16, fp32 accumulation and storage -- BASELINE config 3)
+    wherever the shape allows, fp32 MFMA elsewhere (the 3-channel image layer)."""
     global _conv_math
     if math not in _MATHS:
         raise ValueError(f"conv math must be one of {_MATHS}")
@@ -108,7 +111,8 @@ def conv_math() -> str:
 
 def conv_weight_format(n: int, k: int) -> int:
     """Pack format for a conv GEMM with N output columns and K input channels."""
-    return WFMT_X6 if _conv_math == "x6" and n % 64 == 0 and k % 16 == 0 else WFMT_F32
+    fmt = _MATH_FMT[_conv_math]
+    return fmt if n % 64 == 0 and k % 16 == 0 else WFMT_F32
 
 
 def pack_conv3x3(w, cin_pad: int, mode: int) -> torch.Tensor:
@@ -193,7 +197,7 @@ def conv3x3_wgrad(srcs, dy, dw, db, cin_real, accumulate=0, flops=None):
     d.src[1] = srcs[1].src() if len(srcs) > 1 else NULL_SRC
     d.dy, d.Cout = ptr(dy), dy.shape[-1]
     d.dw, d.Cin_real, d.db, d.accumulate = ptr(dw), cin_real, ptr(db), int(accumulate)
-    d.math = WFMT_X6 if _conv_math == "x6" else WFMT_F32
+    d.math = _MATH_FMT[_conv_math]
     nbytes = lib.ugpg_conv3x3_wgrad_workspace(C.byref(d))
     if nbytes == 0:
         check(-1, "conv3x3_wgrad_workspace")
