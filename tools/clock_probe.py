@@ -1,0 +1,58 @@
+"""In-kernel clock of the x6r forward (diagnostic builds with -D X6R_CLOCK=1 only):
+runs one layer back-to-back for >= 2 s on random data, then reads the median over
+workgroups of core cycles / 100 MHz ticks around the main loop (MI355X_MICROARCH.md
+'DVFS give-back' item 6).
+
+    UGPG_LIB=exp/lib_clock.so python tools/clock_probe.py [--layers inc.3,down2.3]
+"""
+import argparse
+import ctypes
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path[:0] = [str(ROOT), str(ROOT / "ug-pg-unet_amd"), str(ROOT / "tools")]
+
+import torch  # noqa: E402
+
+from conv_bench import B, LAYERS  # noqa: E402
+from ugpg import ops  # noqa: E402
+from ugpg._C import lib  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--layers", default="inc.3,down1.3,down2.3,up4.0")
+    ap.add_argument("--seconds", type=float, default=2.0)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    fn = lib.ugpg_debug_clock
+    fn.argtypes = [ctypes.POINTER(ctypes.c_double)]
+    for name, H, C0, C1, Cout in LAYERS:
+        if name not in a.layers.split(","):
+            continue
+        srcs = [ops.Act(torch.randn(B, H, H, C0, device=dev),
+                        torch.rand(C0, device=dev) + 0.5, torch.randn(C0, device=dev) * 0.1)]
+        if C1:
+            srcs.append(ops.Act(torch.randn(B, H, H, C1, device=dev)))
+        w = torch.randn(Cout, C0 + C1, 3, 3, device=dev) * 0.05
+        out = torch.empty(B, H, H, Cout, device=dev)
+        wpk = ops.pack_conv3x3(w, C0 + C1, 0)
+        st = torch.empty(3 * Cout * ops.conv_ntiles(B, H, H, C0 + C1, Cout, wpk), device=dev)
+        flops = 2.0 * B * H * H * Cout * 9 * (C0 + C1)
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < a.seconds:
+            for _ in range(20):
+                ops.conv3x3_fwd(srcs, wpk, torch.zeros(Cout, device=dev), Cout, [out], stats=st)
+            torch.cuda.synchronize()
+            n += 20
+        dt = (time.perf_counter() - t0) / n
+        mhz = ctypes.c_double(0)
+        nwg = fn(ctypes.byref(mhz))
+        print(f"{name}: {dt*1e3:.3f} ms/launch {flops/dt/1e12:.0f} TF  clock {mhz.value:.0f} MHz "
+              f"(median of {nwg} workgroups)", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -312,12 +312,17 @@ __device__ __forceinline__ void lds_barrier() {
 
 // per-wave epilogue: bias, (dual-destination, accumulate-capable) store, and the
 // wave's BatchNorm partial (count, sum, M2) over its MT*32 pixels x 32 channels into
-// slot 2*tile + wm (stat slots = 2 * ntiles)
+// slot 2*tile + wm (stat slots = 2 * ntiles).  Each 32-pixel MFMA tile is one image
+// row (TW == 32): lane (h, c) holds pixels (r&3) + 8(r>>2) + 4h of row wm*MT + mt,
+// channel c, so addresses are one row base + a per-lane offset + a constant per r;
+// the accumulate and bounds decisions are uniform per item.
 template <int TH, int TW, int MT>
 __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&acc)[MT], int tile,
                                                  int b, int ty0, int tx0, int n0, int wm, int wn) {
-    const int lane = threadIdx.x & 63;
+    static_assert(TW == 32, "one image row per 32-pixel MFMA tile");
+    const int lane = threadIdx.x & 63, h = lane >> 5;
     const int vh = min(TH, a.H - ty0), vw = min(TW, a.W - tx0);
+    const bool fullw = vw == TW;
     float* out;
     int ostride, ocol0, oacc;
     if (n0 < a.split) {
@@ -333,21 +338,31 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
     }
     const int nl = wn * 32 + (lane & 31);
     const float bv = a.bias ? a.bias[n0 + nl] : 0.f;
+    const int lane_off = 4 * h * ostride + ocol0 + nl;
     float psum = 0.f;
+    auto store_rows = [&](auto accumulate) {
+        constexpr bool ACC = decltype(accumulate)::value;
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
+        for (int mt = 0; mt < MT; ++mt) {
+            const int py = wm * MT + mt;
+            if (py >= vh) break;  // uniform
+            float* rowp = out + (size_t)((b * a.H + ty0 + py) * a.W + tx0) * ostride + lane_off;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int m = wm * MT * 32 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-            const int py = m / TW, px = m % TW;
-            const float v = acc[mt][r] + bv;
-            acc[mt][r] = v;
-            if (py < vh && px < vw) {
-                const size_t o = ((size_t)(b * a.H + ty0 + py) * a.W + tx0 + px) * ostride + ocol0 + nl;
-                out[o] = oacc ? out[o] + v : v;
-                psum += v;
+            for (int r = 0; r < 16; ++r) {
+                const int pxc = (r & 3) + 8 * (r >> 2);  // + 4h in lane_off
+                const float v = acc[mt][r] + bv;
+                acc[mt][r] = v;
+                if (fullw || pxc + 4 * h < vw) {
+                    float* p = rowp + pxc * ostride;
+                    if constexpr (ACC) *p += v;
+                    else *p = v;
+                    psum += v;
+                }
             }
         }
+    };
+    if (oacc) store_rows(std::integral_constant<bool, true>{});
+    else store_rows(std::integral_constant<bool, false>{});
     if (a.stats == nullptr) return;
     constexpr int WROWS = MT * 32 / TW;  // image rows of one wave's pixels
     const int rows = min(max(vh - wm * WROWS, 0), WROWS);
@@ -356,15 +371,17 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
     const float mu = cnt > 0.f ? s / cnt : 0.f;
     float q = 0.f;
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
+    for (int mt = 0; mt < MT; ++mt) {
+        if (wm * MT + mt >= vh) break;  // uniform
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const int m = wm * MT * 32 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-            if (m / TW < vh && m % TW < vw) {
+            const int px = (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (fullw || px < vw) {
                 const float d = acc[mt][r] - mu;
                 q = fmaf(d, d, q);
             }
         }
+    }
     q += __shfl_xor(q, 32, 64);
     if (lane < 32) {
         const size_t n = n0 + nl, S = 2 * (size_t)a.ntiles, slot = 2 * (size_t)tile + wm;
@@ -374,6 +391,21 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
     }
 }
 
+#ifdef X6R_CLOCK
+// diagnostic build only: per-workgroup (core cycles, 100 MHz ticks) of the main loop
+__device__ unsigned long long g_clk[8192];
+extern "C" int ugpg_debug_clock(double* mhz) {
+    static unsigned long long h[8192];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_clk), sizeof(h)) != hipSuccess) return -1;
+    double r[4096];
+    int n = 0;
+    for (int i = 0; i < 4096; ++i)
+        if (h[2 * i + 1] > 0) r[n++] = 100.0 * (double)h[2 * i] / (double)h[2 * i + 1];
+    std::sort(r, r + n);
+    *mhz = n ? r[n / 2] : 0.0;
+    return n;
+}
+#endif
 template <int NP>
 __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) {
     constexpr int TH = 8, TW = 32, BN = 64, BKC = 16, MT = 4;
@@ -563,6 +595,10 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
     // the phase's barrier: the barriers only order the loaders' overwrites and expose
     // no LDS latency inside a step.
     lds_barrier();  // step 0 staged
+#ifdef X6R_CLOCK
+    const unsigned long long clk_t0 = __builtin_amdgcn_s_memtime(),
+                             clk_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
     int cc = 0, item = item0;
     Pos cp = pos_of(item0);
     for (int k = 0; k < total; ++k) {
@@ -603,6 +639,12 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
                 for (int r = 0; r < 16; ++r) acc[mt][r] = 0.f;
         }
     }
+#ifdef X6R_CLOCK
+    if (tid == 0 && blockIdx.x < 4096) {
+        g_clk[2 * blockIdx.x] = __builtin_amdgcn_s_memtime() - clk_t0;
+        g_clk[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - clk_r0;
+    }
+#endif
 }
 // ---------------------------------------------------------------------------
 // Split-bf16 weight gradient: dW[co][ci][t] = sum_p dy[p][co] * act(x)[p+t][ci].
