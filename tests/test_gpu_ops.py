@@ -67,11 +67,12 @@ BIG = {5, 6, 7}
 
 
 # x6 kernel forms (tuning knobs "x6_pipe" for forward/dgrad, "x6_wgrad"): 1 = persistent
-# warp-specialized (default), 0 = one workgroup per tile/item
-X6_FORMS = {"x6": 1, "x6s": 0}
+# warp-specialized (default), 0 = one workgroup per tile/item, 2 = persistent with
+# 16x16x32 MFMA tiles (forward/dgrad)
+X6_FORMS = {"x6": 1, "x6s": 0, "x6q": 2}
 
 
-@pytest.fixture(params=["x6", "x6s", "f32", "bf16"])
+@pytest.fixture(params=["x6", "x6s", "x6q", "f32", "bf16"])
 def math(request):
     """Every conv arithmetic form: split-bf16 (default, every kernel form), fp32
     MFMA, and bf16 (BASELINE config 3: operands rounded to bf16, fp32 accumulation)."""

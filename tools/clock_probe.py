@@ -4,6 +4,8 @@ workgroups of core cycles / 100 MHz ticks around the main loop (MI355X_MICROARCH
 'DVFS give-back' item 6).
 
     UGPG_LIB=exp/lib_clock.so python tools/clock_probe.py [--layers inc.3,down2.3]
+    UGPG_LIB=exp/lib_stamp.so python tools/clock_probe.py --stamps   (-D X6R_STAMP=1 build:
+        loader waves' share of the loop spent waiting for global loads / at barriers)
 """
 import argparse
 import ctypes
@@ -25,9 +27,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--layers", default="inc.3,down1.3,down2.3,up4.0")
     ap.add_argument("--seconds", type=float, default=2.0)
+    ap.add_argument("--stamps", action="store_true")
+    ap.add_argument("--pipes", default="1")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
-    fn = lib.ugpg_debug_clock
+    fn = lib.ugpg_debug_stamps if a.stamps else lib.ugpg_debug_clock
     fn.argtypes = [ctypes.POINTER(ctypes.c_double)]
     for name, H, C0, C1, Cout in LAYERS:
         if name not in a.layers.split(","):
@@ -41,17 +45,23 @@ def main():
         wpk = ops.pack_conv3x3(w, C0 + C1, 0)
         st = torch.empty(3 * Cout * ops.conv_ntiles(B, H, H, C0 + C1, Cout, wpk), device=dev)
         flops = 2.0 * B * H * H * Cout * 9 * (C0 + C1)
-        n, t0 = 0, time.perf_counter()
-        while time.perf_counter() - t0 < a.seconds:
-            for _ in range(20):
-                ops.conv3x3_fwd(srcs, wpk, torch.zeros(Cout, device=dev), Cout, [out], stats=st)
-            torch.cuda.synchronize()
-            n += 20
-        dt = (time.perf_counter() - t0) / n
-        mhz = ctypes.c_double(0)
-        nwg = fn(ctypes.byref(mhz))
-        print(f"{name}: {dt*1e3:.3f} ms/launch {flops/dt/1e12:.0f} TF  clock {mhz.value:.0f} MHz "
-              f"(median of {nwg} workgroups)", flush=True)
+        for pipe in a.pipes.split(","):
+            lib.ugpg_set_tuning(b"x6_pipe", int(pipe))
+            n, t0 = 0, time.perf_counter()
+            while time.perf_counter() - t0 < a.seconds:
+                for _ in range(20):
+                    ops.conv3x3_fwd(srcs, wpk, torch.zeros(Cout, device=dev), Cout, [out], stats=st)
+                torch.cuda.synchronize()
+                n += 20
+            dt = (time.perf_counter() - t0) / n
+            v = (ctypes.c_double * 6)()
+            nwg = fn(v)
+            what = (("loader vm_wait/barrier per phase " +
+                     " ".join(f"p{q}:{v[q]:.1%}/{v[3 + q]:.1%}" for q in range(3))) if a.stamps
+                    else f"clock {v[0]:.0f} MHz")
+            print(f"{name} pipe {pipe}: {dt*1e3:.3f} ms/launch {flops/dt/1e12:.0f} TF  {what} "
+                  f"(median of {nwg} workgroups)", flush=True)
+        lib.ugpg_set_tuning(b"x6_pipe", 1)
 
 
 if __name__ == "__main__":

@@ -2,6 +2,7 @@
 process, interleaved rounds (cdna_hip_programming.md §5.4 rule 24).
 
     python tools/conv_bench.py [--rounds 3] [--cfgs -1,0,1,2] [--wgrad]
+    python tools/conv_bench.py --libs exp/a.so,exp/b.so ...   (A/B of builds, one process)
 """
 import argparse
 import sys
@@ -12,8 +13,17 @@ sys.path[:0] = [str(ROOT), str(ROOT / "ug-pg-unet_amd")]
 
 import torch  # noqa: E402
 
-from ugpg import ops  # noqa: E402
+from ugpg import _C, ops  # noqa: E402
 from ugpg._C import lib  # noqa: E402
+
+
+def load_lib(path):
+    import ctypes
+    L = ctypes.CDLL(str(Path(path).resolve()))
+    for name, (res, args) in _C.SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype, fn.argtypes = res, args
+    return L
 
 B = 16
 # name, H, C0, C1, Cout  (forward convs of PGUNet4; C1 = upsampled half of Up's concat)
@@ -47,7 +57,9 @@ def main():
     ap.add_argument("--pipes", default="1", help="x6 forward forms to time (x6_pipe knob)")
     ap.add_argument("--wgrad", action="store_true")
     ap.add_argument("--layers", default="", help="comma-separated layer names (default: all)")
+    ap.add_argument("--libs", default="", help="comma-separated libugpg builds to compare")
     a = ap.parse_args()
+    libs = [(Path(p).stem, load_lib(p)) for p in a.libs.split(",")] if a.libs else [("", None)]
     dev = torch.device("cuda:0")
     cfgs = [int(c) for c in a.cfgs.split(",")]
     rows = {}
@@ -102,6 +114,13 @@ def main():
                     ops.set_conv_math(m)
                     ops.conv3x3_wgrad(srcs, dy, dw, None, real_cin)
                 fns[f"wgrad_{m}"] = wg
+        if libs[0][1] is not None:
+            def with_lib(f, L):
+                def h():
+                    lib._lib = L
+                    f()
+                return h
+            fns = {f"{k}@{tag}": with_lib(f, L) for tag, L in libs for k, f in fns.items()}
         res = {k: [] for k in fns}
         for _ in range(a.rounds):
             for k, f in fns.items():

@@ -91,6 +91,23 @@ __device__ __forceinline__ f32x16 mfma16(u32x4 a, u32x4 b, f32x16 c) {
                                                    __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
 }
 
+__device__ __forceinline__ f32x4 mfma16x16(u32x4 a, u32x4 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                   __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+// sum over the 16 lanes of a DPP row, result in every lane of the row
+__device__ __forceinline__ float row16_sum(float v) {
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
+                                                               0xB1, 0xF, 0xF, false));  // [1,0,3,2]
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
+                                                               0x4E, 0xF, 0xF, false));  // [2,3,0,1]
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
+                                                               0x141, 0xF, 0xF, false));  // half mirror
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
+                                                               0x140, 0xF, 0xF, false));  // mirror
+    return v;
+}
+
 // acc += a*b from the pieces: NP = 3 -> fp32 accuracy (the six products of order
 // <= 2, smallest terms first); NP = 1 -> one bf16 product (the "bf16" arithmetic of
 // BASELINE config 3: operands rounded to bf16, fp32 accumulation)
@@ -291,6 +308,19 @@ __device__ __forceinline__ f32x4 gld16(const void* p) {
     asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p));
     return r;
 }
+// LDS-DMA: 16 bytes per lane from g (per-lane address) to lds_wave + 16*lane (lds_wave
+// wave-uniform), counted by vmcnt like a load; no VGPR destination
+__device__ __forceinline__ void glds16(const void* g, void* lds_wave) {
+    const unsigned m0 =
+        __builtin_amdgcn_readfirstlane((unsigned)reinterpret_cast<uintptr_t>(lds_wave));
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(g), "s"(m0)
+        : "memory");
+}
 template <int N>
 __device__ __forceinline__ void vm_wait() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -391,9 +421,138 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
     }
 }
 
+// Epilogue of the 16x16x32 form: acc[mt][nt] is D[oc][px] of m-tile mt (16 pixels:
+// image row wm*4 + mt/2, columns (mt&1)*16 + 0..15) and n-tile nt (16 channels); lane
+// (g, l) holds channels 4g..4g+3 of pixel l -> one 16-byte store per tile.  BatchNorm
+// partials as x6_epilogue_wave (slot 2*tile + wm), reduced over the pixel lanes of
+// each DPP row.
+template <int TH, int TW>
+__device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a, f32x4 (&acc)[8][2], int tile,
+                                                  int b, int ty0, int tx0, int n0, int wm, int wn) {
+    static_assert(TW == 32 && TH == 8, "8 x 32 tile, 4 rows per wave");
+    const int lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
+    const int vh = min(TH, a.H - ty0), vw = min(TW, a.W - tx0);
+    float* out;
+    int ostride, ocol0, oacc;
+    if (n0 < a.split) {
+        out = a.out0;
+        ostride = a.split;
+        ocol0 = n0;
+        oacc = a.acc0;
+    } else {
+        out = a.out1;
+        ostride = a.Cout - a.split;
+        ocol0 = n0 - a.split;
+        oacc = a.acc1;
+    }
+    const int c0 = wn * 32 + 4 * g;  // + 16 nt
+    f32x4 bv[2];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+#ifdef X6Q_NOBIAS
+        bv[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#else
+        bv[nt] = a.bias ? *reinterpret_cast<const f32x4*>(a.bias + n0 + c0 + 16 * nt)
+                        : f32x4{0.f, 0.f, 0.f, 0.f};
+#endif
+    }
+    f32x4 psum[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    auto store_tiles = [&](auto accumulate) {
+        constexpr bool ACC = decltype(accumulate)::value;
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt) {
+            const int py = wm * 4 + (mt >> 1), px = (mt & 1) * 16 + l16;
+            if (py >= vh) break;  // uniform
+            const bool ok = px < vw;
+            float* p = out + (size_t)((b * a.H + ty0 + py) * a.W + tx0 + px) * ostride + ocol0 + c0;
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) {
+                const f32x4 v = acc[mt][nt] + bv[nt];
+                acc[mt][nt] = v;
+                if (ok) {
+                    f32x4* q = reinterpret_cast<f32x4*>(p + 16 * nt);
+                    if constexpr (ACC) *q = *q + v;
+                    else *q = v;
+                    psum[nt] += v;
+                }
+            }
+        }
+    };
+    if (oacc) store_tiles(std::integral_constant<bool, true>{});
+    else store_tiles(std::integral_constant<bool, false>{});
+    if (a.stats == nullptr) return;
+#ifdef X6Q_NOSTATS
+    return;
+#endif
+    const int rows = min(max(vh - wm * 4, 0), 4);
+    const float cnt = (float)(rows * vw);
+    f32x4 mu[2], q[2];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            psum[nt][i] = row16_sum(psum[nt][i]);
+            mu[nt][i] = cnt > 0.f ? psum[nt][i] / cnt : 0.f;
+        }
+        q[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+        if (wm * 4 + (mt >> 1) >= vh) break;  // uniform
+        if ((mt & 1) * 16 + l16 < vw) {
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) {
+                const f32x4 d = acc[mt][nt] - mu[nt];
+                q[nt] += d * d;
+            }
+        }
+    }
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) q[nt][i] = row16_sum(q[nt][i]);
+    // lane l < 8 of each row writes channel 16*(l>>2) + 4g + (l&3)
+    if (l16 < 8) {
+        const int nt = l16 >> 2, i = l16 & 3;
+        float sv = 0.f, qv = 0.f;
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+            if (t == l16) {
+                sv = psum[t >> 2][t & 3];
+                qv = q[t >> 2][t & 3];
+            }
+        const size_t n = n0 + c0 + 16 * nt + i, S = 2 * (size_t)a.ntiles, slot = 2 * (size_t)tile + wm;
+        a.stats[(0 * (size_t)a.Cout + n) * S + slot] = cnt;
+        a.stats[(1 * (size_t)a.Cout + n) * S + slot] = sv;
+        a.stats[(2 * (size_t)a.Cout + n) * S + slot] = qv;
+    }
+}
+
+#if defined(X6R_CLOCK) || defined(X6R_STAMP)
+__device__ unsigned long long g_clk[8192];
+#endif
+#ifdef X6R_STAMP
+// diagnostic build only: median over workgroups of the loader waves' fraction of the
+// main loop spent in vm_wait (out[0..2], per phase) and at barriers (out[3..5])
+extern "C" int ugpg_debug_stamps(double* out) {
+    static unsigned long long h[8192];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_clk), sizeof(h)) != hipSuccess) return -1;
+    static double f[6][1024];
+    int n = 0;
+    for (int i = 0; i < 1024; ++i)
+        if (h[8 * i] > 0) {
+            for (int q = 0; q < 6; ++q) f[q][n] = (double)h[8 * i + 1 + q] / h[8 * i];
+            ++n;
+        }
+    for (int q = 0; q < 6; ++q) {
+        std::sort(f[q], f[q] + n);
+        out[q] = n ? f[q][n / 2] : 0.0;
+    }
+    return n;
+}
+#endif
 #ifdef X6R_CLOCK
 // diagnostic build only: per-workgroup (core cycles, 100 MHz ticks) of the main loop
-__device__ unsigned long long g_clk[8192];
 extern "C" int ugpg_debug_clock(double* mhz) {
     static unsigned long long h[8192];
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_clk), sizeof(h)) != hipSuccess) return -1;
@@ -406,12 +565,15 @@ extern "C" int ugpg_debug_clock(double* mhz) {
     return n;
 }
 #endif
-template <int NP>
+template <int NP, bool M16>
 __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) {
+    static_assert(!M16 || NP == 3, "the 16x16x32 form pairs the split-bf16 products");
     constexpr int TH = 8, TW = 32, BN = 64, BKC = 16, MT = 4;
     constexpr int HWD = TW + 2, HS = HWD;
     constexpr int NHALO = (TH + 2) * HWD;                   // 340 halo pixels
-    constexpr int NHP = NHALO + 1 + (11 - NHALO % 8) % 8;   // 348: spare slot NHALO, = 4 (mod 8)
+    // spare slot NHALO; plane pitch 348 = 4 (mod 8) for the 32x32 fragment pattern, 352
+    // = 0 (mod 16) for the 16x16 one (ds_read_b128 lane groups, MI355X_MICROARCH.md §LDS)
+    constexpr int NHP = M16 ? (NHALO + 1 + 15) / 16 * 16 : NHALO + 1 + (11 - NHALO % 8) % 8;
     constexpr int A_ITEMS = NHALO * 2;                      // (pixel, channel half)
     constexpr int A_PER = (A_ITEMS + 255) / 256;            // 3
     constexpr int A_VECS = 2 * NP * NHP;
@@ -455,15 +617,16 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
 
     if (loader) {
         // ------------------------------------------------------------ loader waves
-        // per step k:  phase 0: write halo(k+1) and weight row 0 of k+1, load row 1 of
-        // k+1 and halo(k+2);  phase 1: write row 1, load row 2;  phase 2: write row 2,
-        // load row 0 of k+2.  Row r of step j goes to ring slot (3j + r) % 4.
+        // Weight rows form one stream j = 3*step + ky; row j goes to ring slot j % 4 and
+        // to register set j % 3.  Phase ph of step k writes row 3(k+1)+ph (loaded two
+        // phases earlier) and loads row 3(k+1)+ph+2; phase 0 also writes halo(k+1) and
+        // loads halo(k+2) (three phases of flight).  Each wait leaves exactly the loads
+        // issued in the previous phase outstanding.
         const int lt = tid - 256;
         f32x4 ra[A_PER][2];
         unsigned avalid = 0;
         Act4 r0, r1;
         float lo = 0.f;
-        u32x4 rb[R_PER];
         auto load_halo = [&](int k) {
             k = min(k, last);
             const int c = k % nchunk;
@@ -517,62 +680,192 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
                 for (int q = 0; q < NP; ++q) As[(q * 2 + hh) * NHP + hl] = pc[q];
             }
         };
-        auto load_row = [&](int k, int ky) {
-            k = min(k, last);
+        // weight row j -> ring slot j % 4 by LDS-DMA: 16 B per lane, each wave-instruction
+        // one contiguous KiB of the slot; rounds of 256 vectors, the last round's
+        // missing waves repeat a present wave's copy (identical bytes, same place)
+        constexpr int R_LASTW = (R_VEC - (R_PER - 1) * 256) / 64;  // waves with work in the last round
+        static_assert(R_VEC % 64 == 0, "whole wave-instructions");
+        const int lw = lt >> 6;
+        auto dma_row = [&](int j) {
+            const int k = min(j / 3, last), ky = j % 3;
             const int c = k % nchunk;
             const int nb = (item0 + (k / nchunk) * nslots) % NB;
             const u32x4* ws =
                 static_cast<const u32x4*>(a.wpk) + (((size_t)nb * nchunk + c) * 3 + ky) * R_VEC;
-#pragma unroll
-            for (int v = 0; v < R_PER; ++v)
-                rb[v] = __builtin_bit_cast(u32x4, gld16(ws + min(lt + v * 256, R_VEC - 1)));
-        };
-        auto store_row = [&](int k, int ky) {
-            u32x4* Bs = Bring + ((3 * k + ky) % NSLOT) * R_STR;
+            u32x4* Bs = Bring + (j % NSLOT) * R_STR;
 #pragma unroll
             for (int v = 0; v < R_PER; ++v) {
-                const int idx = lt + v * 256;
-                *(idx < R_VEC ? Bs + idx : dummy) = rb[v];
+                const int base = v * 256 + (v + 1 < R_PER ? lw : lw % R_LASTW) * 64;
+                glds16(ws + base + lane, Bs + base);
             }
         };
-        // prologue: step 0 complete in LDS (halo buffer 0, rows in slots 0-2)
+        // prologue: step 0 in LDS (halo buffer 0, rows 0-2), halo(1) in registers
         load_halo(0);
         vm_wait<0>();
         store_halo(0);
-#pragma unroll 1
-        for (int ky = 0; ky < 3; ++ky) {
-            load_row(0, ky);
-            vm_wait<0>();
-            store_row(0, ky);
-        }
-        load_row(1, 0);
+        dma_row(0);
+        dma_row(1);
+        dma_row(2);
         load_halo(1);
+        vm_wait<0>();
         lds_barrier();
+        // Phase ph of step k DMAs row j = 3(k+1)+ph into the slot of row j-4 (read in
+        // the phase before, whose MFMAs consumed it before that phase's barrier) and
+        // retires the previous phase's row before its own closing barrier, so every row
+        // has about two phases of flight and is read one phase after that barrier.
+        // Phase 0 also writes halo(k+1) (loaded a step earlier) and loads halo(k+2).
+        // vmcnt counts the loader's loads and DMAs together, in issue order.
+        constexpr int R = R_PER, H = HALO_LOADS;
+#ifdef X6R_STAMP
+        // diagnostic build: loader cycles spent waiting for global loads / at barriers
+        unsigned long long st_vm[3] = {0, 0, 0}, st_bar[3] = {0, 0, 0};
+        const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();
+#define ST_WAIT(acc, stmt)                                          \
+    {                                                               \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+        stmt;                                                       \
+        acc += __builtin_amdgcn_s_memtime() - t_;                   \
+    }
+#else
+#define ST_WAIT(acc, stmt) stmt
+#endif
         for (int k = 0; k < total; ++k) {
+            const int j = 3 * (k + 1);
             // phase 0
-            vm_wait<0>();
+            dma_row(j);
+            ST_WAIT(st_vm[0], vm_wait<3 * R>());  // halo(k+1) (issued before rows j-2, j-1, j)
             store_halo(k + 1);
-            store_row(k + 1, 0);
-            load_row(k + 1, 1);
             load_halo(k + 2);
-            lds_barrier();
+            ST_WAIT(st_vm[0], vm_wait<R + H>());  // row j-1
+            ST_WAIT(st_bar[0], lds_barrier());
             // phase 1
-            vm_wait<HALO_LOADS>();
-            store_row(k + 1, 1);
-            load_row(k + 1, 2);
-            lds_barrier();
+            dma_row(j + 1);
+            ST_WAIT(st_vm[1], vm_wait<H + R>());  // row j
+            ST_WAIT(st_bar[1], lds_barrier());
             // phase 2
-            vm_wait<0>();
-            store_row(k + 1, 2);
-            load_row(k + 2, 0);
-            lds_barrier();
+            dma_row(j + 2);
+            ST_WAIT(st_vm[2], vm_wait<R>());  // row j+1 (and halo(k+2))
+            ST_WAIT(st_bar[2], lds_barrier());
         }
+#undef ST_WAIT
+#ifdef X6R_STAMP
+        if (tid == 256 && blockIdx.x < 1024) {
+            g_clk[8 * blockIdx.x] = __builtin_amdgcn_s_memtime() - st_t0;
+            for (int q = 0; q < 3; ++q) {
+                g_clk[8 * blockIdx.x + 1 + q] = st_vm[q];
+                g_clk[8 * blockIdx.x + 4 + q] = st_bar[q];
+            }
+        }
+#endif
         vm_wait<0>();  // no load outlives the workgroup
         return;
     }
 
     // ---------------------------------------------------------------- compute waves
     const int wm = wave >> 1, wn = wave & 1;
+    if constexpr (M16) {
+        // 16x16x32 form: D[oc][px] = W x A with the split-bf16 products paired along k:
+        // k-groups (lanes 16g..16g+15) 0,1 = channels 0-7, 8-15 of one piece, 2,3 of
+        // another, so  W00.A01 = b0a0 + b0a1,  W11.A01 = b1a0 + b1a1,  W20.A02 = b2a0 + b0a2
+        // (all six products, three MFMAs per 16x16 tile and tap).  A "unit" is a pair of
+        // m-tiles (one image row, 32 pixels) of one tap: 4 A fragments, 12 MFMAs on four
+        // accumulators; the next unit's A fragments and, spread over the tap, the next
+        // tap's six W fragments are read while it runs.
+        const int g = lane >> 4, l16 = lane & 15;
+        const int a01 = g * NHP + wm * 4 * HS + l16;
+        const int a02 = ((g >> 1) * 4 + (g & 1)) * NHP + wm * 4 * HS + l16;
+        const int bo = (g & 1) * 3 * BN + wn * 32 + l16;
+        const int wq[3] = {bo + 4 * 3 * BN * (g < 2 ? 1 : 0), bo + 2 * 3 * BN, bo};  // W20, W11, W00
+        f32x4 acc[8][2];
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#ifndef X6Q_DEPTH
+#define X6Q_DEPTH 1
+#endif
+        constexpr int DA = X6Q_DEPTH;  // A fragments are read DA units ahead (36 % (DA+1) == 0)
+        static_assert(36 % (DA + 1) == 0, "unit ring must divide a step");
+        u32x4 fa[DA + 1][2][2];  // [unit % (DA+1)][m-tile of the pair][A02, A01]
+        u32x4 fw[3][3][2];     // [tap % 3 (9 taps per step)][W20, W11, W00][nt]
+        auto lda = [&](const u32x4* As, int t, int r, u32x4 (&f)[2][2]) {
+            const int ky = t / 3, kx = t % 3, o = (r + ky) * HS + kx;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                f[h][0] = As[a02 + o + 16 * h];
+                f[h][1] = As[a01 + o + 16 * h];
+            }
+        };
+        auto ldw = [&](const u32x4* Bs, int kx, int e, u32x4 (&f)[3][2]) {
+            f[e >> 1][e & 1] = Bs[wq[e >> 1] + kx * BN + 16 * (e & 1)];
+        };
+        lds_barrier();  // step 0 staged
+#ifdef X6R_CLOCK
+        const unsigned long long clk_t0 = __builtin_amdgcn_s_memtime(),
+                                 clk_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
+        int cc = 0, item = item0;
+        Pos cp = pos_of(item0);
+#pragma unroll
+        for (int uu = 0; uu < DA; ++uu) lda(smem, uu / 4, uu % 4, fa[uu]);
+#pragma unroll
+        for (int e = 0; e < 6; ++e) ldw(Bring, 0, e, fw[0]);
+        for (int k = 0; k < total; ++k) {
+            const u32x4* Ac = smem + (k & 1) * A_VECS;
+            const u32x4* An = smem + ((k + 1) & 1) * A_VECS;
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                const int tn = t + 1 < 9 ? t + 1 : 0;  // next tap (of this step or the next)
+                const u32x4* Bn = Bring + ((3 * k + (t + 1) / 3) % NSLOT) * R_STR;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int u = t * 4 + r;
+                    // next unit's A fragments, then (units 0-2 of the tap) next tap's W
+                    const int un = u + DA;
+                    if (un < 36) lda(Ac, un / 4, un % 4, fa[un % (DA + 1)]);
+                    else lda(An, (un - 36) / 4, (un - 36) % 4, fa[un % (DA + 1)]);
+                    if (r < 3) {
+                        ldw(Bn, tn % 3, 2 * r, fw[(t + 1) % 3]);
+                        ldw(Bn, tn % 3, 2 * r + 1, fw[(t + 1) % 3]);
+                    }
+                    const u32x4(&A)[2][2] = fa[u % (DA + 1)];
+                    const u32x4(&W)[3][2] = fw[t % 3];
+#pragma unroll
+                    for (int e = 0; e < 3; ++e)
+#pragma unroll
+                        for (int h = 0; h < 2; ++h)
+#pragma unroll
+                            for (int nt = 0; nt < 2; ++nt)
+                                acc[2 * r + h][nt] =
+                                    mfma16x16(W[e][nt], A[h][e == 0 ? 0 : 1], acc[2 * r + h][nt]);
+#pragma unroll
+                    for (int i = 0; i < 12; ++i) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+                        if (i < (r < 3 ? 6 : 4)) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                if (t % 3 == 2) read_barrier();
+            }
+            if (++cc == nchunk) {
+                x6q_epilogue_wave<TH, TW>(a, acc, cp.tile, cp.b, cp.ty0, cp.tx0, cp.nb * BN, wm, wn);
+                cc = 0;
+                item += nslots;
+                if (item < iend) cp = pos_of(item);
+#pragma unroll
+                for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+                    for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+#ifdef X6R_CLOCK
+        if (tid == 0 && blockIdx.x < 4096) {
+            g_clk[2 * blockIdx.x] = __builtin_amdgcn_s_memtime() - clk_t0;
+            g_clk[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - clk_r0;
+        }
+#endif
+        return;
+    } else {
     f32x16 acc[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
@@ -645,6 +938,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
         g_clk[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - clk_r0;
     }
 #endif
+    }
 }
 // ---------------------------------------------------------------------------
 // Split-bf16 weight gradient: dW[co][ci][t] = sum_p dy[p][co] * act(x)[p+t][ci].
@@ -1180,10 +1474,15 @@ void launch_fwd_x6(const ConvFwdArgs& a_in, int np, hipStream_t st) {
         // walking a strided share of its XCD's contiguous item range
         int64_t g = std::min<int64_t>(cu_count(st), (items + 7) / 8 * 8);
         g = std::max<int64_t>(8, g / 8 * 8);
-        if (np == 3)
-            hipLaunchKernelGGL(conv3x3_fwd_x6r_kernel<3>, dim3((unsigned)g), dim3(512), 0, st, a);
+        if (np == 3 && g_x6_pipe == 2)
+            hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<3, true>), dim3((unsigned)g), dim3(512), 0,
+                               st, a);
+        else if (np == 3)
+            hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<3, false>), dim3((unsigned)g), dim3(512), 0,
+                               st, a);
         else
-            hipLaunchKernelGGL(conv3x3_fwd_x6r_kernel<1>, dim3((unsigned)g), dim3(512), 0, st, a);
+            hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false>), dim3((unsigned)g), dim3(512), 0,
+                               st, a);
         return;
     }
     const unsigned grid = (unsigned)items;
