@@ -37,8 +37,11 @@ const char* ugpg_last_error(void);
 /* Tuning knobs for benchmarking (process-global; not for production use):
  *   "fwd_cfg": force the 3x3 conv tile config (0 = 16x16x64, 1 = 8x16x128,
  *              2 = 8x8x64) where it is legal for the shape; -1 = heuristic.
- *   "x6_pipe": split-bf16 forward form: 0 = one LDS stage per 16-channel chunk
- *              (default), 1 = kernel-row pipelined, double-buffered.
+ *   "x6_pipe": split-bf16 forward/data-gradient form for images >= 32 wide:
+ *              2 = persistent warp-specialized, 16x16x32 MFMA tiles (default),
+ *              1 = the same with 32x32x16 tiles, 0 = one workgroup per tile.
+ *   "x6_wgrad": split-bf16 weight gradient: 1 = persistent warp-specialized
+ *              (default), 0 = one workgroup per item.
  *   "x6_probe": timing diagnostics of the single-stage form (bit 0: skip the
  *              in-loop prefetch, bit 1: skip the LDS staging) -- results are wrong. */
 int ugpg_set_tuning(const char* key, int value);

@@ -66,13 +66,14 @@ CONV_CASES = [
 BIG = {5, 6, 7}
 
 
-# x6 kernel forms (tuning knobs "x6_pipe" for forward/dgrad, "x6_wgrad"): 1 = persistent
-# warp-specialized (default), 0 = one workgroup per tile/item, 2 = persistent with
-# 16x16x32 MFMA tiles (forward/dgrad)
-X6_FORMS = {"x6": 1, "x6s": 0, "x6q": 2}
+# x6 kernel forms: (x6_pipe, x6_wgrad) tuning knobs.  Default = persistent
+# warp-specialized forward/dgrad with 16x16x32 MFMA tiles and persistent wgrad; "x6w"
+# the forward/dgrad form with 32x32x16 tiles; "x6s" one workgroup per tile/item.
+X6_FORMS = {"x6": (2, 1), "x6w": (1, 1), "x6s": (0, 0)}
+X6_DEFAULT = X6_FORMS["x6"]
 
 
-@pytest.fixture(params=["x6", "x6s", "x6q", "f32", "bf16"])
+@pytest.fixture(params=["x6", "x6w", "x6s", "f32", "bf16"])
 def math(request):
     """Every conv arithmetic form: split-bf16 (default, every kernel form), fp32
     MFMA, and bf16 (BASELINE config 3: operands rounded to bf16, fp32 accumulation)."""
@@ -80,11 +81,12 @@ def math(request):
     from ugpg._C import lib
     old = ops.conv_math()
     ops.set_conv_math({"f32": "f32", "bf16": "bf16"}.get(request.param, "x6"))
-    lib.ugpg_set_tuning(b"x6_pipe", X6_FORMS.get(request.param, 1))
-    lib.ugpg_set_tuning(b"x6_wgrad", X6_FORMS.get(request.param, 1))
+    pipe, wgrad = X6_FORMS.get(request.param, X6_DEFAULT)
+    lib.ugpg_set_tuning(b"x6_pipe", pipe)
+    lib.ugpg_set_tuning(b"x6_wgrad", wgrad)
     yield request.param
-    lib.ugpg_set_tuning(b"x6_pipe", 1)
-    lib.ugpg_set_tuning(b"x6_wgrad", 1)
+    lib.ugpg_set_tuning(b"x6_pipe", X6_DEFAULT[0])
+    lib.ugpg_set_tuning(b"x6_wgrad", X6_DEFAULT[1])
     ops.set_conv_math(old)
 
 

@@ -61,7 +61,7 @@ def main():
                     else f"clock {v[0]:.0f} MHz")
             print(f"{name} pipe {pipe}: {dt*1e3:.3f} ms/launch {flops/dt/1e12:.0f} TF  {what} "
                   f"(median of {nwg} workgroups)", flush=True)
-        lib.ugpg_set_tuning(b"x6_pipe", 1)
+        lib.ugpg_set_tuning(b"x6_pipe", 2)
 
 
 if __name__ == "__main__":

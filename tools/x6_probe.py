@@ -34,4 +34,4 @@ for pipe in (0, 1):
         ms = e0.elapsed_time(e1) / 20
         print(f"pipe {pipe} probe {probe}: {ms:.3f} ms  {fl / ms / 1e9:.0f} TF/s", flush=True)
 lib.ugpg_set_tuning(b"x6_probe", 0)
-lib.ugpg_set_tuning(b"x6_pipe", 1)
+lib.ugpg_set_tuning(b"x6_pipe", 2)

@@ -617,20 +617,52 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
 
     if (loader) {
         // ------------------------------------------------------------ loader waves
-        // Weight rows form one stream j = 3*step + ky; row j goes to ring slot j % 4 and
-        // to register set j % 3.  Phase ph of step k writes row 3(k+1)+ph (loaded two
-        // phases earlier) and loads row 3(k+1)+ph+2; phase 0 also writes halo(k+1) and
-        // loads halo(k+2) (three phases of flight).  Each wait leaves exactly the loads
-        // issued in the previous phase outstanding.
+        // Halo of step s: loaded into register set s & 1 (f32, with its activation
+        // coefficients) three steps ahead, written (activated, split) into A buffer s & 1
+        // during phases 0-1 of step s-1.  Weight rows: LDS-DMA, see below.
         const int lt = tid - 256;
-        f32x4 ra[A_PER][2];
-        unsigned avalid = 0;
-        Act4 r0, r1;
-        float lo = 0.f;
-        auto load_halo = [&](int k) {
-            k = min(k, last);
-            const int c = k % nchunk;
-            const Pos p = pos_of(item0 + (k / nchunk) * nslots);
+        f32x4 ra[2][A_PER][2];
+        unsigned avalid[2] = {0u, 0u};
+        Act4 r0[2], r1[2];
+        float lo[2] = {0.f, 0.f};
+        // cursor over loader steps (clamped to the last one): chunk, item, column block
+        // and tile position, advanced without divisions except at item changes
+        struct Cur {
+            int s, c, itm, nb;
+            Pos p;
+        };
+        auto cur_at = [&](int s) {
+            Cur q;
+            q.s = min(s, last);
+            q.c = q.s % nchunk;
+            q.itm = item0 + (q.s / nchunk) * nslots;
+            q.nb = q.itm % NB;
+            q.p = pos_of(q.itm);
+            return q;
+        };
+        auto advance = [&](Cur& q) {
+            if (q.s >= last) return;
+            ++q.s;
+            if (++q.c == nchunk) {
+                q.c = 0;
+                q.itm += nslots;
+                q.nb = q.itm % NB;
+                q.p = pos_of(q.itm);
+            }
+        };
+        // per-lane halo pixel offsets (row, column within the halo) of the A_PER vectors
+        int hy[A_PER], hx[A_PER];
+#pragma unroll
+        for (int v = 0; v < A_PER; ++v) {
+            const int idx = lt + v * 256;
+            const int hp = idx < A_ITEMS ? idx >> 1 : 0;
+            hy[v] = idx < A_ITEMS ? hp / HWD : -(1 << 20);  // never inside the image
+            hx[v] = hp % HWD;
+        }
+        auto load_halo = [&](const Cur& q, auto S) {
+            constexpr int st = decltype(S)::value;
+            const int c = q.c;
+            const Pos& p = q.p;
             const int cb0 = c * BKC;
             const bool second = cb0 >= a.C0;
             const float* src = second ? a.src1 : a.src0;
@@ -641,35 +673,37 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
             const bool aon = sc != nullptr;
             const float* scp = aon ? sc : g_act_ones;  // identity coefficients without activation
             const float* shp = aon ? sh : g_act_zeros;
-            lo = aon ? 0.f : -INFINITY;
+            lo[st] = aon ? 0.f : -INFINITY;
             const int cc = cb + (lt & 1) * 8;
-            r0.s = gld16(scp + cc);
-            r0.h = gld16(shp + cc);
-            r1.s = gld16(scp + cc + 4);
-            r1.h = gld16(shp + cc + 4);
-            avalid = 0;
+            r0[st].s = gld16(scp + cc);
+            r0[st].h = gld16(shp + cc);
+            r1[st].s = gld16(scp + cc + 4);
+            r1[st].h = gld16(shp + cc + 4);
+            unsigned av = 0;
 #pragma unroll
             for (int v = 0; v < A_PER; ++v) {
-                const int idx = lt + v * 256;
-                const int hp = idx < A_ITEMS ? idx >> 1 : 0, hh = lt & 1;
-                const int gy = p.ty0 - 1 + hp / HWD, gx = p.tx0 - 1 + hp % HWD;
-                const bool ok = idx < A_ITEMS && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
+                const int hh = lt & 1;
+                const int gy = p.ty0 - 1 + hy[v], gx = p.tx0 - 1 + hx[v];
+                const bool ok = gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
                 const int cy = min(max(gy, 0), a.H - 1), cx = min(max(gx, 0), a.W - 1);
-                const float* q = src + ((size_t)(p.b * a.H + cy) * a.W + cx) * Cs + cb + hh * 8;
-                ra[v][0] = gld16(q);
-                ra[v][1] = gld16(q + 4);
-                avalid |= (ok ? 1u : 0u) << v;
+                const float* gp = src + ((size_t)(p.b * a.H + cy) * a.W + cx) * Cs + cb + hh * 8;
+                ra[st][v][0] = gld16(gp);
+                ra[st][v][1] = gld16(gp + 4);
+                av |= (ok ? 1u : 0u) << v;
             }
+            avalid[st] = av;
         };
         constexpr int HALO_LOADS = 4 + 2 * A_PER;
-        auto store_halo = [&](int k) {
+        auto store_halo = [&](int k, auto S, int v0, int v1) {
+            constexpr int st = decltype(S)::value;
             u32x4* As = smem + (k & 1) * A_VECS;
 #pragma unroll
-            for (int v = 0; v < A_PER; ++v) {
+            for (int v = v0; v < v1; ++v) {
                 const int idx = lt + v * 256;
                 const int hp = idx >> 1, hh = idx & 1;
-                const f32x4 lo4 = act_floor4(ra[v][0], r0, lo), hi4 = act_floor4(ra[v][1], r1, lo);
-                const bool ok = (avalid >> v) & 1u;
+                const f32x4 lo4 = act_floor4(ra[st][v][0], r0[st], lo[st]),
+                            hi4 = act_floor4(ra[st][v][1], r1[st], lo[st]);
+                const bool ok = (avalid[st] >> v) & 1u;
                 const f32x8 x = {ok ? lo4.x : 0.f, ok ? lo4.y : 0.f, ok ? lo4.z : 0.f,
                                  ok ? lo4.w : 0.f, ok ? hi4.x : 0.f, ok ? hi4.y : 0.f,
                                  ok ? hi4.z : 0.f, ok ? hi4.w : 0.f};
@@ -680,42 +714,50 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
                 for (int q = 0; q < NP; ++q) As[(q * 2 + hh) * NHP + hl] = pc[q];
             }
         };
+        using Set0 = std::integral_constant<int, 0>;
+        using Set1 = std::integral_constant<int, 1>;
         // weight row j -> ring slot j % 4 by LDS-DMA: 16 B per lane, each wave-instruction
         // one contiguous KiB of the slot; rounds of 256 vectors, the last round's
         // missing waves repeat a present wave's copy (identical bytes, same place)
         constexpr int R_LASTW = (R_VEC - (R_PER - 1) * 256) / 64;  // waves with work in the last round
         static_assert(R_VEC % 64 == 0, "whole wave-instructions");
         const int lw = lt >> 6;
-        auto dma_row = [&](int j) {
-            const int k = min(j / 3, last), ky = j % 3;
-            const int c = k % nchunk;
-            const int nb = (item0 + (k / nchunk) * nslots) % NB;
-            const u32x4* ws =
-                static_cast<const u32x4*>(a.wpk) + (((size_t)nb * nchunk + c) * 3 + ky) * R_VEC;
-            u32x4* Bs = Bring + (j % NSLOT) * R_STR;
+        auto dma_row = [&](const Cur& q, int ky, int slot) {
+            const u32x4* ws = static_cast<const u32x4*>(a.wpk) +
+                              (((size_t)q.nb * nchunk + q.c) * 3 + ky) * R_VEC;
+            u32x4* Bs = Bring + slot * R_STR;
 #pragma unroll
             for (int v = 0; v < R_PER; ++v) {
                 const int base = v * 256 + (v + 1 < R_PER ? lw : lw % R_LASTW) * 64;
                 glds16(ws + base + lane, Bs + base);
             }
         };
-        // prologue: step 0 in LDS (halo buffer 0, rows 0-2), halo(1) in registers
-        load_halo(0);
-        vm_wait<0>();
-        store_halo(0);
-        dma_row(0);
-        dma_row(1);
-        dma_row(2);
-        load_halo(1);
-        vm_wait<0>();
+        // prologue: step 0 in LDS (halo buffer 0, rows 0-2), halos 1 and 2 in registers
+        {
+            const Cur q0 = cur_at(0);
+            load_halo(q0, Set0{});
+            vm_wait<0>();
+            store_halo(0, Set0{}, 0, A_PER);
+            dma_row(q0, 0, 0);
+            dma_row(q0, 1, 1);
+            dma_row(q0, 2, 2);
+            load_halo(cur_at(1), Set1{});
+            load_halo(cur_at(2), Set0{});
+            vm_wait<0>();
+        }
         lds_barrier();
+        Cur cw = cur_at(1), ch = cur_at(3);  // weight rows of step k+1, halo of step k+3
+        int sl = 3;                          // ring slot of row 3(k+1)
         // Phase ph of step k DMAs row j = 3(k+1)+ph into the slot of row j-4 (read in
         // the phase before, whose MFMAs consumed it before that phase's barrier) and
         // retires the previous phase's row before its own closing barrier, so every row
         // has about two phases of flight and is read one phase after that barrier.
-        // Phase 0 also writes halo(k+1) (loaded a step earlier) and loads halo(k+2).
-        // vmcnt counts the loader's loads and DMAs together, in issue order.
+        // Phases 0-1 write halo(k+1) (the compute waves first read it in phase 2), then
+        // phase 2 reloads the freed register set with halo(k+3).  vmcnt counts the
+        // loader's loads and DMAs together, in issue order: retiring a row retires every
+        // older halo load too.
         constexpr int R = R_PER, H = HALO_LOADS;
+        constexpr int HA = (A_PER + 1) / 2;  // halo vectors written in phase 0
 #ifdef X6R_STAMP
         // diagnostic build: loader cycles spent waiting for global loads / at barriers
         unsigned long long st_vm[3] = {0, 0, 0}, st_bar[3] = {0, 0, 0};
@@ -729,24 +771,39 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
 #else
 #define ST_WAIT(acc, stmt) stmt
 #endif
-        for (int k = 0; k < total; ++k) {
-            const int j = 3 * (k + 1);
+#ifdef X6R_NODMA  // diagnostic builds: drop a load stream (results are wrong)
+#define dma_row(...) ((void)0)
+#endif
+#ifdef X6R_NOHALO
+#define load_halo(...) ((void)0)
+#endif
+        auto step = [&](int k, auto S) {  // S = set of halo(k+1); rows j = 3(k+1) + ph
             // phase 0
-            dma_row(j);
-            ST_WAIT(st_vm[0], vm_wait<3 * R>());  // halo(k+1) (issued before rows j-2, j-1, j)
-            store_halo(k + 1);
-            load_halo(k + 2);
-            ST_WAIT(st_vm[0], vm_wait<R + H>());  // row j-1
+            dma_row(cw, 0, sl);
+            store_halo(k + 1, S, 0, HA);
+            ST_WAIT(st_vm[0], vm_wait<H + R>());  // row j-1
             ST_WAIT(st_bar[0], lds_barrier());
             // phase 1
-            dma_row(j + 1);
-            ST_WAIT(st_vm[1], vm_wait<H + R>());  // row j
+            dma_row(cw, 1, (sl + 1) & 3);
+            store_halo(k + 1, S, HA, A_PER);
+            ST_WAIT(st_vm[1], vm_wait<R>());  // row j (and halo(k+2))
             ST_WAIT(st_bar[1], lds_barrier());
             // phase 2
-            dma_row(j + 2);
-            ST_WAIT(st_vm[2], vm_wait<R>());  // row j+1 (and halo(k+2))
+            dma_row(cw, 2, (sl + 2) & 3);
+            load_halo(ch, S);
+            advance(cw);
+            advance(ch);
+            sl = (sl + 3) & 3;
+            ST_WAIT(st_vm[2], vm_wait<R + H>());  // row j+1
             ST_WAIT(st_bar[2], lds_barrier());
+        };
+        static_assert(NSLOT == 4, "slot arithmetic mod 4");
+        for (int k = 0; k < total; k += 2) {
+            step(k, Set1{});
+            if (k + 1 < total) step(k + 1, Set0{});
         }
+#undef dma_row
+#undef load_halo
 #undef ST_WAIT
 #ifdef X6R_STAMP
         if (tid == 256 && blockIdx.x < 1024) {
@@ -1455,14 +1512,14 @@ __global__ void pack_x6_kernel(const float* w, __bf16* wpk, int Cout, int Cin, i
     }
 }
 
-int g_x6_pipe = 1;   // tuning knob "x6_pipe" (see launch_fwd_x6)
+int g_x6_pipe = 2;   // tuning knob "x6_pipe" (see launch_fwd_x6)
 static bool use_x6r(int W) { return g_x6_pipe && W >= 32; }
 int fwd_x6_tile_w(int W) { return W >= 32 ? 32 : 16; }
 int fwd_x6_tile_h(int W) { return use_x6r(W) ? 8 : (W >= 32 ? 4 : 8); }
 int fwd_x6_stat_slots(int ntiles, int W) { return use_x6r(W) ? 2 * ntiles : ntiles; }
 
-// tuning knob "x6_pipe": 1 = conv3x3_fwd_x6r_kernel for images >= 32 wide (default),
-// 0 = conv3x3_fwd_x6_kernel everywhere
+// tuning knob "x6_pipe": conv3x3_fwd_x6r_kernel for images >= 32 wide with 16x16x32
+// tiles (2, default) or 32x32x16 tiles (1); 0 = conv3x3_fwd_x6_kernel everywhere
 int g_x6_probe = 0;  // "x6_probe": timing diagnostics (see ugpg_set_tuning)
 
 void launch_fwd_x6(const ConvFwdArgs& a_in, int np, hipStream_t st) {
