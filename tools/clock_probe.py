@@ -28,7 +28,8 @@ def main():
     ap.add_argument("--layers", default="inc.3,down1.3,down2.3,up4.0")
     ap.add_argument("--seconds", type=float, default=2.0)
     ap.add_argument("--stamps", action="store_true")
-    ap.add_argument("--pipes", default="1")
+    ap.add_argument("--pipes", default="2")
+    ap.add_argument("--wgrad", action="store_true", help="time the weight gradient instead")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     fn = lib.ugpg_debug_stamps if a.stamps else lib.ugpg_debug_clock
@@ -45,20 +46,30 @@ def main():
         wpk = ops.pack_conv3x3(w, C0 + C1, 0)
         st = torch.empty(3 * Cout * ops.conv_ntiles(B, H, H, C0 + C1, Cout, wpk), device=dev)
         flops = 2.0 * B * H * H * Cout * 9 * (C0 + C1)
+        dy = torch.randn(B, H, H, Cout, device=dev)
+        dw = torch.empty_like(w)
         for pipe in a.pipes.split(","):
             lib.ugpg_set_tuning(b"x6_pipe", int(pipe))
             n, t0 = 0, time.perf_counter()
             while time.perf_counter() - t0 < a.seconds:
                 for _ in range(20):
-                    ops.conv3x3_fwd(srcs, wpk, torch.zeros(Cout, device=dev), Cout, [out], stats=st)
+                    if a.wgrad:
+                        ops.conv3x3_wgrad(srcs, dy, dw, None, C0 + C1)
+                    else:
+                        ops.conv3x3_fwd(srcs, wpk, torch.zeros(Cout, device=dev), Cout, [out],
+                                        stats=st)
                 torch.cuda.synchronize()
                 n += 20
             dt = (time.perf_counter() - t0) / n
             v = (ctypes.c_double * 6)()
             nwg = fn(v)
-            what = (("loader vm_wait/barrier per phase " +
-                     " ".join(f"p{q}:{v[q]:.1%}/{v[3 + q]:.1%}" for q in range(3))) if a.stamps
-                    else f"clock {v[0]:.0f} MHz")
+            if not a.stamps:
+                what = f"clock {v[0]:.0f} MHz"
+            elif a.wgrad:
+                what = f"loader vm_wait {v[0]:.1%} barrier {v[3]:.1%}"
+            else:
+                what = "loader vm_wait/barrier per phase " + " ".join(
+                    f"p{q}:{v[q]:.1%}/{v[3 + q]:.1%}" for q in range(3))
             print(f"{name} pipe {pipe}: {dt*1e3:.3f} ms/launch {flops/dt/1e12:.0f} TF  {what} "
                   f"(median of {nwg} workgroups)", flush=True)
         lib.ugpg_set_tuning(b"x6_pipe", 2)

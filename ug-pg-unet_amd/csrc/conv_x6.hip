@@ -528,10 +528,10 @@ __device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a, f32x4 (&
     }
 }
 
-#if defined(X6R_CLOCK) || defined(X6R_STAMP)
+#if defined(X6R_CLOCK) || defined(X6R_STAMP) || defined(X6W_STAMP)
 __device__ unsigned long long g_clk[8192];
 #endif
-#ifdef X6R_STAMP
+#if defined(X6R_STAMP) || defined(X6W_STAMP)
 // diagnostic build only: median over workgroups of the loader waves' fraction of the
 // main loop spent in vm_wait (out[0..2], per phase) and at barriers (out[3..5])
 extern "C" int ugpg_debug_stamps(double* out) {
@@ -805,6 +805,8 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
 #undef dma_row
 #undef load_halo
 #undef ST_WAIT
+        vm_wait<0>();  // no load outlives the workgroup (nothing may run before this wait:
+                       // the last loads' destination registers are dead to the compiler)
 #ifdef X6R_STAMP
         if (tid == 256 && blockIdx.x < 1024) {
             g_clk[8 * blockIdx.x] = __builtin_amdgcn_s_memtime() - st_t0;
@@ -814,7 +816,6 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
             }
         }
 #endif
-        vm_wait<0>();  // no load outlives the workgroup
         return;
     }
 
@@ -1338,14 +1339,38 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
         advance(lc);
         gload(lc);  // step 1
         lds_barrier();
+#ifdef X6W_STAMP
+        // diagnostic build: loader cycles waiting for global loads / at the barrier
+        unsigned long long st_vm = 0, st_bar = 0;
+        const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();
+#define ST_WAIT(acc, stmt)                                          \
+    {                                                               \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+        stmt;                                                       \
+        acc += __builtin_amdgcn_s_memtime() - t_;                   \
+    }
+#else
+#define ST_WAIT(acc, stmt) stmt
+#endif
         for (int k = 0; k < total; ++k) {
-            vm_wait<0>();
+            ST_WAIT(st_vm, vm_wait<0>());
             lstore((k + 1) & 1);  // step k+1
             advance(lc);
+#ifndef X6W_NOLOAD  // diagnostic build: re-store step 1's registers (results are wrong)
             gload(lc);            // step k+2, in flight across the barrier
-            lds_barrier();
+#endif
+            ST_WAIT(st_bar, lds_barrier());
         }
-        vm_wait<0>();  // no load outlives the workgroup
+#undef ST_WAIT
+        vm_wait<0>();  // no load outlives the workgroup (nothing may run before this wait:
+                       // the last loads' destination registers are dead to the compiler)
+#ifdef X6W_STAMP
+        if (tid == 256 && blockIdx.x < 1024) {
+            g_clk[8 * blockIdx.x] = __builtin_amdgcn_s_memtime() - st_t0;
+            g_clk[8 * blockIdx.x + 1] = st_vm;
+            g_clk[8 * blockIdx.x + 4] = st_bar;
+        }
+#endif
         return;
     }
 
