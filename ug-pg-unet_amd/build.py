@@ -44,7 +44,9 @@ def _newest_header() -> float:
 
 # memory-bound kernels: no FMA contraction, so interpolation weights round exactly
 # like ATen's CPU kernels (align_corners source index = rounded(scale*o))
-PER_FILE = {"ops.hip": ["-ffp-contract=off"]}
+# conv_x6.hip: no SLP vectorization -- packed f32 VALU (v_pk_add_f32 ...) issued beside the
+# MFMA waves slows them (MI355X_MICROARCH.md, 'price of one filler beside MFMAs')
+PER_FILE = {"ops.hip": ["-ffp-contract=off"], "conv_x6.hip": ["-fno-slp-vectorize"]}
 
 
 def _compile(src: Path, force: bool, bdir: Path = BUILD, defines=()) -> Path:

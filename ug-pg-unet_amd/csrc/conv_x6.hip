@@ -37,15 +37,40 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x8 __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// (a, b) rounded to bf16 (nearest even) and packed, a in the low half (one
+// v_cvt_pk_bf16_f32); the two rounded values are recovered from the packed word by
+// bit operations, so no element is converted twice
+__device__ __forceinline__ unsigned pk_bf16(float a, float b, float& ra, float& rb) {
+    const unsigned u = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a, b}, bf16x2));
+    ra = __builtin_bit_cast(float, u << 16);
+    rb = __builtin_bit_cast(float, u & 0xffff0000u);
+    return u;
+}
+// the three bf16 pieces of a pair: x = hi + mid + lo to fp32 accuracy
+__device__ __forceinline__ void split3_pair(float a, float b, unsigned& u0, unsigned& u1,
+                                            unsigned& u2) {
+    float ha, hb;
+    u0 = pk_bf16(a, b, ha, hb);
+    a -= ha;
+    b -= hb;
+    u1 = pk_bf16(a, b, ha, hb);
+    a -= ha;
+    b -= hb;
+    u2 = pk_bf16(a, b, ha, hb);
+}
+
 __device__ __forceinline__ void split3(f32x8 v, u32x4& p0, u32x4& p1, u32x4& p2) {
-    const bf16x8 h = __builtin_convertvector(v, bf16x8);
-    f32x8 r = v - __builtin_convertvector(h, f32x8);
-    const bf16x8 m = __builtin_convertvector(r, bf16x8);
-    r = r - __builtin_convertvector(m, f32x8);
-    const bf16x8 l = __builtin_convertvector(r, bf16x8);
-    p0 = __builtin_bit_cast(u32x4, h);
-    p1 = __builtin_bit_cast(u32x4, m);
-    p2 = __builtin_bit_cast(u32x4, l);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        unsigned a, b, c;
+        split3_pair(v[2 * i], v[2 * i + 1], a, b, c);
+        p0[i] = a;
+        p1[i] = b;
+        p2[i] = c;
+    }
 }
 
 // compute units of the stream's device (cached per device)
@@ -467,13 +492,22 @@ __device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a, f32x4 (&
             float* p = out + (size_t)((b * a.H + ty0 + py) * a.W + tx0 + px) * ostride + ocol0 + c0;
 #pragma unroll
             for (int nt = 0; nt < 2; ++nt) {
-                const f32x4 v = acc[mt][nt] + bv[nt];
+                // scalar arithmetic throughout: packed f32 VALU (v_pk_*) beside the
+                // partner waves' MFMAs costs more than it saves (MI355X_MICROARCH.md)
+                f32x4 v;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) v[i] = acc[mt][nt][i] + bv[nt][i];
                 acc[mt][nt] = v;
                 if (ok) {
                     f32x4* q = reinterpret_cast<f32x4*>(p + 16 * nt);
-                    if constexpr (ACC) *q = *q + v;
-                    else *q = v;
-                    psum[nt] += v;
+                    if constexpr (ACC) {
+                        const f32x4 o = *q;
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) v[i] += o[i];
+                    }
+                    *q = v;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) psum[nt][i] += acc[mt][nt][i];
                 }
             }
         }
@@ -502,8 +536,11 @@ __device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a, f32x4 (&
         if ((mt & 1) * 16 + l16 < vw) {
 #pragma unroll
             for (int nt = 0; nt < 2; ++nt) {
-                const f32x4 d = acc[mt][nt] - mu[nt];
-                q[nt] += d * d;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float d = acc[mt][nt][i] - mu[nt][i];
+                    q[nt][i] = fmaf(d, d, q[nt][i]);
+                }
             }
         }
     }
@@ -1015,14 +1052,14 @@ typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void split3_4(f32x4 v, u32x2& p0, u32x2& p1, u32x2& p2) {
-    const bf16x4 h = __builtin_convertvector(v, bf16x4);
-    f32x4 r = v - __builtin_convertvector(h, f32x4);
-    const bf16x4 m = __builtin_convertvector(r, bf16x4);
-    r = r - __builtin_convertvector(m, f32x4);
-    const bf16x4 l = __builtin_convertvector(r, bf16x4);
-    p0 = __builtin_bit_cast(u32x2, h);
-    p1 = __builtin_bit_cast(u32x2, m);
-    p2 = __builtin_bit_cast(u32x2, l);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        unsigned a, b, c;
+        split3_pair(v[2 * i], v[2 * i + 1], a, b, c);
+        p0[i] = a;
+        p1[i] = b;
+        p2[i] = c;
+    }
 }
 
 template <int NP>
@@ -1268,9 +1305,39 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
         Act4 xa;
         float xlo = 0.f;
         unsigned dvalid = 0, xvalid = 0;
-        auto gload = [&](const Cur& c) {
-            const int nb = c.item % NCO, cb = (c.item / NCO) % NCI;
-            const int co0 = nb * 64, ci0 = cb * 64;
+        // the loader's cursor also carries the item's co / ci blocks and the tile's
+        // image position, updated without divisions inside an item
+        struct LCur {
+            Cur c;
+            int nb, cb, b, ty0, tx0;
+        };
+        auto lderive = [&](LCur& l) {
+            l.nb = l.c.item % NCO;
+            l.cb = (l.c.item / NCO) % NCI;
+            const int trem = l.c.tile % tpi;
+            l.b = l.c.tile / tpi;
+            l.ty0 = (trem / a.tiles_x) * TH;
+            l.tx0 = (trem % a.tiles_x) * TW;
+        };
+        auto ladvance = [&](LCur& l) {  // stays on the last step past the end
+            if (l.c.tile + 1 < l.c.tend) {
+                ++l.c.tile;
+                l.tx0 += TW;
+                if (l.tx0 >= a.tiles_x * TW) {
+                    l.tx0 = 0;
+                    l.ty0 += TH;
+                    if (l.ty0 >= a.tiles_y * TH) {
+                        l.ty0 = 0;
+                        ++l.b;
+                    }
+                }
+            } else if (l.c.item + nslots < iend) {
+                item_range(l.c.item + nslots, l.c);
+                lderive(l);
+            }
+        };
+        auto gload = [&](const LCur& c) {
+            const int co0 = c.nb * 64, ci0 = c.cb * 64;
             const bool second = ci0 >= a.C0;
             const float* xsrc = second ? a.src1 : a.src0;
             const float* xsc = second ? a.sc1 : a.sc0;
@@ -1281,30 +1348,67 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
             const int cq = cbase + (lt & 15) * 4;  // q = idx & 15 = lt & 15
             xa.s = gld16((xon ? xsc : g_act_ones) + cq);
             xa.h = gld16((xon ? xsh : g_act_zeros) + cq);
-            const int b = c.tile / tpi, trem = c.tile % tpi;
-            const int ty0 = (trem / a.tiles_x) * TH, tx0 = (trem % a.tiles_x) * TW;
-            dvalid = 0;
+            const int b = c.b, ty0 = c.ty0, tx0 = c.tx0;
+            const int q4 = (lt & 15) * 4;
+            // per-lane pixel positions inside the tile (compile-time divisors): dy
+            // pixels, and halo pixels relative to the tile origin (-1, -1)
+            int dyo[DY_PER], xpy[X_PER], xpx[X_PER];
+            unsigned xin = 0;  // x vectors that exist (idx < X_Q)
 #pragma unroll
             for (int v = 0; v < DY_PER; ++v) {
-                const int idx = lt + v * 256;
-                const int p = idx >> 4, q = idx & 15;
-                const int gy = ty0 + p / TW, gx = tx0 + p % TW;
-                const bool ok = gy < a.H && gx < a.W;
-                const int cy = min(gy, a.H - 1), cx = min(gx, a.W - 1);
-                rdy[v] = gld16(a.dy + ((size_t)(b * a.H + cy) * a.W + cx) * a.Cout + co0 + q * 4);
-                dvalid |= (ok ? 1u : 0u) << v;
+                const int p = (lt + v * 256) >> 4;
+                dyo[v] = (p / TW) * a.W + p % TW;
             }
-            xvalid = 0;
 #pragma unroll
             for (int v = 0; v < X_PER; ++v) {
                 const int idx = lt + v * 256;
-                const int hp = idx < X_Q ? idx >> 4 : 0, q = idx & 15;
-                const int gy = ty0 - 1 + hp / HWD, gx = tx0 - 1 + hp % HWD;
-                const bool ok = idx < X_Q && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
-                const int cy = min(max(gy, 0), a.H - 1), cx = min(max(gx, 0), a.W - 1);
-                rx[v] = gld16(xsrc + ((size_t)(b * a.H + cy) * a.W + cx) * Cs + cbase + q * 4);
-                xvalid |= (ok ? 1u : 0u) << v;
+                const int hp = idx < X_Q ? idx >> 4 : 0;
+                xpy[v] = hp / HWD - 1;
+                xpx[v] = hp % HWD - 1;
+                xin |= (idx < X_Q ? 1u : 0u) << v;
             }
+            // element offsets from the tile origin; only integer work depends on whether
+            // the tile touches the image border, the loads are one straight sequence
+            // (a load inside a branch would leave its registers in flight on the
+            // structurized path that skips it)
+            int dof[DY_PER], xof[X_PER];
+            if (ty0 >= 1 && tx0 >= 1 && ty0 + TH + 1 <= a.H && tx0 + TW + 1 <= a.W) {
+                // interior tile (uniform): every dy pixel and halo pixel is in the image
+#pragma unroll
+                for (int v = 0; v < DY_PER; ++v) dof[v] = dyo[v] * a.Cout;
+#pragma unroll
+                for (int v = 0; v < X_PER; ++v)
+                    xof[v] = ((xin >> v) & 1u) ? (xpy[v] * a.W + xpx[v]) * Cs : 0;
+                dvalid = (1u << DY_PER) - 1;
+                xvalid = xin;
+            } else {
+                dvalid = 0;
+#pragma unroll
+                for (int v = 0; v < DY_PER; ++v) {
+                    const int p = (lt + v * 256) >> 4;
+                    const int gy = ty0 + p / TW, gx = tx0 + p % TW;
+                    const bool ok = gy < a.H && gx < a.W;
+                    const int cy = min(gy, a.H - 1), cx = min(gx, a.W - 1);
+                    dof[v] = ((cy - ty0) * a.W + (cx - tx0)) * a.Cout;
+                    dvalid |= (ok ? 1u : 0u) << v;
+                }
+                xvalid = 0;
+#pragma unroll
+                for (int v = 0; v < X_PER; ++v) {
+                    const int gy = ty0 + xpy[v], gx = tx0 + xpx[v];
+                    const bool ok =
+                        ((xin >> v) & 1u) && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
+                    const int cy = min(max(gy, 0), a.H - 1), cx = min(max(gx, 0), a.W - 1);
+                    xof[v] = ((cy - ty0) * a.W + (cx - tx0)) * Cs;
+                    xvalid |= (ok ? 1u : 0u) << v;
+                }
+            }
+            const float* dyb = a.dy + ((size_t)(b * a.H + ty0) * a.W + tx0) * a.Cout + co0 + q4;
+            const float* xb = xsrc + ((size_t)(b * a.H + ty0) * a.W + tx0) * Cs + cbase + q4;
+#pragma unroll
+            for (int v = 0; v < DY_PER; ++v) rdy[v] = gld16(dyb + dof[v]);
+#pragma unroll
+            for (int v = 0; v < X_PER; ++v) rx[v] = gld16(xb + xof[v]);
         };
         // record layout: [piece][64 ch] bf16 at byte piece*128 + ch*2
         auto put = [&](char* rec, int q, f32x4 v) {
@@ -1331,12 +1435,13 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
                 put(idx < X_Q ? xs + (idx >> 4) * REC : dummy, idx & 15, val);
             }
         };
-        Cur lc;
-        item_range(item0, lc);
+        LCur lc;
+        item_range(item0, lc.c);
+        lderive(lc);
         gload(lc);
         vm_wait<0>();
         lstore(0);
-        advance(lc);
+        ladvance(lc);
         gload(lc);  // step 1
         lds_barrier();
 #ifdef X6W_STAMP
@@ -1355,7 +1460,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
         for (int k = 0; k < total; ++k) {
             ST_WAIT(st_vm, vm_wait<0>());
             lstore((k + 1) & 1);  // step k+1
-            advance(lc);
+            ladvance(lc);
 #ifndef X6W_NOLOAD  // diagnostic build: re-store step 1's registers (results are wrong)
             gload(lc);            // step k+2, in flight across the barrier
 #endif
