@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--secondary-steps", type=int, default=5,
+                    help="steps of the secondary line (S4 fwd+bwd without the uncertainty "
+                         "map, SURVEY.md 8d); 0 = skip")
     ap.add_argument("--conv-math", choices=("x6", "bf16", "f32"), default="x6",
                     help="conv arithmetic: x6 = fp32-accurate split-bf16 (configs[1], default); "
                          "bf16 = bf16 operands, fp32 accumulation (configs[2] arithmetic)")
@@ -143,6 +146,41 @@ def main():
     ms = 1000 * elapsed / args.steps
     value = world * B * args.steps / elapsed
 
+    # secondary line (after the timed region): the pure S4 fwd+bwd step without the
+    # uncertainty map = forward + BCE(pos_weight) + backward + all-reduce + RMSprop
+    secondary = None
+    if args.secondary_steps > 0:
+        from ugpg.dist import allreduce_gradients, overlapped_allreduce
+        from ugpg.loss import weighted_loss_tensors
+
+        def step_plain():
+            mbuf = torch.zeros(8, dtype=torch.float32, device=dev)
+            tr.optimizer.zero_grad()
+            out = tr.current_model(x)
+            final, _ = weighted_loss_tensors(tr.base_criterion, out, t, None, 1.0, out=mbuf[0:2])
+            with overlapped_allreduce():
+                final.backward()
+            tr.optimizer.grad_scale = allreduce_gradients(
+                [p for g in tr.optimizer.param_groups for p in g["params"]])
+            tr.optimizer.step()
+            return mbuf.tolist()
+
+        step_plain()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.secondary_steps):
+            step_plain()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el2 = max_over_ranks(time.perf_counter() - t1, dev)
+        secondary = {"metric": "images/sec Stage-4 256x256 bs16 fwd+bwd without uncertainty map",
+                     "value": round(world * B * args.secondary_steps / el2, 3),
+                     "ms_per_step": round(1000 * el2 / args.secondary_steps, 3),
+                     "steps": args.secondary_steps}
+
     roof = None
     kernels = None
     if timer is not None:
@@ -188,6 +226,7 @@ def main():
         "last_step_metrics": {"loss": last[0], "base_loss": last[1], "dice": last[2],
                               "unc_mean": last[5], "unc_std": last[6]},
         "cpu_baseline": None,
+        "secondary": secondary,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)

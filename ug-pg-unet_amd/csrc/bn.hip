@@ -16,40 +16,45 @@ __global__ void bn_finalize_kernel(const float* __restrict__ stats, int ntiles, 
                                    float* rvar, int64_t* nbt, float momentum, float eps,
                                    float* mean_o, float* invstd_o, float* scale_o,
                                    float* shift_o) {
+    // Parallel-variance combination of the per-tile partials (count, sum, M2) in two
+    // passes: total count and sum -> mean m; then M2 = sum_t M2_t + (sum_t - n_t m)^2 / n_t
+    // (deviations of the tile means from the global mean, no per-slot division chain)
     const int c = blockIdx.x;
     __shared__ double sn[256], sm[256], sq[256];
     const float* cnt = stats + (size_t)c * ntiles;
     const float* sum = stats + ((size_t)C + c) * ntiles;
     const float* m2 = stats + ((size_t)2 * C + c) * ntiles;
-    double n = 0, mu = 0, M = 0;
+    double n = 0, S = 0;
     for (int t = threadIdx.x; t < ntiles; t += blockDim.x) {
-        const double nb = cnt[t];
-        if (nb <= 0) continue;
-        const double mb = (double)sum[t] / nb, Mb = m2[t];
-        const double nn = n + nb, d = mb - mu;
-        mu += d * nb / nn;
-        M += Mb + d * d * n * nb / nn;
-        n = nn;
+        n += cnt[t];
+        S += sum[t];
     }
     sn[threadIdx.x] = n;
-    sm[threadIdx.x] = mu;
-    sq[threadIdx.x] = M;
+    sm[threadIdx.x] = S;
     __syncthreads();
     for (int s = blockDim.x / 2; s > 0; s >>= 1) {
         if (threadIdx.x < s) {
-            const double na = sn[threadIdx.x], nb = sn[threadIdx.x + s];
-            const double nn = na + nb;
-            if (nb > 0) {
-                const double d = sm[threadIdx.x + s] - sm[threadIdx.x];
-                sm[threadIdx.x] += d * nb / nn;
-                sq[threadIdx.x] += sq[threadIdx.x + s] + d * d * na * nb / nn;
-                sn[threadIdx.x] = nn;
-            }
+            sn[threadIdx.x] += sn[threadIdx.x + s];
+            sm[threadIdx.x] += sm[threadIdx.x + s];
         }
         __syncthreads();
     }
+    const double Ntot = sn[0], mean = Ntot > 0 ? sm[0] / Ntot : 0.0;
+    double M = 0;
+    for (int t = threadIdx.x; t < ntiles; t += blockDim.x) {
+        const float nb = cnt[t];
+        if (nb <= 0.f) continue;
+        const double d = (double)sum[t] - (double)nb * mean;
+        M += (double)m2[t] + d * d * (double)(1.0f / nb);
+    }
+    sq[threadIdx.x] = M;
+    __syncthreads();
+    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+        if (threadIdx.x < s) sq[threadIdx.x] += sq[threadIdx.x + s];
+        __syncthreads();
+    }
     if (threadIdx.x == 0) {
-        const double N = sn[0], m = sm[0];
+        const double N = Ntot, m = mean;
         const double var = sq[0] / N;
         const float inv = (float)(1.0 / sqrt(var + (double)eps));
         const float mf = (float)m;
