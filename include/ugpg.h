@@ -284,6 +284,35 @@ int ugpg_relu_bwd(const float* y, const float* dy, float* dx, int64_t n, void* s
 /* elementwise y = x * mask (dropout with a precomputed scaled mask) */
 int ugpg_mul(const float* x, const float* m, float* y, int64_t n, void* stream);
 
+/* ---- MoNuSeg augmentation (aug_monuseg_dataset.py:113-148,
+ * monuseg_dataset.py:137-190): PIL's 8-bit arithmetic reproduced on the GPU. -------- */
+/* One separable pass of PIL's antialiasing resampler (Image.resize BILINEAR): `outer`
+ * rows, resampled axis n_in -> n_out, `inner_after` contiguous bytes per axis position
+ * (C for the horizontal pass over HWC rows, OW*C for the vertical pass);
+ * bounds[2*o] = first tap, bounds[2*o+1] = tap count, kk[o*ksize + t] = PIL's 22-bit
+ * fixed-point coefficients (host-computed, ugpg/augment.py:resample_coeffs). */
+int ugpg_resample_aa_u8(const uint8_t* in, int64_t outer, int n_in, int n_out,
+                        int inner_after, const int* bounds, const int* kk, int ksize,
+                        uint8_t* out, void* stream);
+/* nearest resize (Image.resize NEAREST) of B HWC images with host-tabulated source
+ * rows / columns (PIL's accumulated coordinates) */
+int ugpg_resize_nearest_u8(const uint8_t* in, int64_t B, int H, int W, int C, const int* ytab,
+                           const int* xtab, uint8_t* out, int OH, int OW, void* stream);
+/* sizes of the per-sample parameter records (host layout check) */
+int ugpg_augment_param_sizes(int* geom_bytes, int* color_bytes);
+/* hflip, vflip, Image.rotate (image BILINEAR: double-precision affine map, truncating
+ * bilinear filter; mask NEAREST: 16.16 fixed point), adjust_brightness; B samples of
+ * S x S (RGB HWC uint8 + mask uint8); lsum[B] receives each result's L sum */
+int ugpg_augment_geom(const uint8_t* img, const uint8_t* mask, int S, int64_t B,
+                      const void* params, uint8_t* out_img, uint8_t* out_mask, unsigned* lsum,
+                      void* stream);
+/* adjust_contrast (grey level int(mean L + .5)), adjust_saturation, adjust_hue (PIL HSV
+ * round trip, uint8 hue shift), ToTensor (u8_to_f32[256] = torch's v/255) -> out
+ * (B,3,S,S) float; mask -> out_mask (B,1,S,S) float */
+int ugpg_augment_color(const uint8_t* img, const uint8_t* mask, int S, int64_t B,
+                       const void* params, const unsigned* lsum, const float* u8_to_f32,
+                       float* out, float* out_mask, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

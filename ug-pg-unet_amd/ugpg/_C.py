@@ -85,6 +85,11 @@ SIGNATURES = {
     "ugpg_adam_step": (_i, [_p, _p, _p, _p, _i64, _f, _f, _f, _f, _f, _i64, _f, _p]),
     "ugpg_relu_bwd": (_i, [_p, _p, _p, _i64, _p]),
     "ugpg_mul": (_i, [_p, _p, _p, _i64, _p]),
+    "ugpg_resample_aa_u8": (_i, [_p, _i64, _i, _i, _i, _p, _p, _i, _p, _p]),
+    "ugpg_resize_nearest_u8": (_i, [_p, _i64, _i, _i, _i, _p, _p, _p, _i, _i, _p]),
+    "ugpg_augment_param_sizes": (_i, [C.POINTER(_i), C.POINTER(_i)]),
+    "ugpg_augment_geom": (_i, [_p, _p, _i, _i64, _p, _p, _p, _p, _p]),
+    "ugpg_augment_color": (_i, [_p, _p, _i, _i64, _p, _p, _p, _p, _p, _p]),
 }
 
 

@@ -16,5 +16,6 @@ from .loss import UncertaintyGuidedLoss  # noqa: F401
 from .optim import RMSprop  # noqa: F401
 from .trainer import UncertaintyGuidedProgressiveTrainer  # noqa: F401
 from .evaluation import MoNuSegTester, evaluate_logits, predict_masks  # noqa: F401
+from .augment import AugMoNuSegDataset, MoNuSegAugmenter, MoNuSegDataset  # noqa: F401
 
 __version__ = "0.1.0"
