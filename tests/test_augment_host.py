@@ -85,3 +85,19 @@ def test_xml_annotations_rasterise_like_the_reference(tmp_path):
 def test_parameter_records_match_the_library_layout():
     A._check_layout()  # struct sizes from the C-ABI (no GPU needed)
     assert A.GEOM_DTYPE.fields["fa"][1] == 48 and A.GEOM_DTYPE.fields["brightness"][1] == 84
+
+
+def test_create_train_val_split_follows_the_reference_sampling(tmp_path):
+    import os
+    import random
+    for d in ("images", "annots"):
+        os.makedirs(tmp_path / "train" / d)
+    names = [f"t{k:02d}.tif" for k in range(10)]
+    for n in names:
+        (tmp_path / "train" / "images" / n).write_bytes(b"x")
+        (tmp_path / "train" / "annots" / n.replace(".tif", ".xml")).write_text("<a/>")
+    got = A.create_train_val_split(str(tmp_path), val_ratio=0.3, seed=7)
+    random.seed(7)
+    assert got == random.sample(sorted(names), 3)
+    assert sorted(os.listdir(tmp_path / "val" / "images")) == sorted(got)
+    assert len(os.listdir(tmp_path / "train" / "images")) == 10  # copy, not move

@@ -3,7 +3,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-bash tools/gpu_tests.sh tests/test_gpu_ops.py tests/test_gpu_models.py tests/test_gpu_herlev.py tests/test_gpu_eval.py || exit $?
+bash tools/gpu_tests.sh tests/test_gpu_ops.py tests/test_gpu_models.py tests/test_gpu_herlev.py tests/test_gpu_eval.py tests/test_gpu_augment.py || exit $?
 timeout -k 10 600 python bench.py --steps 10 --warmup 3 > gpurun_out/bench.json 2> gpurun_out/bench.err
 rc=$?; echo "bench rc=$rc"; tail -c 3000 gpurun_out/bench.json; tail -3 gpurun_out/bench.err
 [ $rc -ne 0 ] && exit $rc

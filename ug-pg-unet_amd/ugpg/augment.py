@@ -371,3 +371,32 @@ class MoNuSegDataset(_MoNuSegBase):
 
     def _augmenting(self):
         return self.augment and self.split == "train"
+
+
+def create_train_val_split(data_dir: str, val_ratio: float = 0.2, seed: int = 42,
+                           move: bool = False):
+    """monuseg_dataset.py:245-299: copy (or move) a seeded random sample of
+    train/images/*.tif and their annots/*.xml into val/ (random.seed(seed);
+    random.sample over the sorted file list, as the reference)."""
+    import shutil
+    train_dir, val_dir = os.path.join(data_dir, "train"), os.path.join(data_dir, "val")
+    os.makedirs(os.path.join(val_dir, "images"), exist_ok=True)
+    os.makedirs(os.path.join(val_dir, "annots"), exist_ok=True)
+    image_files = sorted(f for f in os.listdir(os.path.join(train_dir, "images"))
+                         if f.endswith(".tif"))
+    random.seed(seed)
+    n_val = int(len(image_files) * val_ratio)
+    val_files = random.sample(image_files, n_val)
+    action = "move" if move else "copy"
+    print(f"{action.title()}ing {n_val} files to validation set (move={move})...")
+    op = shutil.move if move else shutil.copy2
+    for img_file in val_files:
+        annot_file = img_file.replace(".tif", ".xml")
+        op(os.path.join(train_dir, "images", img_file), os.path.join(val_dir, "images", img_file))
+        src_annot = os.path.join(train_dir, "annots", annot_file)
+        if os.path.exists(src_annot):
+            op(src_annot, os.path.join(val_dir, "annots", annot_file))
+    print("Train/Val split complete:")
+    print(f"  Training: {len(os.listdir(os.path.join(train_dir, 'images')))} samples")
+    print(f"  Validation: {len(os.listdir(os.path.join(val_dir, 'images')))} samples")
+    return val_files
