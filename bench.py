@@ -102,8 +102,10 @@ def main():
     from ugpg.dist import broadcast_parameters, init_from_env, max_over_ranks
 
     ops.set_conv_math(args.conv_math)
-    rank, world = init_from_env("nccl")
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # UGPG_DIST_BACKEND / UGPG_BENCH_DEVICE: rehearsal of the N-rank path on one GPU
+    # (gloo, every rank on device 0); the driver's runs use RCCL, one GPU per rank
+    rank, world = init_from_env(os.environ.get("UGPG_DIST_BACKEND", "nccl"))
+    local = int(os.environ.get("UGPG_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0")))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world != args.gpus and rank == 0:

@@ -39,7 +39,8 @@ const char* ugpg_last_error(void);
  *              2 = 8x8x64) where it is legal for the shape; -1 = heuristic.
  *   "x6_pipe": split-bf16 forward/data-gradient form for images >= 32 wide:
  *              2 = persistent warp-specialized, 16x16x32 MFMA tiles (default),
- *              1 = the same with 32x32x16 tiles, 0 = one workgroup per tile.
+ *              1 = the same with 32x32x16 tiles, 3 = as 2 plus 16x16-pixel items
+ *              for images 16-31 wide, 0 = one workgroup per tile.
  *   "x6_wgrad": split-bf16 weight gradient: 1 = persistent warp-specialized
  *              (default), 0 = one workgroup per item.
  *   "x6_probe": timing diagnostics of the single-stage form (bit 0: skip the

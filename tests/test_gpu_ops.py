@@ -62,18 +62,21 @@ CONV_CASES = [
     (3, 40, 24, 8, 0, 128, True),      # ragged 8x16 wgrad tiles, 2 co blocks, lazy affine
     (2, 4, 4, 512, 0, 512, True),      # Down4 of a 64^2 stage: 4x4 image in a 8x16 tile
     (2, 8, 8, 256, 256, 256, True),    # Up1 of a 64^2 stage
+    (2, 20, 24, 64, 0, 64, True),      # 16x16-item persistent form: ragged rows and columns
+    (1, 18, 17, 128, 64, 128, True),   # same, concat input, 2 partial tiles per side
 ]
 BIG = {5, 6, 7}
 
 
 # x6 kernel forms: (x6_pipe, x6_wgrad) tuning knobs.  Default = persistent
 # warp-specialized forward/dgrad with 16x16x32 MFMA tiles and persistent wgrad; "x6w"
-# the forward/dgrad form with 32x32x16 tiles; "x6s" one workgroup per tile/item.
-X6_FORMS = {"x6": (2, 1), "x6w": (1, 1), "x6s": (0, 0)}
+# the forward/dgrad form with 32x32x16 tiles; "x6t" adds 16x16-pixel items for images
+# 16-31 wide; "x6s" one workgroup per tile/item.
+X6_FORMS = {"x6": (2, 1), "x6w": (1, 1), "x6t": (3, 1), "x6s": (0, 0)}
 X6_DEFAULT = X6_FORMS["x6"]
 
 
-@pytest.fixture(params=["x6", "x6w", "x6s", "f32", "bf16"])
+@pytest.fixture(params=["x6", "x6w", "x6t", "x6s", "f32", "bf16"])
 def math(request):
     """Every conv arithmetic form: split-bf16 (default, every kernel form), fp32
     MFMA, and bf16 (BASELINE config 3: operands rounded to bf16, fp32 accumulation)."""

@@ -633,8 +633,11 @@ extern "C" int ugpg_set_tuning(const char* key, int value) {
 
 extern "C" int ugpg_conv3x3_fwd_ntiles(int B, int H, int W, int Cin, int Cout, int wfmt) {
     (void)Cin;
-    if (wfmt == UGPG_WFMT_X6 || wfmt == UGPG_WFMT_BF16)
-        return fwd_x6_stat_slots((int)(B * cdiv(H, fwd_x6_tile_h(W)) * cdiv(W, fwd_x6_tile_w(W))), W);
+    if (wfmt == UGPG_WFMT_X6 || wfmt == UGPG_WFMT_BF16) {
+        const int np = wfmt == UGPG_WFMT_X6 ? 3 : 1;
+        return fwd_x6_stat_slots(
+            (int)(B * cdiv(H, fwd_x6_tile_h(W, np)) * cdiv(W, fwd_x6_tile_w(W, np))), W, np);
+    }
     const int cfg = pick_fwd_cfg(B, H, W, Cout, Cout);
     return (int)(B * cdiv(H, kFwd[cfg].th) * cdiv(W, kFwd[cfg].tw));
 }
@@ -689,10 +692,11 @@ extern "C" int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream) {
     a.Cout = p->Cout;
     hipStream_t st = as_stream(stream);
     if (split) {
-        a.tiles_x = (int)cdiv(p->W, fwd_x6_tile_w(p->W));
-        a.tiles_y = (int)cdiv(p->H, fwd_x6_tile_h(p->W));
+        const int np = p->wfmt == UGPG_WFMT_X6 ? 3 : 1;
+        a.tiles_x = (int)cdiv(p->W, fwd_x6_tile_w(p->W, np));
+        a.tiles_y = (int)cdiv(p->H, fwd_x6_tile_h(p->W, np));
         a.ntiles = p->B * a.tiles_x * a.tiles_y;
-        launch_fwd_x6(a, p->wfmt == UGPG_WFMT_X6 ? 3 : 1, st);
+        launch_fwd_x6(a, np, st);
         return check_launch("conv3x3_fwd_x6");
     }
     const int cfg = pick_fwd_cfg(p->B, p->H, p->W, p->Cout, p->out_split);

@@ -162,9 +162,9 @@ struct WgradArgs {
 // split-bf16 path (conv_x6.hip)
 void launch_fwd_x6(const ConvFwdArgs& a, int np, hipStream_t st);  // np: bf16 pieces (3 or 1)
 extern int g_x6_pipe, g_x6_probe;
-int fwd_x6_tile_w(int W);  // 32 or 16
-int fwd_x6_tile_h(int W);  // 4 or 8
-int fwd_x6_stat_slots(int ntiles, int W);  // BatchNorm partial slots the forward writes
+int fwd_x6_tile_w(int W, int np);  // 32 or 16 (np = bf16 pieces: 3 split, 1 bf16)
+int fwd_x6_tile_h(int W, int np);  // 4, 8 or 16
+int fwd_x6_stat_slots(int ntiles, int W, int np);  // BatchNorm partial slots the forward writes
 void launch_wgrad_x6(const WgradArgs& a, unsigned grid, int np, hipStream_t st);
 extern int g_x6_wgrad;  // tuning knob "x6_wgrad"
 // split plan of the persistent split-bf16 wgrad (deterministic: planned for `cus` CUs)

@@ -454,7 +454,10 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
 template <int TH, int TW>
 __device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a, f32x4 (&acc)[8][2], int tile,
                                                   int b, int ty0, int tx0, int n0, int wm, int wn) {
-    static_assert(TW == 32 && TH == 8, "8 x 32 tile, 4 rows per wave");
+    static_assert(TH * TW == 256 && (TW == 32 || TW == 16), "256-pixel tiles");
+    constexpr int WR = TH / 2;  // image rows of one wave
+    auto prow = [](int mt) { return TW == 32 ? mt >> 1 : mt; };
+    auto pcol = [](int mt) { return TW == 32 ? (mt & 1) * 16 : 0; };
     const int lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
     const int vh = min(TH, a.H - ty0), vw = min(TW, a.W - tx0);
     float* out;
@@ -486,7 +489,7 @@ __device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a, f32x4 (&
         constexpr bool ACC = decltype(accumulate)::value;
 #pragma unroll
         for (int mt = 0; mt < 8; ++mt) {
-            const int py = wm * 4 + (mt >> 1), px = (mt & 1) * 16 + l16;
+            const int py = wm * WR + prow(mt), px = pcol(mt) + l16;
             if (py >= vh) break;  // uniform
             const bool ok = px < vw;
             float* p = out + (size_t)((b * a.H + ty0 + py) * a.W + tx0 + px) * ostride + ocol0 + c0;
@@ -518,7 +521,7 @@ __device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a, f32x4 (&
 #ifdef X6Q_NOSTATS
     return;
 #endif
-    const int rows = min(max(vh - wm * 4, 0), 4);
+    const int rows = min(max(vh - wm * WR, 0), WR);
     const float cnt = (float)(rows * vw);
     f32x4 mu[2], q[2];
 #pragma unroll
@@ -532,8 +535,8 @@ __device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a, f32x4 (&
     }
 #pragma unroll
     for (int mt = 0; mt < 8; ++mt) {
-        if (wm * 4 + (mt >> 1) >= vh) break;  // uniform
-        if ((mt & 1) * 16 + l16 < vw) {
+        if (wm * WR + prow(mt) >= vh) break;  // uniform
+        if (pcol(mt) + l16 < vw) {
 #pragma unroll
             for (int nt = 0; nt < 2; ++nt) {
 #pragma unroll
@@ -602,12 +605,14 @@ extern "C" int ugpg_debug_clock(double* mhz) {
     return n;
 }
 #endif
-template <int NP, bool M16>
+template <int NP, bool M16, int TWT = 32>
 __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) {
     static_assert(!M16 || NP == 3, "the 16x16x32 form pairs the split-bf16 products");
-    constexpr int TH = 8, TW = 32, BN = 64, BKC = 16, MT = 4;
+    static_assert(TWT == 32 || (M16 && TWT == 16), "16-wide tiles only in the 16x16x32 form");
+    // 256-pixel items: 8 x 32 (images >= 32 wide) or 16 x 16 (16-31 wide, 16x16x32 form)
+    constexpr int TW = TWT, TH = 256 / TWT, BN = 64, BKC = 16, MT = 4;
     constexpr int HWD = TW + 2, HS = HWD;
-    constexpr int NHALO = (TH + 2) * HWD;                   // 340 halo pixels
+    constexpr int NHALO = (TH + 2) * HWD;                   // 340 / 324 halo pixels
     // spare slot NHALO; plane pitch 348 = 4 (mod 8) for the 32x32 fragment pattern, 352
     // = 0 (mod 16) for the 16x16 one (ds_read_b128 lane groups, MI355X_MICROARCH.md §LDS)
     constexpr int NHP = M16 ? (NHALO + 1 + 15) / 16 * 16 : NHALO + 1 + (11 - NHALO % 8) % 8;
@@ -867,8 +872,10 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
         // accumulators; the next unit's A fragments and, spread over the tap, the next
         // tap's six W fragments are read while it runs.
         const int g = lane >> 4, l16 = lane & 15;
-        const int a01 = g * NHP + wm * 4 * HS + l16;
-        const int a02 = ((g >> 1) * 4 + (g & 1)) * NHP + wm * 4 * HS + l16;
+        // m-tile mt of a wave = 16 pixels: row mt/2, columns 16(mt&1).. (8 x 32 tiles) or
+        // row mt (16 x 16 tiles); a wave covers TH/2 image rows
+        const int a01 = g * NHP + wm * (TH / 2) * HS + l16;
+        const int a02 = ((g >> 1) * 4 + (g & 1)) * NHP + wm * (TH / 2) * HS + l16;
         const int bo = (g & 1) * 3 * BN + wn * 32 + l16;
         const int wq[3] = {bo + 4 * 3 * BN * (g < 2 ? 1 : 0), bo + 2 * 3 * BN, bo};  // W20, W11, W00
         f32x4 acc[8][2];
@@ -884,11 +891,12 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
         u32x4 fa[DA + 1][2][2];  // [unit % (DA+1)][m-tile of the pair][A02, A01]
         u32x4 fw[3][3][2];     // [tap % 3 (9 taps per step)][W20, W11, W00][nt]
         auto lda = [&](const u32x4* As, int t, int r, u32x4 (&f)[2][2]) {
-            const int ky = t / 3, kx = t % 3, o = (r + ky) * HS + kx;
+            const int ky = t / 3, kx = t % 3;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                f[h][0] = As[a02 + o + 16 * h];
-                f[h][1] = As[a01 + o + 16 * h];
+                const int o = TW == 32 ? (r + ky) * HS + kx + 16 * h : (2 * r + h + ky) * HS + kx;
+                f[h][0] = As[a02 + o];
+                f[h][1] = As[a01 + o];
             }
         };
         auto ldw = [&](const u32x4* Bs, int kx, int e, u32x4 (&f)[3][2]) {
@@ -1643,25 +1651,38 @@ __global__ void pack_x6_kernel(const float* w, __bf16* wpk, int Cout, int Cin, i
 }
 
 int g_x6_pipe = 2;   // tuning knob "x6_pipe" (see launch_fwd_x6)
-static bool use_x6r(int W) { return g_x6_pipe && W >= 32; }
-int fwd_x6_tile_w(int W) { return W >= 32 ? 32 : 16; }
-int fwd_x6_tile_h(int W) { return use_x6r(W) ? 8 : (W >= 32 ? 4 : 8); }
-int fwd_x6_stat_slots(int ntiles, int W) { return use_x6r(W) ? 2 * ntiles : ntiles; }
+// persistent form for this image width / piece count: 8x32 items for W >= 32; with
+// x6_pipe = 3 also 16x16 items for 16 <= W < 32 (16x16x32 split-bf16 form only).  Not
+// the default: at bs16 the 16-wide layers have 64-128 such items for 256 CUs and the
+// single-stage kernel's 128-pixel tiles fill the chip better (0.120 vs 0.124 ms,
+// down4 of S4).
+static bool use_x6r(int W, int np) {
+    return g_x6_pipe && (W >= 32 || (g_x6_pipe == 3 && np == 3 && W >= 16));
+}
+int fwd_x6_tile_w(int W, int np) { return W >= 32 ? 32 : 16; }
+int fwd_x6_tile_h(int W, int np) {
+    return use_x6r(W, np) ? (W >= 32 ? 8 : 16) : (W >= 32 ? 4 : 8);
+}
+int fwd_x6_stat_slots(int ntiles, int W, int np) { return use_x6r(W, np) ? 2 * ntiles : ntiles; }
 
 // tuning knob "x6_pipe": conv3x3_fwd_x6r_kernel for images >= 32 wide with 16x16x32
-// tiles (2, default) or 32x32x16 tiles (1); 0 = conv3x3_fwd_x6_kernel everywhere
+// tiles (2, default) or 32x32x16 tiles (1); 3 = as 2 plus 16x16-pixel items for images
+// 16-31 wide; 0 = conv3x3_fwd_x6_kernel everywhere
 int g_x6_probe = 0;  // "x6_probe": timing diagnostics (see ugpg_set_tuning)
 
 void launch_fwd_x6(const ConvFwdArgs& a_in, int np, hipStream_t st) {
     ConvFwdArgs a = a_in;
     a.probe = g_x6_probe;
     const int64_t items = (int64_t)a.ntiles * (a.Cout / 64);
-    if (use_x6r(a.W)) {
+    if (use_x6r(a.W, np)) {
         // persistent: one workgroup per CU (a multiple of 8: blockIdx % 8 = XCD), each
         // walking a strided share of its XCD's contiguous item range
         int64_t g = std::min<int64_t>(cu_count(st), (items + 7) / 8 * 8);
         g = std::max<int64_t>(8, g / 8 * 8);
-        if (np == 3 && g_x6_pipe == 2)
+        if (np == 3 && g_x6_pipe >= 2 && a.W < 32)
+            hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<3, true, 16>), dim3((unsigned)g), dim3(512),
+                               0, st, a);
+        else if (np == 3 && g_x6_pipe >= 2)
             hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<3, true>), dim3((unsigned)g), dim3(512), 0,
                                st, a);
         else if (np == 3)
@@ -1673,7 +1694,7 @@ void launch_fwd_x6(const ConvFwdArgs& a_in, int np, hipStream_t st) {
         return;
     }
     const unsigned grid = (unsigned)items;
-    const bool wide = fwd_x6_tile_w(a.W) == 32;
+    const bool wide = fwd_x6_tile_w(a.W, np) == 32;
     if (np == 3) {
         if (wide)
             hipLaunchKernelGGL((conv3x3_fwd_x6_kernel<4, 32, false, 3>), dim3(grid), dim3(256), 0, st, a);
