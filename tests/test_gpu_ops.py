@@ -110,17 +110,18 @@ def test_conv3x3_fwd_stats(dev, case, math):
     inp = act_ref(x0, sc0, sh0)
     if C1:
         inp = torch.cat([inp, act_ref(x1, sc1, sh1) if affine else x1], 1)
-    half = math == "bf16" and cin % 16 == 0  # runs in bf16 arithmetic
+    kp = ops.conv_pack_k(cin)  # 8-channel sources: zero-extended to K = 16 (x6 / bf16)
+    half = math == "bf16" and kp % 16 == 0  # runs in bf16 arithmetic
     ref = F.conv2d(bq(inp, half).double(), bq(w, half).double(), b.double(), padding=1)
 
     g = lambda t: None if t is None else t.to(dev)
     srcs = [ops.Act(nhwc(x0).to(dev), g(sc0), g(sh0))]
     if C1:
         srcs.append(ops.Act(nhwc(x1).to(dev), g(sc1), g(sh1)))
-    wpk = ops.pack_conv3x3(w.to(dev), cin, 0)
+    wpk = ops.pack_conv3x3(w.to(dev), kp, 0)
     out = torch.empty(B, H, W, Cout, device=dev)
     fmt = {"f32": ops.WFMT_F32, "bf16": ops.WFMT_BF16}.get(math, ops.WFMT_X6)
-    assert wpk.ugpg_fmt == (fmt if cin % 16 == 0 else ops.WFMT_F32)
+    assert wpk.ugpg_fmt == (fmt if kp % 16 == 0 else ops.WFMT_F32)
     nt = ops.conv_ntiles(B, H, W, cin, Cout, wpk)
     stats = torch.empty(3 * Cout * nt, device=dev)
     ops.conv3x3_fwd(srcs, wpk, b.to(dev), Cout, [out], stats=stats)

@@ -663,7 +663,10 @@ extern "C" int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream) {
         set_error("conv3x3_fwd: unknown weight format %d", p->wfmt);
         return UGPG_ERR_INVALID;
     }
-    if (split && (C0 % 16 || C1 % 16)) {
+    // an 8-channel single source (the padded image) is zero-extended to one 16-channel
+    // chunk: the weights must then be packed with K = 16 (ugpg_pack_conv3x3 cin_pad 16)
+    const bool ext8 = split && C0 == 8 && C1 == 0;
+    if (split && !ext8 && (C0 % 16 || C1 % 16)) {
         set_error("conv3x3_fwd: split-bf16 path needs 16-channel sources (C0=%d C1=%d)", C0, C1);
         return UGPG_ERR_INVALID;
     }
@@ -688,7 +691,7 @@ extern "C" int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream) {
     a.B = p->B;
     a.H = p->H;
     a.W = p->W;
-    a.Cin = Cin;
+    a.Cin = ext8 ? 16 : Cin;
     a.Cout = p->Cout;
     hipStream_t st = as_stream(stream);
     if (split) {

@@ -208,10 +208,13 @@ __global__ void __launch_bounds__(256) conv3x3_fwd_x6_kernel(ConvFwdArgs a) {
             Cs = a.C1;
             cb -= a.C0;
         }
-        // this thread's channel half is fixed (hh = idx & 1 = tid & 1)
+        // this thread's channel half is fixed (hh = idx & 1 = tid & 1); an 8-channel
+        // source is zero-extended to the 16-channel chunk (upper half never read)
+        const bool cok = cb + (tid & 1) * 8 < Cs;
+        const int ch = cb + (cok ? (tid & 1) * 8 : 0);
         aon = sc != nullptr;
-        ract0 = act_load4(sc, sh, cb + (tid & 1) * 8);
-        ract1 = act_load4(sc, sh, cb + (tid & 1) * 8 + 4);
+        ract0 = act_load4(sc, sh, ch);
+        ract1 = act_load4(sc, sh, ch + 4);
         avalid = 0;
         // branch-free: every lane loads from a clamped (valid) address and the halo
         // mask is applied at LDS-store time, so no loaded register is merged at a
@@ -219,11 +222,11 @@ __global__ void __launch_bounds__(256) conv3x3_fwd_x6_kernel(ConvFwdArgs a) {
 #pragma unroll
         for (int v = 0; v < A_PER; ++v) {
             const int idx = tid + v * 256;
-            const int hp = idx < A_ITEMS ? idx >> 1 : 0, hh = tid & 1;
+            const int hp = idx < A_ITEMS ? idx >> 1 : 0;
             const int gy = ty0 - 1 + hp / HWD, gx = tx0 - 1 + hp % HWD;
-            const bool ok = idx < A_ITEMS && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
+            const bool ok = cok && idx < A_ITEMS && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
             const int cy = min(max(gy, 0), a.H - 1), cx = min(max(gx, 0), a.W - 1);
-            const float* p = src + ((size_t)(b * a.H + cy) * a.W + cx) * Cs + cb + hh * 8;
+            const float* p = src + ((size_t)(b * a.H + cy) * a.W + cx) * Cs + ch;
             ra[v][0] = *reinterpret_cast<const f32x4*>(p);
             ra[v][1] = *reinterpret_cast<const f32x4*>(p + 4);
             avalid |= (ok ? 1u : 0u) << v;
@@ -716,7 +719,9 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
             const float* scp = aon ? sc : g_act_ones;  // identity coefficients without activation
             const float* shp = aon ? sh : g_act_zeros;
             lo[st] = aon ? 0.f : -INFINITY;
-            const int cc = cb + (lt & 1) * 8;
+            // an 8-channel source is zero-extended to the 16-channel chunk
+            const bool cok = cb + (lt & 1) * 8 < Cs;
+            const int cc = cb + (cok ? (lt & 1) * 8 : 0);
             r0[st].s = gld16(scp + cc);
             r0[st].h = gld16(shp + cc);
             r1[st].s = gld16(scp + cc + 4);
@@ -724,11 +729,10 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
             unsigned av = 0;
 #pragma unroll
             for (int v = 0; v < A_PER; ++v) {
-                const int hh = lt & 1;
                 const int gy = p.ty0 - 1 + hy[v], gx = p.tx0 - 1 + hx[v];
-                const bool ok = gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
+                const bool ok = cok && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
                 const int cy = min(max(gy, 0), a.H - 1), cx = min(max(gx, 0), a.W - 1);
-                const float* gp = src + ((size_t)(p.b * a.H + cy) * a.W + cx) * Cs + cb + hh * 8;
+                const float* gp = src + ((size_t)(p.b * a.H + cy) * a.W + cx) * Cs + cc;
                 ra[st][v][0] = gld16(gp);
                 ra[st][v][1] = gld16(gp + 4);
                 av |= (ok ? 1u : 0u) << v;

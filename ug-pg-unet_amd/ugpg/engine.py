@@ -68,7 +68,7 @@ def double_conv_forward(mod, srcs, ctx: BlockCtx, save: bool):
         cout = w.shape[0]
         if w.shape[1] > cin:
             raise ValueError(f"conv expects {w.shape[1]} input channels, got {cin}")
-        wpk = ops.pack_conv3x3(w.detach(), cin, 0)
+        wpk = ops.pack_conv3x3(w.detach(), ops.conv_pack_k(cin), 0)
         y = ops.empty(B, H, W, cout, like=srcs[0].y)
         train = _bn_mode(bn)
         stats = None

@@ -115,6 +115,15 @@ def conv_weight_format(n: int, k: int) -> int:
     return fmt if n % 64 == 0 and k % 16 == 0 else WFMT_F32
 
 
+def conv_pack_k(cin: int) -> int:
+    """K the forward weights are packed with for `cin` source channels: an 8-channel
+    source (the padded image) is zero-extended by the split-bf16 kernels to one
+    16-channel chunk, so under math x6 its weights are packed with K = 16 (fp32-class
+    like every x6 conv).  Math bf16 keeps the image layer in fp32 (its weight gradient
+    is the fp32 narrow-input kernel; §3b)."""
+    return 16 if cin == 8 and _conv_math == "x6" else cin
+
+
 def pack_conv3x3(w, cin_pad: int, mode: int) -> torch.Tensor:
     """Repack OIHW weights for conv3x3_fwd (mode 0) or its data gradient (mode 1).
     The result carries its pack format in ``.ugpg_fmt``."""
