@@ -271,10 +271,12 @@ def test_maxpool(dev):
     close(nchw(din.cpu()) - 1.0, a.grad, 1e-6, "maxpool bwd")
 
 
-@pytest.mark.parametrize("hi,wi,ho,wo", [(16, 16, 32, 32), (8, 8, 16, 16), (7, 5, 13, 11), (32, 32, 16, 16)])
-def test_bilinear_nhwc(dev, hi, wi, ho, wo):
+@pytest.mark.parametrize("hi,wi,ho,wo,C", [(16, 16, 32, 32, 64), (8, 8, 16, 16, 64), (7, 5, 13, 11, 64),
+                                            (32, 32, 16, 16, 64), (64, 64, 128, 128, 128),
+                                            (9, 11, 18, 22, 96), (16, 16, 32, 32, 1024)])
+def test_bilinear_nhwc(dev, hi, wi, ho, wo, C):
     from ugpg import ops
-    B, C = 2, 64
+    B = 2
     y = rnd((B, C, hi, wi), 40, "y")
     sc, sh = rnd((C,), 41, "s", 0.5) + 1, rnd((C,), 42, "h", 0.3)
     # fp32 reference: ATen derives the align_corners weights in fp32 (fp64 rounds differently)

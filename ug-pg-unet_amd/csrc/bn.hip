@@ -100,9 +100,7 @@ __global__ void __launch_bounds__(256)
         const f32x4 sc = *reinterpret_cast<const f32x4*>(scale + c);
         const f32x4 sh = *reinterpret_cast<const f32x4*>(shift + c);
         const int64_t p0 = blockIdx.x * ppb, p1 = min(npix, p0 + ppb);
-        for (int64_t p = p0 + slot; p < p1; p += slots) {
-            const f32x4 d = *reinterpret_cast<const f32x4*>(da + p * C + c);
-            const f32x4 v = *reinterpret_cast<const f32x4*>(y + p * C + c);
+        auto accum = [&](f32x4 d, f32x4 v) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const float g = fmaf(v[k], sc[k], sh[k]) > 0.f ? d[k] : 0.f;
@@ -111,7 +109,23 @@ __global__ void __launch_bounds__(256)
                 sgx[k] = fmaf(g, xh, sgx[k]);
                 sx[k] += xh;
             }
+        };
+        // four pixels' loads in flight per thread before any is consumed (the loop
+        // was latency-bound at one pair of 16-byte loads per thread: 4.7 TB/s)
+        int64_t p = p0 + slot;
+        for (; p + 3 * slots < p1; p += 4 * slots) {
+            f32x4 d[4], v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                d[u] = *reinterpret_cast<const f32x4*>(da + (p + u * slots) * C + c);
+                v[u] = *reinterpret_cast<const f32x4*>(y + (p + u * slots) * C + c);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) accum(d[u], v[u]);
         }
+        for (; p < p1; p += slots)
+            accum(*reinterpret_cast<const f32x4*>(da + p * C + c),
+                  *reinterpret_cast<const f32x4*>(y + p * C + c));
     }
     rs[tid] = sg;
     rq[tid] = sgx;
@@ -175,18 +189,21 @@ __global__ void bn_bwd_apply_kernel(const float* da, const float* __restrict__ y
                                     const float* scale, const float* shift, const float* coef,
                                     float* dy) {
     const int64_t n4 = npix * C / 4;
+    auto ld4 = [](const float* p, int c) { return *reinterpret_cast<const f32x4*>(p + c); };
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
          i += (int64_t)gridDim.x * blockDim.x) {
         const int c = (int)((i * 4) % C);
         const f32x4 d = reinterpret_cast<const f32x4*>(da)[i];
         const f32x4 v = reinterpret_cast<const f32x4*>(y)[i];
+        // per-channel parameters as 16-byte loads (C % 4 == 0, 16-byte aligned arrays)
+        const f32x4 sc = ld4(scale, c), sh = ld4(shift, c), mu = ld4(mean, c),
+                    is = ld4(invstd, c), k0 = ld4(coef, c), k1 = ld4(coef, C + c);
         f32x4 o;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int cc = c + k;
-            const float g = fmaf(v[k], scale[cc], shift[cc]) > 0.f ? d[k] : 0.f;
-            const float xh = (v[k] - mean[cc]) * invstd[cc];
-            o[k] = (g - coef[cc] - xh * coef[C + cc]) * scale[cc];
+            const float g = fmaf(v[k], sc[k], sh[k]) > 0.f ? d[k] : 0.f;
+            const float xh = (v[k] - mu[k]) * is[k];
+            o[k] = (g - k0[k] - xh * k1[k]) * sc[k];
         }
         reinterpret_cast<f32x4*>(dy)[i] = o;
     }

@@ -8,6 +8,8 @@
 //   RMSprop               uncertainty_guided_trainer.py:84-88  (K15)
 //   avgpool/Linear head   Herlev/train_herlev.py:66-77         (K16)
 // All reductions are deterministic (fixed-order block partials, fp64 merge).
+#include <algorithm>
+
 #include "common.h"
 
 namespace ugpg {
@@ -108,58 +110,84 @@ __device__ __forceinline__ float ac_weight(int o, int i, int in, int out) {
     return w;
 }
 
+// Row-blocked forms: blockIdx.y = output (input) row, so the row's interpolation
+// indices/weights and the 64-bit image offsets are computed once per thread, and a
+// thread keeps one channel quad (the x-stride is a multiple of C/4), loading the lazy
+// BatchNorm coefficients once.  Same arithmetic, same order as the flat forms.
 __global__ void bilinear_nhwc_fwd_kernel(const float* x, const float* sc, const float* sh, int B,
                                          int Hi, int Wi, int C, float* out, int Ho, int Wo) {
     const int C4 = C / 4;
-    const int64_t total = (int64_t)B * Ho * Wo * C4;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const int c = (int)(i % C4) * 4;
-        int64_t r = i / C4;
-        const int ox = (int)(r % Wo);
-        r /= Wo;
-        const int oy = (int)(r % Ho), b = (int)(r / Ho);
-        int y0, y1, x0, x1;
-        float ly0, ly1, lx0, lx1;
-        ac_index(oy, Hi, Ho, y0, y1, ly0, ly1);
+    const int row = blockIdx.y;  // b * Ho + oy
+    const int b = row / Ho, oy = row % Ho;
+    int y0, y1, x0, x1;
+    float ly0, ly1, lx0, lx1;
+    ac_index(oy, Hi, Ho, y0, y1, ly0, ly1);
+    const float* r0 = x + ((size_t)b * Hi + y0) * Wi * C;
+    const float* r1 = x + ((size_t)b * Hi + y1) * Wi * C;
+    float* orow = out + (size_t)row * Wo * C;
+    const int n = Wo * C4, stride = gridDim.x * blockDim.x;
+    const bool fixed_c = stride % C4 == 0;  // then a thread keeps its channel quad
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    int c = (t % C4) * 4;
+    f32x4 s4 = {1.f, 1.f, 1.f, 1.f}, h4 = {0.f, 0.f, 0.f, 0.f};
+    auto coef = [&]() {
+        if (sc) {
+            s4 = *reinterpret_cast<const f32x4*>(sc + c);
+            h4 = *reinterpret_cast<const f32x4*>(sh + c);
+        }
+    };
+    coef();
+    auto act = [&](f32x4 v) {
+        if (sc) {
+            v.x = fmaxf(fmaf(v.x, s4.x, h4.x), 0.0f);
+            v.y = fmaxf(fmaf(v.y, s4.y, h4.y), 0.0f);
+            v.z = fmaxf(fmaf(v.z, s4.z, h4.z), 0.0f);
+            v.w = fmaxf(fmaf(v.w, s4.w, h4.w), 0.0f);
+        }
+        return v;
+    };
+    for (; t < n; t += stride) {
+        if (!fixed_c) {
+            c = (t % C4) * 4;
+            coef();
+        }
+        const int ox = t / C4;
         ac_index(ox, Wi, Wo, x0, x1, lx0, lx1);
-        const float* base = x + (size_t)b * Hi * Wi * C + c;
-        const f32x4 a00 = act_apply4(*reinterpret_cast<const f32x4*>(base + ((size_t)y0 * Wi + x0) * C), sc, sh, c);
-        const f32x4 a01 = act_apply4(*reinterpret_cast<const f32x4*>(base + ((size_t)y0 * Wi + x1) * C), sc, sh, c);
-        const f32x4 a10 = act_apply4(*reinterpret_cast<const f32x4*>(base + ((size_t)y1 * Wi + x0) * C), sc, sh, c);
-        const f32x4 a11 = act_apply4(*reinterpret_cast<const f32x4*>(base + ((size_t)y1 * Wi + x1) * C), sc, sh, c);
+        const f32x4 a00 = act(*reinterpret_cast<const f32x4*>(r0 + (size_t)x0 * C + c));
+        const f32x4 a01 = act(*reinterpret_cast<const f32x4*>(r0 + (size_t)x1 * C + c));
+        const f32x4 a10 = act(*reinterpret_cast<const f32x4*>(r1 + (size_t)x0 * C + c));
+        const f32x4 a11 = act(*reinterpret_cast<const f32x4*>(r1 + (size_t)x1 * C + c));
         const f32x4 v = ly0 * (lx0 * a00 + lx1 * a01) + ly1 * (lx0 * a10 + lx1 * a11);
-        *reinterpret_cast<f32x4*>(out + i * 4) = v;
+        *reinterpret_cast<f32x4*>(orow + (size_t)ox * C + c) = v;
     }
 }
 
 __global__ void bilinear_nhwc_bwd_kernel(const float* dout, int B, int Ho, int Wo, int C,
                                          float* din, int Hi, int Wi, int acc) {
     const int C4 = C / 4;
-    const int64_t total = (int64_t)B * Hi * Wi * C4;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const int c = (int)(i % C4) * 4;
-        int64_t r = i / C4;
-        const int ix = (int)(r % Wi);
-        r /= Wi;
-        const int iy = (int)(r % Hi), b = (int)(r / Hi);
-        int ylo, yhi, xlo, xhi;
-        ac_range(iy, Hi, Ho, ylo, yhi);
+    const int row = blockIdx.y;  // b * Hi + iy
+    const int b = row / Hi, iy = row % Hi;
+    int ylo, yhi;
+    ac_range(iy, Hi, Ho, ylo, yhi);
+    const int n = Wi * C4, stride = gridDim.x * blockDim.x;
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += stride) {
+        const int c = (t % C4) * 4, ix = t / C4;
+        int xlo, xhi;
         ac_range(ix, Wi, Wo, xlo, xhi);
         f32x4 s = {0.f, 0.f, 0.f, 0.f};
         for (int oy = ylo; oy <= yhi; ++oy) {
-            const float wy = ac_weight(oy, iy, Hi, Ho);
-            if (wy == 0.f) continue;
+            const float wyk = ac_weight(oy, iy, Hi, Ho);
+            if (wyk == 0.f) continue;
             for (int ox = xlo; ox <= xhi; ++ox) {
                 const float wx = ac_weight(ox, ix, Wi, Wo);
                 if (wx == 0.f) continue;
                 const f32x4 d = *reinterpret_cast<const f32x4*>(
                     dout + ((size_t)(b * Ho + oy) * Wo + ox) * C + c);
-                s += (wy * wx) * d;
+                s += (wyk * wx) * d;
             }
         }
-        f32x4* dst = reinterpret_cast<f32x4*>(din + i * 4);
+        f32x4* dst = reinterpret_cast<f32x4*>(din + ((size_t)row * Wi + ix) * C + c);
         if (acc) s += *dst;
         *dst = s;
     }
@@ -332,27 +360,40 @@ __global__ void head_split_bwd_kernel(const float* dl, int B, int H, int W, int 
     }
 }
 
-// da (+)= dh @ w ; per-block partials of dW = dh^T act and db = sum dh
+// da (+)= dh @ w ; per-block partials of dW = dh^T act and db = sum dh.  Compile-time
+// class count NC and 64-channel slices CJ keep the accumulators in registers (runtime
+// bounds put them in scratch); two pixels per iteration keep 2x the loads in flight.
+template <int NC, int CJ>
 __global__ void __launch_bounds__(256) head_bwd_kernel(const float* x, const float* sc,
                                                        const float* sh, int64_t npix, int C,
                                                        const float* w, int nc, const float* dh,
                                                        float* da, int acc_da, int64_t ppb,
                                                        float* part, int nblk) {
-    const int tid = threadIdx.x, l16 = tid & 15, slot = tid >> 4, CJ = C / 64;
-    f32x4 gw[HEAD_NC_MAX][HEAD_CJ_MAX];
-    float gb[HEAD_NC_MAX] = {0.f, 0.f, 0.f, 0.f};
-    for (int k = 0; k < HEAD_NC_MAX; ++k)
-        for (int j = 0; j < HEAD_CJ_MAX; ++j) gw[k][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int tid = threadIdx.x, l16 = tid & 15, slot = tid >> 4;
+    f32x4 gw[NC][CJ];
+    float gb[NC];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+        gb[k] = 0.f;
+#pragma unroll
+        for (int j = 0; j < CJ; ++j) gw[k][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    f32x4 wk[NC][CJ];
+#pragma unroll
+    for (int k = 0; k < NC; ++k)
+#pragma unroll
+        for (int j = 0; j < CJ; ++j)
+            wk[k][j] = *reinterpret_cast<const f32x4*>(w + (size_t)k * C + l16 * 4 + 64 * j);
     const int64_t p0 = blockIdx.x * ppb, p1 = min(npix, p0 + ppb);
-    for (int64_t p = p0 + slot; p < p1; p += 16) {
-        float d[HEAD_NC_MAX];
-        for (int k = 0; k < nc; ++k) d[k] = dh[p * nc + k];
+    auto pixel = [&](int64_t p, const float (&d)[NC], const f32x4 (&xv)[CJ]) {
+#pragma unroll
         for (int j = 0; j < CJ; ++j) {
             const int c = l16 * 4 + 64 * j;
-            const f32x4 v = act_apply4(*reinterpret_cast<const f32x4*>(x + p * C + c), sc, sh, c);
+            const f32x4 v = act_apply4(xv[j], sc, sh, c);
             f32x4 g = {0.f, 0.f, 0.f, 0.f};
-            for (int k = 0; k < nc; ++k) {
-                g += d[k] * *reinterpret_cast<const f32x4*>(w + (size_t)k * C + c);
+#pragma unroll
+            for (int k = 0; k < NC; ++k) {
+                g += d[k] * wk[k][j];
                 gw[k][j] += d[k] * v;
             }
             f32x4* dst = reinterpret_cast<f32x4*>(da + p * C + c);
@@ -360,11 +401,41 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(const float* x, const flo
             *dst = g;
         }
         if (l16 == 0)
-            for (int k = 0; k < nc; ++k) gb[k] += d[k];
+#pragma unroll
+            for (int k = 0; k < NC; ++k) gb[k] += d[k];
+    };
+    int64_t p = p0 + slot;
+    for (; p + 16 < p1; p += 32) {
+        float d0[NC], d1[NC];
+        f32x4 x0[CJ], x1[CJ];
+#pragma unroll
+        for (int k = 0; k < NC; ++k) {
+            d0[k] = dh[p * NC + k];
+            d1[k] = dh[(p + 16) * NC + k];
+        }
+#pragma unroll
+        for (int j = 0; j < CJ; ++j) {
+            x0[j] = *reinterpret_cast<const f32x4*>(x + p * C + l16 * 4 + 64 * j);
+            x1[j] = *reinterpret_cast<const f32x4*>(x + (p + 16) * C + l16 * 4 + 64 * j);
+        }
+        pixel(p, d0, x0);
+        pixel(p + 16, d1, x1);
+    }
+    for (; p < p1; p += 16) {
+        float d0[NC];
+        f32x4 x0[CJ];
+#pragma unroll
+        for (int k = 0; k < NC; ++k) d0[k] = dh[p * NC + k];
+#pragma unroll
+        for (int j = 0; j < CJ; ++j)
+            x0[j] = *reinterpret_cast<const f32x4*>(x + p * C + l16 * 4 + 64 * j);
+        pixel(p, d0, x0);
     }
     __shared__ f32x4 red[256];
     __shared__ float redb[16];
-    for (int k = 0; k < nc; ++k) {
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+#pragma unroll
         for (int j = 0; j < CJ; ++j) {
             red[tid] = gw[k][j];
             if (l16 == 0) redb[slot] = gb[k];
@@ -372,7 +443,7 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(const float* x, const flo
             if (slot == 0) {
                 f32x4 s = red[l16];
                 for (int q = 1; q < 16; ++q) s += red[q * 16 + l16];
-                float* dst = part + ((size_t)blockIdx.x * nc + k) * (C + 1) + l16 * 4 + 64 * j;
+                float* dst = part + ((size_t)blockIdx.x * NC + k) * (C + 1) + l16 * 4 + 64 * j;
                 dst[0] = s.x;
                 dst[1] = s.y;
                 dst[2] = s.z;
@@ -380,7 +451,7 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(const float* x, const flo
                 if (l16 == 0 && j == 0) {
                     float sb = 0.f;
                     for (int q = 0; q < 16; ++q) sb += redb[q];
-                    part[((size_t)blockIdx.x * nc + k) * (C + 1) + C] = sb;
+                    part[((size_t)blockIdx.x * NC + k) * (C + 1) + C] = sb;
                 }
             }
             __syncthreads();
@@ -896,8 +967,9 @@ extern "C" int ugpg_maxpool2_bwd(const float* dout, const uint8_t* am, int B, in
 extern "C" int ugpg_bilinear_nhwc_fwd(ugpg_src_t s, int B, int Hi, int Wi, float* out, int Ho,
                                       int Wo, void* stream) {
     UGPG_REQUIRE(s.data && out && s.C % 4 == 0 && Ho > 0 && Wo > 0, "bilinear_nhwc_fwd");
-    const int64_t total = (int64_t)B * Ho * Wo * (s.C / 4);
-    hipLaunchKernelGGL(bilinear_nhwc_fwd_kernel, dim3(stream_grid(total)), dim3(256), 0,
+    UGPG_REQUIRE((int64_t)B * Ho < 65536, "bilinear_nhwc_fwd: shape");
+    const unsigned gx = (unsigned)std::min<int64_t>(cdiv((int64_t)Wo * (s.C / 4), 256), 64);
+    hipLaunchKernelGGL(bilinear_nhwc_fwd_kernel, dim3(gx, (unsigned)(B * Ho)), dim3(256), 0,
                        as_stream(stream), s.data, s.scale, s.shift, B, Hi, Wi, s.C, out, Ho, Wo);
     return check_launch("bilinear_nhwc_fwd");
 }
@@ -905,8 +977,9 @@ extern "C" int ugpg_bilinear_nhwc_fwd(ugpg_src_t s, int B, int Hi, int Wi, float
 extern "C" int ugpg_bilinear_nhwc_bwd(const float* dout, int B, int Ho, int Wo, int C, float* din,
                                       int Hi, int Wi, int acc, void* stream) {
     UGPG_REQUIRE(dout && din && C % 4 == 0, "bilinear_nhwc_bwd");
-    const int64_t total = (int64_t)B * Hi * Wi * (C / 4);
-    hipLaunchKernelGGL(bilinear_nhwc_bwd_kernel, dim3(stream_grid(total)), dim3(256), 0,
+    UGPG_REQUIRE((int64_t)B * Hi < 65536, "bilinear_nhwc_bwd: shape");
+    const unsigned gx = (unsigned)std::min<int64_t>(cdiv((int64_t)Wi * (C / 4), 256), 64);
+    hipLaunchKernelGGL(bilinear_nhwc_bwd_kernel, dim3(gx, (unsigned)(B * Hi)), dim3(256), 0,
                        as_stream(stream), dout, B, Ho, Wo, C, din, Hi, Wi, acc);
     return check_launch("bilinear_nhwc_bwd");
 }
@@ -995,8 +1068,16 @@ extern "C" int ugpg_head_bwd(ugpg_src_t s, int64_t npix, const float* w, int nc,
     int64_t ppb;
     const int nblk = head_nblk(npix, ppb);
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(head_bwd_kernel, dim3(nblk), dim3(256), 0, st, s.data, s.scale, s.shift,
-                       npix, s.C, w, nc, dh, da, acc_da, ppb, static_cast<float*>(ws), nblk);
+    using K = void (*)(const float*, const float*, const float*, int64_t, int, const float*, int,
+                       const float*, float*, int, int64_t, float*, int);
+    static const K table[HEAD_NC_MAX][HEAD_CJ_MAX] = {
+        {head_bwd_kernel<1, 1>, head_bwd_kernel<1, 2>, head_bwd_kernel<1, 3>, head_bwd_kernel<1, 4>},
+        {head_bwd_kernel<2, 1>, head_bwd_kernel<2, 2>, head_bwd_kernel<2, 3>, head_bwd_kernel<2, 4>},
+        {head_bwd_kernel<3, 1>, head_bwd_kernel<3, 2>, head_bwd_kernel<3, 3>, head_bwd_kernel<3, 4>},
+        {head_bwd_kernel<4, 1>, head_bwd_kernel<4, 2>, head_bwd_kernel<4, 3>, head_bwd_kernel<4, 4>}};
+    hipLaunchKernelGGL(table[nc - 1][s.C / 64 - 1], dim3(nblk), dim3(256), 0, st, s.data, s.scale,
+                       s.shift, npix, s.C, w, nc, dh, da, acc_da, ppb, static_cast<float*>(ws),
+                       nblk);
     if (int e = check_launch("head_bwd")) return e;
     hipLaunchKernelGGL(head_bwd_finalize_kernel, dim3((unsigned)cdiv(nc * (s.C + 1), 64)), dim3(1024), 0,
                        st, static_cast<const float*>(ws), nblk, nc, s.C, dw, db);
