@@ -16,43 +16,42 @@ __global__ void bn_finalize_kernel(const float* __restrict__ stats, int ntiles, 
                                    float* rvar, int64_t* nbt, float momentum, float eps,
                                    float* mean_o, float* invstd_o, float* scale_o,
                                    float* shift_o) {
-    // Parallel-variance combination of the per-tile partials (count, sum, M2) in two
-    // passes: total count and sum -> mean m; then M2 = sum_t M2_t + (sum_t - n_t m)^2 / n_t
-    // (deviations of the tile means from the global mean, no per-slot division chain)
+    // Parallel-variance combination of the per-tile partials (count, sum, M2) in ONE
+    // pass, shifted by K = the first non-empty tile's mean (close to the global mean, so
+    // no cancellation): with e_t = sum_t - n_t K,  m = K + sum e_t / N  and
+    // M2 = sum M2_t + sum e_t^2 / n_t - (sum e_t)^2 / N.  1024 threads per channel.
     const int c = blockIdx.x;
-    __shared__ double sn[256], sm[256], sq[256];
+    __shared__ double sn[1024], se[1024], sq[1024];
     const float* cnt = stats + (size_t)c * ntiles;
     const float* sum = stats + ((size_t)C + c) * ntiles;
     const float* m2 = stats + ((size_t)2 * C + c) * ntiles;
-    double n = 0, S = 0;
-    for (int t = threadIdx.x; t < ntiles; t += blockDim.x) {
-        n += cnt[t];
-        S += sum[t];
-    }
-    sn[threadIdx.x] = n;
-    sm[threadIdx.x] = S;
-    __syncthreads();
-    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-        if (threadIdx.x < s) {
-            sn[threadIdx.x] += sn[threadIdx.x + s];
-            sm[threadIdx.x] += sm[threadIdx.x + s];
-        }
-        __syncthreads();
-    }
-    const double Ntot = sn[0], mean = Ntot > 0 ? sm[0] / Ntot : 0.0;
-    double M = 0;
+    int t0 = 0;
+    while (t0 < ntiles && !(cnt[t0] > 0.f)) ++t0;  // uniform: the first tile is normally full
+    const double K = t0 < ntiles ? (double)sum[t0] / (double)cnt[t0] : 0.0;
+    double n = 0, E = 0, M = 0;
     for (int t = threadIdx.x; t < ntiles; t += blockDim.x) {
         const float nb = cnt[t];
         if (nb <= 0.f) continue;
-        const double d = (double)sum[t] - (double)nb * mean;
-        M += (double)m2[t] + d * d * (double)(1.0f / nb);
+        const double e = (double)sum[t] - (double)nb * K;
+        n += nb;
+        E += e;
+        M += (double)m2[t] + e * e * (double)(1.0f / nb);
     }
+    sn[threadIdx.x] = n;
+    se[threadIdx.x] = E;
     sq[threadIdx.x] = M;
     __syncthreads();
-    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-        if (threadIdx.x < s) sq[threadIdx.x] += sq[threadIdx.x + s];
+    for (int s2 = blockDim.x / 2; s2 > 0; s2 >>= 1) {
+        if (threadIdx.x < s2) {
+            sn[threadIdx.x] += sn[threadIdx.x + s2];
+            se[threadIdx.x] += se[threadIdx.x + s2];
+            sq[threadIdx.x] += sq[threadIdx.x + s2];
+        }
         __syncthreads();
     }
+    const double Ntot = sn[0];
+    const double mean = Ntot > 0 ? K + se[0] / Ntot : 0.0;
+    if (threadIdx.x == 0 && Ntot > 0) sq[0] -= se[0] * se[0] / Ntot;
     if (threadIdx.x == 0) {
         const double N = Ntot, m = mean;
         const double var = sq[0] / N;
@@ -247,7 +246,7 @@ extern "C" int ugpg_bn_finalize(const float* stats, int ntiles, int C, const flo
         set_error("bn_finalize: bad arguments");
         return UGPG_ERR_INVALID;
     }
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, as_stream(stream), stats,
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(1024), 0, as_stream(stream), stats,
                        ntiles, C, gamma, beta, running_mean, running_var, nbt, momentum, eps,
                        mean, invstd, scale, shift);
     return check_launch("bn_finalize");
