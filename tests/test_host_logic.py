@@ -182,3 +182,40 @@ def test_tester_checkpoint_formats(tmp_path):
     torch.save([1, 2, 3], tmp_path / "c.pth")
     with pytest.raises(RuntimeError, match="Unrecognized checkpoint"):
         ugpg.MoNuSegTester(str(tmp_path / "c.pth"), device="cpu")
+
+
+def test_herlev_progressive_driver_early_stop_and_scheduler(tmp_path, monkeypatch):
+    """train_herlev.py:404-489 control flow with scripted epoch results: the
+    scheduler steps on val_loss (factor 0.5 after 5 bad epochs), a checkpoint is
+    written on each val_acc improvement, early stop after `early_stopping_patience`
+    stale epochs, history JSON with the reference's keys."""
+    from ugpg.herlev import HerlevTrainer
+    cfg = {"device": "cpu", "epochs_per_stage": 12, "num_classes": 7, "stages": [1, 2],
+           "early_stopping_patience": 8}
+    tr = HerlevTrainer(cfg)
+    script = {1: [(1.0, 10.0)] + [(1.0, 5.0)] * 11,             # (val_loss, val_acc)
+              2: [(2.0, 1.0), (1.5, 2.0), (1.0, 3.0)] + [(1.0, 3.0)] * 9}
+    calls = {1: 0, 2: 0}
+
+    def train_epoch(loader, stage):
+        return (0.5, 0.4, 50.0, 0.0, 0.0)
+
+    def validate_epoch(loader, stage):
+        vl, va = script[stage][calls[stage]]
+        calls[stage] += 1
+        return (vl, vl, va, 1.0, 0.0)
+
+    monkeypatch.setattr(tr, "train_epoch", train_epoch)
+    monkeypatch.setattr(tr, "validate_epoch", validate_epoch)
+    tr.train_progressive({1: None, 2: None}, {1: None, 2: None}, str(tmp_path))
+    assert calls == {1: 9, 2: 11}          # best at epoch 1 (3), then 8 stale epochs
+    assert tr.optimizers[1].param_groups[0]["lr"] == pytest.approx(1.5e-4)   # halved once
+    assert tr.optimizers[2].param_groups[0]["lr"] == pytest.approx(5e-5)
+    ck = torch.load(tmp_path / "herlev_stage2_best.pth", weights_only=True)
+    assert ck["epoch"] == 3 and ck["val_acc"] == 3.0 and ck["stage"] == 2
+    assert set(ck) == {"model_state_dict", "optimizer_state_dict", "stage", "epoch",
+                       "train_loss", "val_loss", "train_acc", "val_acc", "config"}
+    h = json.loads((tmp_path / "training_history.json").read_text())
+    assert len(h["val_loss"]) == 20 and h["base_loss"][0] == 1.0
+    assert [t["stage"] for t in h["stage_transitions"]] == [1, 2]
+    assert h["stage_transitions"][0]["best_val_acc"] == 10.0

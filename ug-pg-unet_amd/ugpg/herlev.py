@@ -15,8 +15,10 @@ consumes the global RNG.  ugpg sets the width statically and does not probe.
 """
 from __future__ import annotations
 
+import json
 import math
 import os
+from datetime import datetime
 
 import torch
 import torch.nn as nn
@@ -143,9 +145,9 @@ class HerlevClassificationModel(nn.Module):
 
 
 class HerlevTrainer:
-    """The uncertainty-guided step of HerlevTrainer (train_herlev.py:124-357):
-    stage configs, models, class-weighted criterion, Adam + ReduceLROnPlateau,
-    classifier weight transfer, forward pass, train/validate epochs."""
+    """HerlevTrainer (train_herlev.py:124-489): stage configs, models,
+    class-weighted criterion, Adam + ReduceLROnPlateau, classifier weight transfer,
+    forward pass, train/validate epochs, progressive driver with early stop."""
 
     def __init__(self, config):
         self.config = config
@@ -254,3 +256,66 @@ class HerlevTrainer:
     def validate_epoch(self, dataloader, stage):
         return self._epoch(dataloader, stage, False)
 
+
+    def train_progressive(self, train_loaders, val_loaders, save_dir):
+        """Stage loop of train_herlev.py:404-489: per stage a fresh Adam +
+        ReduceLROnPlateau(min, 0.5, 5) stepped on the validation loss, classifier
+        transfer from the previous stage, a checkpoint whenever validation accuracy
+        improves, early stop after `early_stopping_patience` (15) epochs without one,
+        and the history JSON at the end.  Checkpoints carry the reference's keys."""
+        os.makedirs(save_dir, exist_ok=True)
+        from .dist import world
+        rank, _ = world()
+        for stage in self.config["stages"]:
+            print(f"\n{'=' * 60}")
+            print(f"Training Stage {stage} - Resolution: {self.stage_configs[stage]['resolution']}")
+            print(f"{'=' * 60}")
+            self.current_stage = stage
+            self.setup_optimizer_scheduler(stage)
+            if stage > 1 and (stage - 1) in self.models:
+                self.transfer_weights(stage - 1, stage)
+            train_loader, val_loader = train_loaders[stage], val_loaders[stage]
+            best_val_loss, best_val_acc, stale = float("inf"), 0, 0
+            for epoch in range(self.stage_configs[stage]["epochs"]):
+                print(f"\nStage {stage}, Epoch {epoch + 1}/{self.stage_configs[stage]['epochs']}")
+                tr_loss, tr_base, tr_acc, tr_um, tr_us = self.train_epoch(train_loader, stage)
+                va_loss, va_base, va_acc, va_um, va_us = self.validate_epoch(val_loader, stage)
+                self.schedulers[stage].step(va_loss)
+                h = self.history
+                h["train_loss"].append(tr_loss)
+                h["val_loss"].append(va_loss)
+                h["train_acc"].append(tr_acc)
+                h["val_acc"].append(va_acc)
+                h["uncertainty_weights_mean"].append(va_um)
+                h["uncertainty_weights_std"].append(va_us)
+                h["base_loss"].append(va_base)
+                print(f"Train Loss: {tr_loss:.4f}, Base Loss: {tr_base:.4f}, Train Acc: {tr_acc:.2f}%")
+                print(f"Val Loss: {va_loss:.4f}, Base Loss: {va_base:.4f}, Val Acc: {va_acc:.2f}%")
+                if stage > 1:
+                    print(f"Train Uncertainty - Mean: {tr_um:.4f}, Std: {tr_us:.4f}")
+                    print(f"Val Uncertainty - Mean: {va_um:.4f}, Std: {va_us:.4f}")
+                if va_acc > best_val_acc:
+                    best_val_loss, best_val_acc, stale = va_loss, va_acc, 0
+                    if rank == 0:
+                        torch.save({"model_state_dict": self.models[stage].state_dict(),
+                                    "optimizer_state_dict": self.optimizers[stage].state_dict(),
+                                    "stage": stage, "epoch": epoch + 1,
+                                    "train_loss": tr_loss, "val_loss": va_loss,
+                                    "train_acc": tr_acc, "val_acc": va_acc,
+                                    "config": self.config},
+                                   os.path.join(save_dir, f"herlev_stage{stage}_best.pth"))
+                    print(f"New best model saved! Val Acc: {va_acc:.2f}%")
+                else:
+                    stale += 1
+                if stale >= self.config.get("early_stopping_patience", 15):
+                    print(f"Early stopping after {stale} epochs without improvement")
+                    break
+            self.history["stage_transitions"].append(
+                {"stage": stage, "completed_at": datetime.now().isoformat(),
+                 "best_val_acc": best_val_acc, "best_val_loss": best_val_loss})
+            print(f"Stage {stage} completed. Best Val Acc: {best_val_acc:.2f}%")
+        if rank == 0:
+            path = os.path.join(save_dir, "training_history.json")
+            with open(path, "w") as f:
+                json.dump(self.history, f, indent=2)
+            print(f"Training history saved to: {path}")
