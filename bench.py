@@ -81,7 +81,8 @@ def pmc_traffic(family):
     """HBM bytes per launch of a kernel family from the newest committed PMC summary
     (profiles/*_pmc.json, written by tools/pmc_summary.py from separate FETCH_SIZE /
     WRITE_SIZE passes with the gfx950 x2 read correction); None when absent."""
-    files = sorted((ROOT / "profiles").glob("*_pmc.json"), key=lambda p: p.stat().st_mtime)
+    # newest = last by name (r1c < r1d < ...): a checkout gives every file the same mtime
+    files = sorted((ROOT / "profiles").glob("*_pmc.json"), key=lambda p: p.name)
     if not files:
         return None, None
     rows = json.load(open(files[-1]))
@@ -100,6 +101,7 @@ def main():
     import ugpg
     from ugpg import ops
     from ugpg.dist import broadcast_parameters, init_from_env, max_over_ranks
+    from ugpg.trainer import MetricsReadback
 
     ops.set_conv_math(args.conv_math)
     # UGPG_DIST_BACKEND / UGPG_BENCH_DEVICE: rehearsal of the N-rank path on one GPU
@@ -125,20 +127,25 @@ def main():
     tr.current_model.train()
     tr.models[3].eval()
 
-    def step():
-        mbuf = tr.train_step(x, t, 4)
-        return mbuf.tolist()
+    def run(n):
+        # the trainer's epoch loop: step k's metrics are read back (pinned copy +
+        # event) after step k+1 has been enqueued, so the GPU never waits on Python
+        pending, last = None, None
+        for _ in range(n):
+            cur = MetricsReadback(tr.train_step(x, t, 4))
+            if pending is not None:
+                last = pending.values()
+            pending = cur
+        return pending.values() if pending is not None else last
 
-    for _ in range(args.warmup):
-        last = step()
+    last = run(args.warmup)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     timer = None if args.no_roofline else ops.KernelTimer()
     ops.TIMER = timer
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        last = step()
+    last = run(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

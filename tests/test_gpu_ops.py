@@ -348,6 +348,22 @@ def test_heads(dev, nc):
         close(nchw(da.cpu()), a.grad, 1e-5, f"head{i} da")
 
 
+@pytest.mark.parametrize("nc", [1, 3])
+def test_heads_split_bwd_full(dev, nc):
+    """dh of each deep-supervision head at the Stage-4 shapes (x8/x4/x2/x1 to 256^2,
+    PGUNet4.forward, UG_unet.py:294-303) against fp64 autograd of F.interpolate."""
+    from ugpg import ops
+    B, H = 2, 256
+    dl = rnd((B, nc, H, H), 97, "dl")
+    hres = [32, 64, 128, 256]
+    dhs = ops.heads_split_bwd(dl.to(dev), hres)
+    for R, dh in zip(hres, dhs):
+        h = torch.zeros(B, nc, R, R, dtype=torch.float64, requires_grad=True)
+        up = h if R == H else F.interpolate(h, size=(H, H), mode="bilinear", align_corners=True)
+        up.backward(dl.double())
+        close(nchw(dh.reshape(B, R, R, nc).cpu()), h.grad, 1e-5, f"split bwd R={R}")
+
+
 @pytest.mark.parametrize("pw,with_u,cu", [(5.0, True, 1), (None, True, 1), (5.0, False, 1), (2.0, True, 2)])
 def test_ug_loss(dev, pw, with_u, cu):
     from ugpg import ops

@@ -110,6 +110,16 @@ __device__ __forceinline__ float ac_weight(int o, int i, int in, int out) {
     return w;
 }
 
+// ac_range is conservative (about 2/scale + 5 candidates, most of zero weight: 7 per
+// dimension for x2, 49 ac_weight evaluations per input quad); trimming the zero-weight
+// ends leaves the 2-3 real contributors.  The skipped terms had zero weight and were
+// skipped anyway, so sums and their order are unchanged.
+__device__ __forceinline__ void ac_range_tight(int i, int in, int out, int& lo, int& hi) {
+    ac_range(i, in, out, lo, hi);
+    while (lo < hi && ac_weight(lo, i, in, out) == 0.f) ++lo;
+    while (hi > lo && ac_weight(hi, i, in, out) == 0.f) --hi;
+}
+
 // Row-blocked forms: blockIdx.y = output (input) row, so the row's interpolation
 // indices/weights and the 64-bit image offsets are computed once per thread, and a
 // thread keeps one channel quad (the x-stride is a multiple of C/4), loading the lazy
@@ -169,12 +179,12 @@ __global__ void bilinear_nhwc_bwd_kernel(const float* dout, int B, int Ho, int W
     const int row = blockIdx.y;  // b * Hi + iy
     const int b = row / Hi, iy = row % Hi;
     int ylo, yhi;
-    ac_range(iy, Hi, Ho, ylo, yhi);
+    ac_range_tight(iy, Hi, Ho, ylo, yhi);
     const int n = Wi * C4, stride = gridDim.x * blockDim.x;
     for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += stride) {
         const int c = (t % C4) * 4, ix = t / C4;
         int xlo, xhi;
-        ac_range(ix, Wi, Wo, xlo, xhi);
+        ac_range_tight(ix, Wi, Wo, xlo, xhi);
         f32x4 s = {0.f, 0.f, 0.f, 0.f};
         for (int oy = ylo; oy <= yhi; ++oy) {
             const float wyk = ac_weight(oy, iy, Hi, Ho);
@@ -326,37 +336,52 @@ __global__ void heads_combine_kernel(HeadSet hs, int B, int H, int W, int nc, fl
     }
 }
 
-// dh (NHWC, R x R, nc) from NCHW dlogits (H x W)
-__global__ void head_split_bwd_kernel(const float* dl, int B, int H, int W, int nc, float* dh,
-                                      int R) {
-    const int64_t total = (int64_t)B * R * R * nc;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const int k = (int)(i % nc);
-        int64_t r = i / nc;
-        const int ix = (int)(r % R);
-        r /= R;
-        const int iy = (int)(r % R), b = (int)(r / R);
+// dh (NHWC, R x R, nc) from NCHW dlogits (H x W): the transpose of the align-corners
+// upsample R -> H.  One block per (b, iy); for R < 256 the threads split the output
+// rows that feed the input row into 256/R interleaved parts, reduced through LDS, so
+// the 32-wide head (x8: ~15x15 contributing pixels per input pixel) runs on B*R
+// blocks rather than B*R*R/256 (64 blocks at bs16: 70 us -> a few us).
+__global__ void __launch_bounds__(256) head_split_bwd_kernel(const float* dl, int B, int H,
+                                                             int W, int nc, float* dh, int R) {
+    __shared__ float red[256];
+    const int b = blockIdx.x / R, iy = blockIdx.x % R, tid = threadIdx.x;
+    const int parts = R < 256 ? 256 / R : 1;
+    const int part = R < 256 ? tid / R : 0, lane = R < 256 ? tid % R : tid;
+    int ylo, yhi;
+    ac_range_tight(iy, R, H, ylo, yhi);
+    for (int k = 0; k < nc; ++k) {
         const float* src = dl + ((size_t)b * nc + k) * H * W;
-        float s;
-        if (R == H) {
-            s = src[(size_t)iy * W + ix];
-        } else {
-            int ylo, yhi, xlo, xhi;
-            ac_range(iy, R, H, ylo, yhi);
-            ac_range(ix, R, W, xlo, xhi);
-            s = 0.f;
-            for (int oy = ylo; oy <= yhi; ++oy) {
-                const float wy = ac_weight(oy, iy, R, H);
-                if (wy == 0.f) continue;
-                for (int ox = xlo; ox <= xhi; ++ox) {
-                    const float wx = ac_weight(ox, ix, R, W);
-                    if (wx == 0.f) continue;
-                    s += (wy * wx) * src[(size_t)oy * W + ox];
+        for (int ix0 = 0; ix0 < R; ix0 += 256) {
+            const int ix = ix0 + lane;
+            float s = 0.f;
+            if (part < parts && ix < R) {
+                if (R == H) {
+                    if (part == 0) s = src[(size_t)iy * W + ix];
+                } else {
+                    int xlo, xhi;
+                    ac_range_tight(ix, R, W, xlo, xhi);
+                    for (int oy = ylo + part; oy <= yhi; oy += parts) {
+                        const float wy = ac_weight(oy, iy, R, H);
+                        if (wy == 0.f) continue;
+                        const float* row = src + (size_t)oy * W;
+                        float r = 0.f;
+                        for (int ox = xlo; ox <= xhi; ++ox) {
+                            const float wx = ac_weight(ox, ix, R, W);
+                            if (wx != 0.f) r = fmaf(wx, row[ox], r);
+                        }
+                        s = fmaf(wy, r, s);
+                    }
                 }
             }
+            if (parts > 1) {
+                __syncthreads();  // previous channel's reads of red are done
+                red[tid] = s;
+                __syncthreads();
+                if (part == 0)
+                    for (int q = 1; q < parts; ++q) s += red[q * R + lane];
+            }
+            if (part == 0 && ix < R) dh[(((size_t)b * R + iy) * R + ix) * nc + k] = s;
         }
-        dh[i] = s;
     }
 }
 
@@ -1040,8 +1065,8 @@ extern "C" int ugpg_heads_split_bwd(const float* dl, int B, int H, int W, int nc
                                     const int* hres, int n, void* stream) {
     UGPG_REQUIRE(dl && dh && hres && n >= 1 && H == W, "heads_split_bwd");
     for (int i = 0; i < n; ++i) {
-        const int64_t total = (int64_t)B * hres[i] * hres[i] * nc;
-        hipLaunchKernelGGL(head_split_bwd_kernel, dim3(stream_grid(total)), dim3(256), 0,
+        UGPG_REQUIRE(hres[i] >= 1 && hres[i] <= H, "heads_split_bwd: head resolution");
+        hipLaunchKernelGGL(head_split_bwd_kernel, dim3((unsigned)(B * hres[i])), dim3(256), 0,
                            as_stream(stream), dl, B, H, W, nc, dh[i], hres[i]);
         if (int e = check_launch("heads_split_bwd")) return e;
     }

@@ -33,6 +33,27 @@ except Exception:  # pragma: no cover
     MATPLOTLIB_AVAILABLE = False
 
 
+class MetricsReadback:
+    """The 8-float device metrics buffer of one batch, copied to pinned host memory
+    behind an event.  Reading batch k after batch k+1 has been enqueued keeps the GPU
+    busy while Python prepares the next step (the host gap between a blocking
+    ``.tolist()`` and the next batch's first kernel was ~0.45 ms of a 20 ms step)."""
+
+    def __init__(self, mbuf):
+        if mbuf.is_cuda:
+            self.host = torch.empty(mbuf.shape, dtype=mbuf.dtype, pin_memory=True)
+            self.host.copy_(mbuf, non_blocking=True)
+            self.event = torch.cuda.Event()
+            self.event.record()
+        else:
+            self.host, self.event = mbuf, None
+
+    def values(self):
+        if self.event is not None:
+            self.event.synchronize()
+        return self.host.tolist()
+
+
 class UncertaintyGuidedProgressiveTrainer:
     def __init__(self, in_channels=3, num_classes=1, device="cuda", uncertainty_alpha=1.0):
         self.device = device
@@ -155,7 +176,19 @@ class UncertaintyGuidedProgressiveTrainer:
             self.models[stage - 1].eval()
         tot = np.zeros(6)
         res = self.stage_configs[stage]["resolution"]
-        nb = 0
+
+        def consume(batch_idx, npx, rb):
+            nonlocal tot
+            v = rb.values()  # the one host synchronisation of the batch
+            acc = 1 - v[4] / npx
+            um, us = (v[5], v[6]) if stage > 1 else (0.0, 0.0)
+            tot += (v[0], v[1], v[2], acc, um, us)
+            if train and batch_idx % 10 == 0:
+                extra = f", Unc_mean: {um:.4f}" if stage > 1 else ""
+                print(f"Stage {stage}, Batch {batch_idx}, Loss: {v[0]:.4f}, Base_Loss: {v[1]:.4f}, "
+                      f"Dice: {v[2]:.4f}, Acc: {acc:.4f}{extra}")
+
+        pending = None  # batch k is read back after batch k+1 is enqueued
         for batch_idx, (data, target) in enumerate(dataloader):
             data, target = self._resize_batch(data, target, res)
             if train:
@@ -165,16 +198,12 @@ class UncertaintyGuidedProgressiveTrainer:
                 with torch.no_grad():
                     output, umap, _, _ = self._forward_device(data, target, stage, mbuf)
                     self._metrics_device(output, target, umap, mbuf)
-            v = mbuf.tolist()  # the one host synchronisation of the batch
-            npx = data.shape[0] * res * res
-            acc = 1 - v[4] / npx
-            um, us = (v[5], v[6]) if stage > 1 else (0.0, 0.0)
-            tot += (v[0], v[1], v[2], acc, um, us)
-            nb += 1
-            if train and batch_idx % 10 == 0:
-                extra = f", Unc_mean: {um:.4f}" if stage > 1 else ""
-                print(f"Stage {stage}, Batch {batch_idx}, Loss: {v[0]:.4f}, Base_Loss: {v[1]:.4f}, "
-                      f"Dice: {v[2]:.4f}, Acc: {acc:.4f}{extra}")
+            cur = (batch_idx, data.shape[0] * res * res, MetricsReadback(mbuf))
+            if pending is not None:
+                consume(*pending)
+            pending = cur
+        if pending is not None:
+            consume(*pending)
         num = len(dataloader)
         avg = tot / num
         kind = "training" if train else "validation"
