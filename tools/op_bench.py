@@ -1,0 +1,44 @@
+"""Per-op HIP-event timing of the memory-bound helper kernels at their Stage-4 shapes
+(bs16).  python tools/op_bench.py  ->  one line per op: shape, µs/launch, GB/s."""
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "ug-pg-unet_amd")]
+
+import torch  # noqa: E402
+from ugpg import ops  # noqa: E402
+
+
+def timeit(fn, n=20):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / n
+
+
+def main():
+    dev = torch.device("cuda:0")
+    B = 16
+    for (h, c) in [(16, 512), (32, 256), (64, 128), (128, 64)]:
+        y = torch.randn(B, h, h, c, device=dev)
+        sc = torch.rand(c, device=dev) + 0.5
+        sh = torch.randn(c, device=dev) * 0.1
+        a = ops.Act(y, sc, sh)
+        us = timeit(lambda: ops.bilinear_nhwc_fwd(a, 2 * h, 2 * h))
+        gb = (y.numel() + 4 * y.numel()) * 4 / (us * 1e-6) / 1e9
+        print(f"bilinear_fwd {h}->{2 * h} C{c}: {us:7.1f} us  {gb:6.0f} GB/s", flush=True)
+        dout = torch.randn(B, 2 * h, 2 * h, c, device=dev)
+        din = torch.empty_like(y)
+        us = timeit(lambda: ops.bilinear_nhwc_bwd(dout, h, h, din, False))
+        gb = (dout.numel() + y.numel()) * 4 / (us * 1e-6) / 1e9
+        print(f"bilinear_bwd {2 * h}->{h} C{c}: {us:7.1f} us  {gb:6.0f} GB/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()

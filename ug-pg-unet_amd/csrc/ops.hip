@@ -157,6 +157,34 @@ __global__ void bilinear_nhwc_fwd_kernel(const float* x, const float* sc, const 
         }
         return v;
     };
+    constexpr int U = 4;
+    if (fixed_c && n % (U * stride) == 0) {
+        // U output quads per thread, all 4U loads issued before the first store
+        // (uniform trip count: no predication, the operands stay in VGPRs)
+        const int step = stride / C4;  // output pixels between a thread's quads
+        for (; t < n; t += U * stride) {
+            const int ox0 = t / C4;
+            f32x4 a[U][4];
+            float wx0[U], wx1[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                ac_index(ox0 + u * step, Wi, Wo, x0, x1, wx0[u], wx1[u]);
+                a[u][0] = *reinterpret_cast<const f32x4*>(r0 + (size_t)x0 * C + c);
+                a[u][1] = *reinterpret_cast<const f32x4*>(r0 + (size_t)x1 * C + c);
+                a[u][2] = *reinterpret_cast<const f32x4*>(r1 + (size_t)x0 * C + c);
+                a[u][3] = *reinterpret_cast<const f32x4*>(r1 + (size_t)x1 * C + c);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const f32x4 a00 = act(a[u][0]), a01 = act(a[u][1]), a10 = act(a[u][2]),
+                            a11 = act(a[u][3]);
+                const f32x4 v = ly0 * (wx0[u] * a00 + wx1[u] * a01) +
+                                ly1 * (wx0[u] * a10 + wx1[u] * a11);
+                *reinterpret_cast<f32x4*>(orow + (size_t)(ox0 + u * step) * C + c) = v;
+            }
+        }
+        return;
+    }
     for (; t < n; t += stride) {
         if (!fixed_c) {
             c = (t % C4) * 4;
@@ -181,11 +209,39 @@ __global__ void bilinear_nhwc_bwd_kernel(const float* dout, int B, int Ho, int W
     int ylo, yhi;
     ac_range_tight(iy, Hi, Ho, ylo, yhi);
     const int n = Wi * C4, stride = gridDim.x * blockDim.x;
+    // x2-type ranges (<= 4 contributors per dimension): weights hoisted, all loads
+    // issued before the first accumulate, same terms in the same order as the loop form
+    float wy[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wy[j] = ylo + j <= yhi ? ac_weight(ylo + j, iy, Hi, Ho) : 0.f;
     for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += stride) {
         const int c = (t % C4) * 4, ix = t / C4;
         int xlo, xhi;
         ac_range_tight(ix, Wi, Wo, xlo, xhi);
         f32x4 s = {0.f, 0.f, 0.f, 0.f};
+        if (yhi - ylo <= 3 && xhi - xlo <= 3) {
+            float wx[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) wx[k] = xlo + k <= xhi ? ac_weight(xlo + k, ix, Wi, Wo) : 0.f;
+            f32x4 d[4][4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    d[j][k] = wy[j] != 0.f && wx[k] != 0.f
+                                  ? *reinterpret_cast<const f32x4*>(
+                                        dout + ((size_t)(b * Ho + ylo + j) * Wo + xlo + k) * C + c)
+                                  : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (wy[j] != 0.f && wx[k] != 0.f) s += (wy[j] * wx[k]) * d[j][k];
+            f32x4* dst = reinterpret_cast<f32x4*>(din + ((size_t)row * Wi + ix) * C + c);
+            if (acc) s += *dst;
+            *dst = s;
+            continue;
+        }
         for (int oy = ylo; oy <= yhi; ++oy) {
             const float wyk = ac_weight(oy, iy, Hi, Ho);
             if (wyk == 0.f) continue;
@@ -993,7 +1049,11 @@ extern "C" int ugpg_bilinear_nhwc_fwd(ugpg_src_t s, int B, int Hi, int Wi, float
                                       int Wo, void* stream) {
     UGPG_REQUIRE(s.data && out && s.C % 4 == 0 && Ho > 0 && Wo > 0, "bilinear_nhwc_fwd");
     UGPG_REQUIRE((int64_t)B * Ho < 65536, "bilinear_nhwc_fwd: shape");
-    const unsigned gx = (unsigned)std::min<int64_t>(cdiv((int64_t)Wo * (s.C / 4), 256), 64);
+    // a quarter of the row's quads in threads when that divides evenly (the kernel's
+    // 4-quads-per-thread form), else one quad per thread
+    const int64_t nq = (int64_t)Wo * (s.C / 4);
+    const unsigned gx = nq % 1024 == 0 ? (unsigned)std::min<int64_t>(nq / 1024, 64)
+                                       : (unsigned)std::min<int64_t>(cdiv(nq, 256), 64);
     hipLaunchKernelGGL(bilinear_nhwc_fwd_kernel, dim3(gx, (unsigned)(B * Ho)), dim3(256), 0,
                        as_stream(stream), s.data, s.scale, s.shift, B, Hi, Wi, s.C, out, Ho, Wo);
     return check_launch("bilinear_nhwc_fwd");
