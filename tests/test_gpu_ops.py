@@ -64,6 +64,7 @@ CONV_CASES = [
     (2, 8, 8, 256, 256, 256, True),    # Up1 of a 64^2 stage
     (2, 20, 24, 64, 0, 64, True),      # 16x16-item persistent form: ragged rows and columns
     (1, 18, 17, 128, 64, 128, True),   # same, concat input, 2 partial tiles per side
+    (1, 16, 16, 512, 512, 512, True),  # Up-shaped 16-wide concat: 4-way split-K forward/dgrad
 ]
 BIG = {5, 6, 7}
 
