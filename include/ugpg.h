@@ -111,6 +111,14 @@ int ugpg_conv3x3_fwd_ntiles(int B, int H, int W, int Cin, int Cout, int wfmt);
 size_t ugpg_pack_conv3x3_bytes(int Cout, int Cin_pad, int wfmt);
 int ugpg_pack_conv3x3(const float* w_oihw, void* wpk, int Cout, int Cin, int Cin_pad,
                       int mode, int wfmt, void* stream);
+/* Many ugpg_pack_conv3x3 calls of one split-bf16 format (UGPG_WFMT_X6 / _BF16) in
+ * one launch (a step's forward and data-gradient packs): same bytes per item. */
+typedef struct {
+    const float* w;        /* OIHW fp32 [Cout][Cin][3][3] */
+    void* wpk;             /* ugpg_pack_conv3x3_bytes(Cout, Cin_pad, wfmt) bytes */
+    int Cout, Cin, Cin_pad, mode;
+} ugpg_pack_item_t;
+int ugpg_pack_conv3x3_batch(const ugpg_pack_item_t* items, int n, int wfmt, void* stream);
 
 /* Weight gradient (aten convolution_backward grad_weight/grad_bias, K3):
  *   dw[co][ci][ky][kx] (+)= sum_p dy[p][co] * act(x)[p + (ky-1,kx-1)][ci]

@@ -450,3 +450,31 @@ def test_avgpool_linear(dev):
     close(dx.cpu(), xin.grad, 1e-5, "linear dx")
     close(dw.cpu(), w.grad, 1e-5, "linear dw")
     close(db.cpu(), b.grad, 1e-5, "linear db")
+
+
+@pytest.mark.parametrize("conv_math", ["x6", "bf16"])
+def test_pack_batch_matches_single_packs(dev, conv_math):
+    """ugpg_pack_conv3x3_batch writes the same bytes as one ugpg_pack_conv3x3 per item
+    (forward and data-gradient layouts, the 16-channel image layer, > 48 items)."""
+    from ugpg import ops
+    old = ops.conv_math()
+    ops.set_conv_math(conv_math)
+    try:
+        shapes = [(64, 3, 16, 0), (64, 64, 64, 0), (128, 64, 64, 1), (64, 128, 128, 1),
+                  (512, 1024, 1024, 0), (256, 512, 512, 1)] * 9
+        ws = [rnd((co, ci, 3, 3), 200 + i, "pw").to(dev) for i, (co, ci, _, _) in enumerate(shapes)]
+        specs = [(w, k, m) for w, (_, _, k, m) in zip(ws, shapes)]
+        table = ops.prepack(specs)
+        assert len(table) == len(specs)
+        for w, k, m in specs:
+            got = table[ops._pack_key(w, k, m)]
+            want = ops.pack_conv3x3(w, k, m)
+            assert got.ugpg_fmt == want.ugpg_fmt
+            assert torch.equal(got.cpu(), want.cpu())
+        with ops.prepacked(table):
+            w, k, m = specs[1]
+            assert ops.pack_conv3x3(w, k, m) is table[ops._pack_key(w, k, m)]
+            w.add_(0.5)  # an in-place change retires the entry (version counter)
+            assert ops.pack_conv3x3(w, k, m) is not table.get(ops._pack_key(w, k, m), None)
+    finally:
+        ops.set_conv_math(old)

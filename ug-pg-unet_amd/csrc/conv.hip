@@ -1,3 +1,4 @@
+#include <vector>
 // 3x3 / pad-1 convolution for gfx950: forward, data-gradient (same kernel with a
 // rotated/transposed weight pack) and weight-gradient, all NHWC fp32 on
 // v_mfma_f32_32x32x2_f32 (exact fp32 FMA chains, 157 TF/s peak).
@@ -757,6 +758,29 @@ extern "C" int ugpg_pack_conv3x3(const float* w, void* wpk, int Cout, int Cin, i
     hipLaunchKernelGGL(pack_conv3x3_kernel, dim3(stream_grid(total)), dim3(256), 0,
                        as_stream(stream), w, static_cast<float*>(wpk), Cout, Cin, Cin_pad, mode);
     return check_launch("pack_conv3x3");
+}
+
+extern "C" int ugpg_pack_conv3x3_batch(const ugpg_pack_item_t* items, int n, int wfmt,
+                                       void* stream) {
+    if (!items || n < 0 || (wfmt != UGPG_WFMT_X6 && wfmt != UGPG_WFMT_BF16)) {
+        set_error("pack_conv3x3_batch: bad arguments (n=%d wfmt=%d)", n, wfmt);
+        return UGPG_ERR_INVALID;
+    }
+    std::vector<PackItem> v((size_t)n);
+    for (int i = 0; i < n; ++i) {
+        const ugpg_pack_item_t& q = items[i];
+        const int N = q.mode == 0 ? q.Cout : q.Cin_pad, K = q.mode == 0 ? q.Cin_pad : q.Cout;
+        if (!q.w || !q.wpk || q.Cin_pad < q.Cin || q.Cin_pad % 8 || q.mode < 0 || q.mode > 1 ||
+            (q.mode == 1 && q.Cout % 8) || N % 64 || K % 16) {
+            set_error("pack_conv3x3_batch: bad item %d (Cout=%d Cin=%d Cin_pad=%d mode=%d)", i,
+                      q.Cout, q.Cin, q.Cin_pad, q.mode);
+            return UGPG_ERR_INVALID;
+        }
+        v[i] = PackItem{q.w, q.wpk, q.Cout, q.Cin, q.Cin_pad, q.mode};
+    }
+    if (n == 0) return UGPG_OK;
+    launch_pack_x6_batch(v.data(), n, wfmt == UGPG_WFMT_X6 ? 3 : 1, as_stream(stream));
+    return check_launch("pack_conv3x3_batch");
 }
 
 static int wgrad_check(const ugpg_wgrad_t* p) {

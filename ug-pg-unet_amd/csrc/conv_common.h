@@ -161,6 +161,19 @@ struct WgradArgs {
 
 // split-bf16 path (conv_x6.hip)
 void launch_fwd_x6(const ConvFwdArgs& a, int np, hipStream_t st);  // np: bf16 pieces (3 or 1)
+// batched weight packing (ugpg_pack_conv3x3_batch), kernel-argument descriptors
+struct PackItem {
+    const float* w;
+    void* wpk;
+    int Cout, Cin, Cin_pad, mode;
+};
+constexpr int PACK_BATCH_MAX = 48;
+struct PackBatch {
+    PackItem item[PACK_BATCH_MAX];
+    int first[PACK_BATCH_MAX + 1];
+    int n;
+};
+void launch_pack_x6_batch(const PackItem* items, int n, int np, hipStream_t st);
 extern int g_x6_pipe, g_x6_probe;
 int fwd_x6_tile_w(int W, int np);  // 32 or 16 (np = bf16 pieces: 3 split, 1 bf16)
 int fwd_x6_tile_h(int W, int np);  // 4, 8 or 16

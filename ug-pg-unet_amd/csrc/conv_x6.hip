@@ -1617,41 +1617,60 @@ void launch_wgrad_x6(const WgradArgs& a, unsigned grid, int np, hipStream_t st) 
 // by 180 degrees.  Layout [N/64][K/16][ky 3][piece 3][half 2][kx 3][64][8] bf16:
 // the slab of one (column block, chunk, kernel row) is contiguous (18 KB) and
 // equals one LDS weight stage of the kernels below.
+__device__ __forceinline__ void pack_x6_elem(const float* w, __bf16* wpk, int Cin, int K,
+                                             int mode, int np, int64_t e) {
+    const int nchunk = K / 16;
+    const int64_t plane = 3 * 64 * 8;  // one (ky, piece, half) sub-slab: kx x co x 8
+    const int j = (int)(e & 7);
+    int64_t r = e >> 3;
+    const int co = (int)(r % 64);
+    r /= 64;
+    const int kx = (int)(r % 3);
+    r /= 3;
+    const int h = (int)(r % 2);
+    r /= 2;
+    const int ky = (int)(r % 3);
+    r /= 3;
+    const int chunk = (int)(r % nchunk), nb = (int)(r / nchunk);
+    const int t = ky * 3 + kx;
+    const int n = nb * 64 + co, k = chunk * 16 + h * 8 + j;
+    float v;
+    if (mode == 0) v = k < Cin ? w[((size_t)n * Cin + k) * 9 + t] : 0.f;
+    else v = n < Cin ? w[((size_t)k * Cin + n) * 9 + (8 - t)] : 0.f;
+    const __bf16 p0 = (__bf16)v;
+    const float r1 = v - (float)p0;
+    const __bf16 p1 = (__bf16)r1;
+    const __bf16 p2 = (__bf16)(r1 - (float)p1);
+    const size_t base = ((size_t)((nb * nchunk + chunk) * 3 + ky) * np * 2) * plane;
+    const size_t off = ((size_t)kx * 64 + co) * 8 + j;
+    wpk[base + (0 * 2 + h) * plane + off] = p0;
+    if (np == 3) {
+        wpk[base + (1 * 2 + h) * plane + off] = p1;
+        wpk[base + (2 * 2 + h) * plane + off] = p2;
+    }
+}
+
 __global__ void pack_x6_kernel(const float* w, __bf16* wpk, int Cout, int Cin, int N, int K,
                                int mode, int np) {
-    const int nchunk = K / 16;
+    (void)Cout;
     const int64_t total = (int64_t)N * K * 9;
-    const int64_t plane = 3 * 64 * 8;  // one (ky, piece, half) sub-slab: kx x co x 8
     for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
-         e += (int64_t)gridDim.x * blockDim.x) {
-        const int j = (int)(e & 7);
-        int64_t r = e >> 3;
-        const int co = (int)(r % 64);
-        r /= 64;
-        const int kx = (int)(r % 3);
-        r /= 3;
-        const int h = (int)(r % 2);
-        r /= 2;
-        const int ky = (int)(r % 3);
-        r /= 3;
-        const int chunk = (int)(r % nchunk), nb = (int)(r / nchunk);
-        const int t = ky * 3 + kx;
-        const int n = nb * 64 + co, k = chunk * 16 + h * 8 + j;
-        float v;
-        if (mode == 0) v = k < Cin ? w[((size_t)n * Cin + k) * 9 + t] : 0.f;
-        else v = n < Cin ? w[((size_t)k * Cin + n) * 9 + (8 - t)] : 0.f;
-        const __bf16 p0 = (__bf16)v;
-        const float r1 = v - (float)p0;
-        const __bf16 p1 = (__bf16)r1;
-        const __bf16 p2 = (__bf16)(r1 - (float)p1);
-        const size_t base = ((size_t)((nb * nchunk + chunk) * 3 + ky) * np * 2) * plane;
-        const size_t off = ((size_t)kx * 64 + co) * 8 + j;
-        wpk[base + (0 * 2 + h) * plane + off] = p0;
-        if (np == 3) {
-            wpk[base + (1 * 2 + h) * plane + off] = p1;
-            wpk[base + (2 * 2 + h) * plane + off] = p2;
-        }
-    }
+         e += (int64_t)gridDim.x * blockDim.x)
+        pack_x6_elem(w, wpk, Cin, K, mode, np, e);
+}
+
+// Every weight of a step in one launch: item i owns blocks [first[i], first[i+1]) and
+// walks its N*K*9 elements with that block range (same element code as pack_x6_kernel).
+__global__ void pack_x6_batch_kernel(PackBatch pb, int np) {
+    int i = 0;
+    while (i + 1 < pb.n && (int)blockIdx.x >= pb.first[i + 1]) ++i;  // uniform
+    const PackItem& it = pb.item[i];
+    const int N = it.mode == 0 ? it.Cout : it.Cin_pad, K = it.mode == 0 ? it.Cin_pad : it.Cout;
+    const int64_t total = (int64_t)N * K * 9;
+    const int64_t nthr = (int64_t)(pb.first[i + 1] - pb.first[i]) * blockDim.x;
+    for (int64_t e = (blockIdx.x - pb.first[i]) * (int64_t)blockDim.x + threadIdx.x; e < total;
+         e += nthr)
+        pack_x6_elem(it.w, static_cast<__bf16*>(it.wpk), it.Cin, K, it.mode, np, e);
 }
 
 int g_x6_pipe = 2;   // tuning knob "x6_pipe" (see launch_fwd_x6)
@@ -1717,6 +1736,24 @@ void launch_pack_x6(const float* w, void* wpk, int Cout, int Cin, int Cin_pad, i
     const int N = mode == 0 ? Cout : Cin_pad, K = mode == 0 ? Cin_pad : Cout;
     hipLaunchKernelGGL(pack_x6_kernel, dim3(stream_grid((int64_t)N * K * 9)), dim3(256), 0, st, w,
                        static_cast<__bf16*>(wpk), Cout, Cin, N, K, mode, np);
+}
+
+void launch_pack_x6_batch(const PackItem* items, int n, int np, hipStream_t st) {
+    for (int i0 = 0; i0 < n; i0 += PACK_BATCH_MAX) {
+        PackBatch pb;
+        pb.n = std::min(PACK_BATCH_MAX, n - i0);
+        int blocks = 0;
+        for (int i = 0; i < pb.n; ++i) {
+            const PackItem& it = items[i0 + i];
+            pb.item[i] = it;
+            pb.first[i] = blocks;
+            const int N = it.mode == 0 ? it.Cout : it.Cin_pad, K = it.mode == 0 ? it.Cin_pad : it.Cout;
+            // ~4 elements per thread
+            blocks += (int)std::min<int64_t>(cdiv((int64_t)N * K * 9, 1024), 2048);
+        }
+        pb.first[pb.n] = blocks;
+        hipLaunchKernelGGL(pack_x6_batch_kernel, dim3((unsigned)blocks), dim3(256), 0, st, pb, np);
+    }
 }
 
 }  // namespace ugpg

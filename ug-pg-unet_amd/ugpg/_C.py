@@ -28,6 +28,11 @@ class ConvDesc(C.Structure):
                 ("stats", _p), ("wfmt", _i)]
 
 
+class PackItem(C.Structure):
+    """ugpg_pack_item_t."""
+    _fields_ = [("w", _p), ("wpk", _p), ("Cout", _i), ("Cin", _i), ("Cin_pad", _i), ("mode", _i)]
+
+
 class WgradDesc(C.Structure):
     """ugpg_wgrad_t."""
     _fields_ = [("B", _i), ("H", _i), ("W", _i), ("src", Src * 2), ("dy", _p), ("Cout", _i),
@@ -42,6 +47,7 @@ SIGNATURES = {
     "ugpg_conv3x3_fwd": (_i, [C.POINTER(ConvDesc), _p]),
     "ugpg_conv3x3_fwd_ntiles": (_i, [_i, _i, _i, _i, _i, _i]),
     "ugpg_pack_conv3x3_bytes": (_sz, [_i, _i, _i]),
+    "ugpg_pack_conv3x3_batch": (_i, [C.POINTER(PackItem), _i, _i, _p]),
     "ugpg_pack_conv3x3": (_i, [_p, _p, _i, _i, _i, _i, _i, _p]),
     "ugpg_conv3x3_wgrad_workspace": (_sz, [C.POINTER(WgradDesc)]),
     "ugpg_conv3x3_wgrad": (_i, [C.POINTER(WgradDesc), _p, _sz, _p]),

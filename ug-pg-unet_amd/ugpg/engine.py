@@ -161,10 +161,35 @@ class UNetGraph:
         self.blocks = list(blocks)
         self.heads = list(heads)
 
+    # -------------------------------------------------------------- weight packs
+    def _pack_specs(self, cpad, save):
+        """(weight, K, mode) of every 3x3 pack this forward (and, when saving for the
+        backward, its data gradients) will request -- the arguments double_conv_forward
+        and double_conv_backward pass to ops.pack_conv3x3."""
+        specs = []
+        for blk in self.blocks:
+            (c1, _), (c2, _) = _conv_bn(blk.mod.conv_op)
+            w1, w2 = c1.weight.detach(), c2.weight.detach()
+            cin = cpad if blk.kind == "inc" else w1.shape[1]
+            specs += [(w1, ops.conv_pack_k(cin), 0), (w2, ops.conv_pack_k(w2.shape[1]), 0)]
+            if save:
+                specs.append((w2, w2.shape[1], 1))
+                if blk.kind != "inc":  # the image input gets no data gradient by default
+                    specs.append((w1, w1.shape[1], 1))
+        return specs
+
     # -------------------------------------------------------------- forward
     def forward(self, x, save: bool):
         if x.dim() != 4:
             raise ValueError(f"expected NCHW input, got shape {tuple(x.shape)}")
+        packs = ops.prepack(self._pack_specs(ceil_to(x.shape[1], 8), save))
+        with ops.prepacked(packs):
+            logits, state = self._forward(x, save)
+        if save:
+            state["packs"] = packs
+        return logits, state
+
+    def _forward(self, x, save: bool):
         B, cx, H, W = x.shape
         cpad = ceil_to(cx, 8)
         x0 = ops.nchw_to_nhwc(x.detach().to(torch.float32), cpad)
@@ -208,6 +233,10 @@ class UNetGraph:
 
     # -------------------------------------------------------------- backward
     def backward(self, state, grads, dlogits=None, dout_act=None, need_dx=False, on_done=None):
+        with ops.prepacked(state.get("packs")):
+            return self._backward(state, grads, dlogits, dout_act, need_dx, on_done)
+
+    def _backward(self, state, grads, dlogits=None, dout_act=None, need_dx=False, on_done=None):
         """dlogits: NCHW gradient of the combined head output, or dout_act: NHWC
         gradient w.r.t. the last block's activation (encoder-only graphs).
         grads: {param: destination tensor or None}.  on_done(views) is called with the

@@ -11,7 +11,7 @@ import os
 
 import torch
 
-from ._C import ConvDesc, Src, WgradDesc, check, lib
+from ._C import ConvDesc, PackItem, Src, WgradDesc, check, lib
 
 F32 = torch.float32
 
@@ -124,9 +124,68 @@ def conv_pack_k(cin: int) -> int:
     return 16 if cin == 8 and _conv_math == "x6" else cin
 
 
+# packs made ahead for the running forward/backward (see prepack / UNetGraph); a miss
+# (or None) packs on the spot, so the table only saves launches, never changes results
+_PREPACK = None
+_PREPACK_ON = os.environ.get("UGPG_PREPACK", "1") != "0"  # A/B switch
+
+
+def _pack_key(w, cin_pad, mode):
+    return (w.data_ptr(), w._version, tuple(w.shape), int(cin_pad), int(mode), _conv_math)
+
+
+def prepack(specs):
+    """Pack many (weight, cin_pad, mode) in one launch (split-bf16 formats only);
+    returns {key: packed} for pack_conv3x3 to consult while the table is active."""
+    table = {}
+    if _conv_math not in ("x6", "bf16") or not specs or not _PREPACK_ON:
+        return table
+    items, outs = [], []
+    for w, cin_pad, mode in specs:
+        cout, cin = w.shape[0], w.shape[1]
+        fmt = conv_weight_format(cout, cin_pad) if mode == 0 else conv_weight_format(cin_pad, cout)
+        if fmt != _MATH_FMT[_conv_math] or not w.is_contiguous() or w.dtype != F32:
+            continue
+        key = _pack_key(w, cin_pad, mode)
+        if key in table:
+            continue
+        out = torch.empty(lib.ugpg_pack_conv3x3_bytes(cout, cin_pad, fmt), dtype=torch.uint8,
+                          device=w.device)
+        out.ugpg_fmt = fmt
+        table[key] = out
+        items.append(PackItem(ptr(w), ptr(out), cout, cin, int(cin_pad), int(mode)))
+        outs.append(out)
+    if items:
+        arr = (PackItem * len(items))(*items)
+        check(lib.ugpg_pack_conv3x3_batch(arr, len(items), _MATH_FMT[_conv_math], stream()),
+              "pack_conv3x3_batch")
+    return table
+
+
+class prepacked:
+    """Context manager: make `table` visible to pack_conv3x3 (restores the previous)."""
+
+    def __init__(self, table):
+        self.table = table
+
+    def __enter__(self):
+        global _PREPACK
+        self.prev, _PREPACK = _PREPACK, self.table
+        return self.table
+
+    def __exit__(self, *exc):
+        global _PREPACK
+        _PREPACK = self.prev
+        return False
+
+
 def pack_conv3x3(w, cin_pad: int, mode: int) -> torch.Tensor:
     """Repack OIHW weights for conv3x3_fwd (mode 0) or its data gradient (mode 1).
     The result carries its pack format in ``.ugpg_fmt``."""
+    if _PREPACK:
+        hit = _PREPACK.get(_pack_key(w, cin_pad, mode))
+        if hit is not None:
+            return hit
     cout, cin = w.shape[0], w.shape[1]
     fmt = conv_weight_format(cout, cin_pad) if mode == 0 else conv_weight_format(cin_pad, cout)
     out = torch.empty(lib.ugpg_pack_conv3x3_bytes(cout, cin_pad, fmt), dtype=torch.uint8,
