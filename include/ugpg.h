@@ -252,6 +252,17 @@ size_t ugpg_mean_std_workspace(int64_t n);
 int ugpg_mean_std(const float* x, int64_t n, float* out, void* ws, size_t ws_bytes,
                   void* stream);
 
+/* ---- data-parallel metrics exchange (metrics all-reduced under DP; the
+ * reference is single-process, its per-batch metrics are uncertainty_guided_trainer.py:
+ * 171-182, 221-234 and Herlev/train_herlev.py:288-294, 328-337).
+ * m[0..n) (n <= 32): entries with bit i of avg_mask are per-rank means (averaged over
+ * ranks), other entries are sums; [ip, ip+1) is a (mean, unbiased std) pair over n_stat
+ * values per rank (ip = -1: none).  pack writes double sums[n+2] for a SUM all-reduce;
+ * unpack turns the reduced sums back into global metrics (Chan-style pooled std). */
+int ugpg_metrics_pack(const float* m, int n, int ip, double n_stat, double* sums, void* stream);
+int ugpg_metrics_unpack(const double* sums, int n, int ip, unsigned avg_mask, float* m,
+                        void* stream);
+
 /* ---- RMSprop (torch.optim.RMSprop rule, uncertainty_guided_trainer.py:84-88, K15)
  * g = grad*grad_scale + wd*p;  v = alpha*v + (1-alpha)*g^2;  p -= lr*g/(sqrt(v)+eps) */
 int ugpg_rmsprop_step(float* param, const float* grad, float* square_avg, int64_t n, float lr,

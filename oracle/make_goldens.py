@@ -13,10 +13,18 @@ Fixture map:
                           grad stats + fp64 noise floor, BN running stats, post-RMSprop stats
   g2_umap.npz             uncertainty maps S1@32->64 and S3@128->256, bs2
   g3_loss.npz             weighted loss for alpha in {0,.5,1,2,5}
+  g3b_loss_reduction.npz  weighted loss for reduction none/mean/sum, vector pos_weight, weight
   g4_pgunet4.npz          PGUNet4 bs2 64^2 (+ bs1 256^2 logits), UG loss w/ S3 map, grads
   g5_transfer.json        transfer_weights 1->2, 2->3, 3->4 copied keys + checksums
   g6_train_epoch.json     trainer.train_epoch 6-tuples, stage 1 and stage 2
   g7_herlev.npz           Herlev S4 classifier (eval logits, UG CE loss, grads w/o dropout)
+  g7b_herlev_trainer_step.npz  the reference HerlevTrainer's UG step at 224^2, bs4
+  g7c_herlev_ctor.npz     HerlevClassificationModel constructor: RNG position + probe BN state
+  g7d_herlev_binary.npz   the reference's binary (num_classes 2) Herlev UG step
+  g8_dp_shards.npz        DP semantics: mean of 2 per-shard local-BN gradients, step, 6-tuple
+  g9_rng.json             RNG positions after ProgressiveUNet / trainer ctor / transfer
+  g10_monuseg_eval.npz    MoNuSegEvaluator.calculate_metrics and predict_image, run for real
+  g4b_pgunet4_bs16.npz    config 2 at bs16 x 256^2: checksums, fp32 noise floors
 """
 from __future__ import annotations
 
@@ -183,6 +191,34 @@ def g3(RU):
     save_npz("g3_loss.npz", rows=np.array(rows))
 
 
+def g3b(RU):
+    """apply_uncertainty_weighted_loss over criterion reductions / pos_weight forms:
+    the reference's result (final, base) per case, and the oracle's equality with it."""
+    loss_mod = RU.UncertaintyGuidedLoss(device="cpu")
+    out = G.randn(30, (2, 1, 64, 64), "logits")
+    t = G.bernoulli(31, (2, 1, 64, 64), 0.3, "t")
+    u = torch.from_numpy(G.uniform(32, 2 * 64 * 64, "u").reshape(2, 1, 64, 64)).float()
+    out2 = G.randn(33, (2, 2, 32, 32), "logits2")
+    t2 = G.bernoulli(34, (2, 2, 32, 32), 0.3, "t2")
+    u2 = torch.from_numpy(G.uniform(35, 2 * 32 * 32, "u2").reshape(2, 1, 32, 32)).float()
+    fx = {}
+
+    def run(name, crit, o, tt, uu, a):
+        f_ref, b_ref = loss_mod.apply_uncertainty_weighted_loss(crit, o, tt, uu, a)
+        f_o, b_o = O.weighted_loss(crit(o, tt), uu, a)
+        assert torch.equal(f_ref, f_o) and b_ref == b_o, name
+        fx[name] = np.array([f_o.item(), b_o])
+
+    for red, pw, use_u, a in O.LOSS_CASES:
+        run(O.loss_case_name(red, pw, use_u, a), O.loss_case_criterion(red, pw), out, t,
+            u if use_u else None, a)
+    for red, kind in O.LOSS_CASES_C2:
+        for use_u in (False, True):
+            run(f"c2,red={red},{kind},u={int(use_u)}", O.loss_case_criterion_c2(red, kind),
+                out2, t2, u2 if use_u else None, 1.5)
+    save_npz("g3b_loss_reduction.npz", **fx)
+
+
 def g4(RU):
     fx = {}
     state = det_state(4, 3, 1)
@@ -341,6 +377,326 @@ def g7(RU):
     save_npz("g7_herlev.npz", **fx)
 
 
+def _herlev_ref():
+    """Import Herlev/train_herlev.py with in-process stubs for its dataset imports
+    (torchvision, herlev_dataset: absent here, unused by the model and the step)."""
+    import types
+    for mod in ("torchvision", "torchvision.transforms", "herlev_dataset"):
+        if mod not in sys.modules:
+            m = types.ModuleType(mod)
+            m.HerlevDataset = object
+            m.transforms = m
+            sys.modules[mod] = m
+    hp = os.path.join(REF, "Herlev")
+    if hp not in sys.path:
+        sys.path.insert(0, hp)
+    import train_herlev as H  # noqa: E402
+    return H
+
+
+G4B = dict(B=16, res=256, x_seed=101, t_seed=102, w_seed=0, prev_seed=13)
+
+
+def g4b(RU):
+    """Config 2 at its benchmarked size: PGUNet4 UG step, bs16 x 256^2 (S3@128 U map,
+    weighted BCE pos_weight 5, RMSprop lr 1e-4).  Checksums of the reference's logits,
+    loss, U, every gradient, BN buffers and post-step parameters, plus the per-tensor
+    fp32 noise floor (unperturbed and ulp-perturbed runs vs fp64) used by the GPU test."""
+    from tests._parity import noise_floor
+    c = G4B
+    state = det_state(4, 3, 1, seed=c["w_seed"])
+    prev = det_state(3, 3, 1, seed=c["prev_seed"])
+    x = G.randn(c["x_seed"], (c["B"], 3, c["res"], c["res"]), "x")
+    t = G.bernoulli(c["t_seed"], (c["B"], 1, c["res"], c["res"]), 0.5, "t")
+    loss_mod = RU.UncertaintyGuidedLoss(device="cpu")
+    ref_prev = RU.PGUNet3(3, 1)
+    ref_prev.load_state_dict(prev)
+    u_ref = loss_mod.generate_uncertainty_map(x, ref_prev, 128, 256)
+    u = O.uncertainty_map(3, prev, x, 128, 256)
+    assert torch.equal(u, u_ref)
+    ref = RU.PGUNet4(3, 1)
+    ref.load_state_dict(state)
+    out_ref = ref(x)
+    crit = nn.BCEWithLogitsLoss(pos_weight=torch.tensor([5.0]), reduction="none")
+    f_ref, b_ref = loss_mod.apply_uncertainty_weighted_loss(crit, out_ref, t, u_ref, 1.0)
+    f_ref.backward()
+    logits, final, base, g32, P = oracle_grads(4, state, x, t, 5.0, u, 1.0)
+    assert torch.equal(logits, out_ref.detach()) and torch.equal(final, f_ref.detach())
+    for k, p in ref.named_parameters():
+        assert torch.equal(g32[k], p.grad), f"G4b: grad {k} differs"
+    _, final64, _, g64, _ = oracle_grads(4, state, x, t, 5.0, u, 1.0, dtype=torch.float64)
+    floor = noise_floor(4, state, x, t, g32, g64, umap=u, alpha=1.0)
+    keys = param_keys(state)
+    opt = torch.optim.RMSprop(ref.parameters(), lr=1e-4, weight_decay=1e-4)
+    opt.step()
+    sd = ref.state_dict()
+    pred = O.predictions(logits)
+    fx = dict(loss=np.array([final.item(), base, final64.item()]),
+              logits_stats=tstats("logits", logits), logits_sample_sums=logits.double().sum(
+                  dim=(1, 2, 3)).numpy(), u_stats=np.array([u.mean().item(), u.std().item()]),
+              dice_acc=np.array([O.dice(pred, t.squeeze(1)).item(),
+                                 O.accuracy(pred, t.squeeze(1).long())]))
+    fx.update(grad_fixture("", keys, g32, g64))
+    for k in keys:
+        fx[f"floor_pert/{k}"] = np.array(floor[k])
+        fx[f"post/{k}"] = tstats(k, sd[k])
+    for k, v in sd.items():
+        if O._is_buffer(k) and v.is_floating_point():
+            fx[f"buf/{k}"] = v.numpy()
+        elif k.endswith("num_batches_tracked"):
+            fx[f"buf/{k}"] = np.array(int(v))
+    save_npz("g4b_pgunet4_bs16.npz", **fx)
+
+
+def g7b(RU):
+    """Herlev UG step through the reference's own HerlevTrainer.uncertainty_guided_forward_pass
+    (train_herlev.py:216-296) at its Stage-4 resolution 224, bs4, 7 classes, class
+    weights, dropout off: final/base loss, weight mean/std, logits and gradients."""
+    H = _herlev_ref()
+    K, B, res = 7, 4, 224
+    cw = [0.5, 0.75, 1.0, 1.25, 1.5, 1.75, 2.0]
+    torch.manual_seed(0)
+    tr = H.HerlevTrainer({"device": "cpu", "epochs_per_stage": 1, "num_classes": K,
+                          "class_weights": cw, "uncertainty_alpha": 1.0, "weight_decay": 1e-4})
+    s4 = G.make_state(O.state_spec(4, 3, 1, key_prefix="unet.") + O.herlev_head_spec(512, K), 75)
+    s3 = G.make_state(O.state_spec(3, 3, 1, key_prefix="unet.") + O.herlev_head_spec(512, K), 76)
+    tr.models[4].load_state_dict(s4)
+    tr.models[3].load_state_dict(s3)
+    tr.models[4].train()
+    for m in tr.models[4].modules():
+        if isinstance(m, nn.Dropout):
+            m.p = 0.0
+    x = G.randn(77, (B, 3, res, res), "x")
+    y = G.randint(78, (B,), K, "y")
+    final, met = tr.uncertainty_guided_forward_pass(x, y, 4)
+    final.backward()
+    # the oracle restatement must reproduce it exactly
+    P = {k: v.clone() for k, v in s4.items()}
+    for k in param_keys(P):
+        P[k].requires_grad_(True)
+    out_o = O.herlev_forward(4, P, x, training=True)
+    P3 = {k: v.clone() for k, v in s3.items()}
+    with torch.no_grad():
+        prev = O.herlev_forward(3, P3, O.resize_bilinear(x, 128), training=False)
+    f_o, b_o, w_o = O.herlev_ug_loss(out_o, y, prev, 1.0, K, torch.tensor(cw))
+    f_o.backward()
+    assert torch.equal(out_o, met["output"]) and torch.equal(f_o, final)
+    assert b_o.item() == met["base_loss"]
+    assert w_o.mean().item() == met["uncertainty_weight_mean"]
+    assert w_o.std().item() == met["uncertainty_weight_std"]
+    fx = dict(loss=np.array([met["final_loss"], met["base_loss"], met["uncertainty_weight_mean"],
+                             met["uncertainty_weight_std"]]),
+              logits=met["output"].detach().numpy(), prev_logits=prev.numpy(), y=y.numpy(),
+              class_weights=np.array(cw, dtype=np.float32))
+    for k, p in tr.models[4].named_parameters():
+        if p.grad is None:
+            assert P[k].grad is None, k
+            continue
+        assert torch.equal(P[k].grad, p.grad), f"G7b grad {k}"
+        fx[f"grad32/{k}"] = tstats(k, p.grad)
+    save_npz("g7b_herlev_trainer_step.npz", **fx)
+
+
+def g7d(RU):
+    """The reference's binary Herlev branch (num_classes 2, train_herlev.py:258-261): sigmoid
+    uncertainty per logit, weights broadcast against the per-sample CE (B = 2, the only
+    batch size besides 1 at which the reference's broadcast is defined)."""
+    H = _herlev_ref()
+    K, B, res = 2, 2, 64
+    torch.manual_seed(0)
+    tr = H.HerlevTrainer({"device": "cpu", "epochs_per_stage": 1, "num_classes": K,
+                          "class_weights": None, "uncertainty_alpha": 0.7, "weight_decay": 1e-4})
+    tr.stage_configs[4]["resolution"] = res
+    s4 = G.make_state(O.state_spec(4, 3, 1, key_prefix="unet.") + O.herlev_head_spec(512, K), 85)
+    s3 = G.make_state(O.state_spec(3, 3, 1, key_prefix="unet.") + O.herlev_head_spec(512, K), 86)
+    tr.models[4].load_state_dict(s4)
+    tr.models[3].load_state_dict(s3)
+    tr.models[4].train()
+    for m in tr.models[4].modules():
+        if isinstance(m, nn.Dropout):
+            m.p = 0.0
+    x = G.randn(87, (B, 3, res, res), "x")
+    y = G.randint(88, (B,), K, "y")
+    final, met = tr.uncertainty_guided_forward_pass(x, y, 4)
+    final.backward()
+    P3 = {k: v.clone() for k, v in s3.items()}
+    with torch.no_grad():
+        prev = O.herlev_forward(3, P3, O.resize_bilinear(x, 128), training=False)
+    f_o, b_o, w_o = O.herlev_ug_loss(met["output"].detach(), y, prev, 0.7, K, None)
+    assert torch.equal(f_o, final.detach()) and b_o.item() == met["base_loss"]
+    fx = dict(loss=np.array([met["final_loss"], met["base_loss"], met["uncertainty_weight_mean"],
+                             met["uncertainty_weight_std"]]),
+              logits=met["output"].detach().numpy(), y=y.numpy())
+    for k, p in tr.models[4].named_parameters():
+        if p.grad is not None:
+            fx[f"grad32/{k}"] = tstats(k, p.grad)
+    save_npz("g7d_herlev_binary.npz", **fx)
+
+
+def g7c(RU):
+    """Constructor side effects of HerlevClassificationModel (train_herlev.py:59-63): the
+    RNG stream after construction and the BatchNorm state left by the probe forward."""
+    H = _herlev_ref()
+    torch.manual_seed(5)
+    m = H.HerlevClassificationModel(stage=4, num_classes=7)
+    after = torch.rand(4)
+    fx = {"rng_after": after.numpy()}
+    for k, v in m.state_dict().items():
+        if O._is_buffer(k) and v.is_floating_point():
+            fx[f"buf/{k}"] = v.numpy()
+        elif k.endswith("num_batches_tracked"):
+            fx[f"buf/{k}"] = np.array(int(v))
+        else:
+            fx[f"sum/{k}"] = np.array(v.double().sum().item())
+    save_npz("g7c_herlev_ctor.npz", **fx)
+
+
+G8 = dict(stage=2, B=4, res=64, shards=2, w_seed=80, prev_seed=81, x_seed=82, t_seed=83)
+
+
+def g8(RU):
+    """Data-parallel semantics (local BatchNorm): 2 shards of a bs4 Stage-2
+    UG step (U map from Stage 1), each through a fresh reference model; the mean of
+    the per-shard gradients, one RMSprop step on it, and the DP train_epoch 6-tuple
+    (shard means of loss/Dice, global accuracy and U statistics)."""
+    c = G8
+    stage, B, res, S = c["stage"], c["B"], c["res"], c["shards"]
+    state = det_state(stage, 3, 1, seed=c["w_seed"])
+    prev = det_state(stage - 1, 3, 1, seed=c["prev_seed"])
+    x = G.randn(c["x_seed"], (B, 3, res, res), "x")
+    t = G.bernoulli(c["t_seed"], (B, 1, res, res), 0.5, "t")
+    loss_mod = RU.UncertaintyGuidedLoss(device="cpu")
+    ref_prev = RU.PGUNet1(3, 1)
+    ref_prev.load_state_dict(prev)
+    crit = nn.BCEWithLogitsLoss(pos_weight=torch.tensor([5.0]), reduction="none")
+    keys = param_keys(state)
+    gsum, rows, bufs0 = None, [], None
+    per = B // S
+    for r in range(S):
+        xs, ts = x[r * per:(r + 1) * per], t[r * per:(r + 1) * per]
+        m = RU.PGUNet2(3, 1)
+        m.load_state_dict(state)
+        m.train()
+        out = m(xs)
+        u = loss_mod.generate_uncertainty_map(xs, ref_prev, 32, 64)
+        f, b = loss_mod.apply_uncertainty_weighted_loss(crit, out, ts, u, 1.0)
+        f.backward()
+        lo, fo, bo, go, Po = oracle_grads(stage, state, xs, ts, 5.0,
+                                          O.uncertainty_map(1, prev, xs, 32, 64), 1.0)
+        assert torch.equal(lo, out.detach()) and torch.equal(fo, f.detach()) and bo == b
+        g = {k: p.grad.clone() for k, p in m.named_parameters()}
+        for k in keys:
+            assert torch.equal(go[k], g[k]), f"G8 grad {k}"
+        gsum = g if gsum is None else {k: gsum[k] + g[k] for k in keys}
+        pred = O.predictions(out.detach())
+        rows.append([f.item(), b, O.dice(pred, ts.squeeze(1)).item()])
+        if r == 0:
+            bufs0 = {k: v.clone() for k, v in m.state_dict().items() if O._is_buffer(k)}
+    avg = {k: gsum[k] / S for k in keys}
+    m = RU.PGUNet2(3, 1)
+    m.load_state_dict(state)
+    for k, p in m.named_parameters():
+        p.grad = avg[k].clone()
+    torch.optim.RMSprop(m.parameters(), lr=1e-4, weight_decay=1e-4).step()
+    sd = m.state_dict()
+    u_all = loss_mod.generate_uncertainty_map(x, ref_prev, 32, 64)
+    # accuracy of the whole batch (per-shard logits), U stats of the whole batch
+    preds = []
+    for r in range(S):
+        mm = RU.PGUNet2(3, 1)
+        mm.load_state_dict(state)
+        preds.append(O.predictions(mm(x[r * per:(r + 1) * per]).detach()))
+    acc = O.accuracy(torch.cat(preds), t.squeeze(1).long())
+    rows = np.array(rows)
+    tup = [rows[:, 0].mean(), rows[:, 1].mean(), rows[:, 2].mean(), acc,
+           u_all.mean().item(), u_all.std().item()]
+    fx = dict(shard_rows=rows, epoch_tuple=np.array(tup))
+    for k in keys:
+        fx[f"avg_grad/{k}"] = tstats(k, avg[k])
+        fx[f"post/{k}"] = tstats(k, sd[k])
+    for k, v in bufs0.items():
+        fx[f"buf0/{k}"] = v.numpy() if v.is_floating_point() else np.array(int(v))
+    save_npz("g8_dp_shards.npz", **fx)
+
+
+def g9(RU):
+    """RNG stream positions: after ProgressiveUNet(3, 1), after the trainer constructor,
+    and after trainer.transfer_weights(1, 2) (which builds a ProgressiveUNet)."""
+    import uncertainty_guided_trainer as RT  # noqa: E402
+    out = {}
+    torch.manual_seed(0)
+    RU.ProgressiveUNet(3, 1)
+    out["after_progressive_unet"] = torch.rand(4).tolist()
+    torch.manual_seed(1)
+    tr = RT.UncertaintyGuidedProgressiveTrainer(3, 1, device="cpu")
+    out["after_trainer_ctor"] = torch.rand(4).tolist()
+    tr.transfer_weights(1, 2)
+    out["after_transfer_1_2"] = torch.rand(4).tolist()
+    (OUT / "g9_rng.json").write_text(json.dumps(out, indent=1))
+    print("wrote g9_rng.json")
+
+
+def g10(RU):
+    """MoNuSegEvaluator (MoNuSegImprove/test_monuseg.py:100-297) run for real: module-level
+    imports cv2 / monuseg_dataset / preprocessing_utils are stubbed in-process (unused by
+    calculate_metrics and predict_image).  calculate_metrics on edge-case and random
+    masks; predict_image of a PIL image with a Stage-1 model (target_size 32)."""
+    import tempfile
+    import types
+    from PIL import Image
+    for mod, attrs in (("cv2", {}), ("monuseg_dataset", {"MoNuSegDataset": object}),
+                       ("preprocessing_utils", {"xml_to_mask": None})):
+        if mod not in sys.modules:
+            m = types.ModuleType(mod)
+            for a, v in attrs.items():
+                setattr(m, a, v)
+            sys.modules[mod] = m
+    mp = os.path.join(REF, "MoNuSegImprove")
+    if mp not in sys.path:
+        sys.path.insert(0, mp)
+    import test_monuseg as TM  # noqa: E402
+    ev = object.__new__(TM.MoNuSegEvaluator)
+    ev.device = "cpu"
+    fx = {}
+    cases = {"empty_pred": (np.zeros((40, 50), np.float32), G.bernoulli(110, (40, 50), .3, "g").numpy()),
+             "empty_gt": (G.bernoulli(111, (40, 50), .3, "p").numpy(), np.zeros((40, 50), np.float32)),
+             "both_empty": (np.zeros((40, 50), np.float32), np.zeros((40, 50), np.float32)),
+             "all_ones": (np.ones((40, 50), np.float32), np.ones((40, 50), np.float32))}
+    for i in range(4):
+        cases[f"rand{i}"] = (G.bernoulli(120 + i, (256, 256), 0.2 + 0.2 * i, "p").numpy(),
+                             G.bernoulli(130 + i, (256, 256), 0.3, "g").numpy())
+    for name, (pm, gm) in cases.items():
+        r = ev.calculate_metrics(pm, gm)
+        o = O.calculate_metrics(pm, gm)
+        for k in r:
+            assert np.float32(r[k]) == np.float32(o[k]), (name, k)
+        fx[f"metrics/{name}"] = np.array([r[k] for k in ("iou", "dice", "accuracy", "precision",
+                                                         "recall", "specificity")])
+        fx[f"pred/{name}"], fx[f"gt/{name}"] = pm, gm
+    # predict_image with a real image file and a Stage-1 model
+    state = det_state(1, 3, 1, seed=140)
+    model = RU.PGUNet1(3, 1)
+    model.load_state_dict(state)
+    model.eval()
+    ev.model = model
+    img = (G.uniform(141, 45 * 61 * 3, "img").reshape(45, 61, 3) * 256).astype(np.uint8)
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "img.png")
+        Image.fromarray(img).save(path)
+        orig, mask, conf = ev.predict_image(path, target_size=32)
+        resized = Image.open(path).convert("RGB").resize((32, 32))
+    tensor = torch.from_numpy(np.array(resized)).permute(2, 0, 1).float() / 255.0
+    assert np.array_equal(orig, img)
+    with torch.no_grad():
+        logits = O.pgunet_forward(1, {k: v.clone() for k, v in state.items()}, tensor[None],
+                                  training=False)
+    want, probs = O.predict_mask(logits, (45, 61))
+    assert np.array_equal(want.squeeze().numpy(), mask) and probs.mean().item() == conf
+    fx.update(predict_input=tensor.numpy(), predict_mask=mask, predict_conf=np.array(conf),
+              predict_logits=logits.numpy())
+    save_npz("g10_monuseg_eval.npz", **fx)
+
+
 def g0(RU):
     """state_dict keys/shapes/dtypes of every reference model (checkpoint format)."""
     out = {}
@@ -360,15 +716,28 @@ def g0(RU):
 def main():
     torch.set_num_threads(8)
     RU = _ref()
+    only = sys.argv[1:]
+    if only:  # python -m oracle.make_goldens g8 g9 ...
+        for name in only:
+            globals()[name](RU)
+        return
     g0(RU)
     g1(RU, 1)
     g1(RU, 2)
     g2(RU)
     g3(RU)
+    g3b(RU)
     g4(RU)
     g5(RU)
     g6(RU)
     g7(RU)
+    g7b(RU)
+    g7c(RU)
+    g7d(RU)
+    g8(RU)
+    g9(RU)
+    g10(RU)
+    g4b(RU)
 
 
 if __name__ == "__main__":

@@ -227,6 +227,33 @@ def weighted_loss(pixel_loss, umap=None, alpha: float = 1.0):
     return final, torch.mean(pixel_loss).item()
 
 
+# Criterion variants fed to apply_uncertainty_weighted_loss (golden G3b): every
+# reduction of BCEWithLogitsLoss with and without pos_weight / U, a per-channel
+# pos_weight and element weight on a 2-channel output (U broadcast over channels).
+LOSS_CASES = [(red, pw, use_u, a) for red in ("none", "mean", "sum") for pw in (None, 5.0)
+              for use_u, a in ((False, 1.0), (True, 0.5), (True, 2.0))]
+LOSS_CASES_C2 = [("none", "vec_pw"), ("mean", "vec_pw"), ("none", "weight"), ("sum", "weight")]
+
+
+def loss_case_name(red, pw, use_u, alpha):
+    return f"red={red},pw={pw},u={int(use_u)},a={alpha}"
+
+
+def loss_case_criterion(red, pw, device="cpu"):
+    import torch.nn as nn
+    p = None if pw is None else torch.tensor([float(pw)], device=device)
+    return nn.BCEWithLogitsLoss(pos_weight=p, reduction=red)
+
+
+def loss_case_criterion_c2(red, kind, device="cpu"):
+    """2-channel criteria: pos_weight (2,1,1) = [5, 2], or element weight (2,1,1) = [.7, 1.3]."""
+    import torch.nn as nn
+    v = torch.tensor([5.0, 2.0] if kind == "vec_pw" else [0.7, 1.3], device=device).view(2, 1, 1)
+    if kind == "vec_pw":
+        return nn.BCEWithLogitsLoss(pos_weight=v, reduction=red)
+    return nn.BCEWithLogitsLoss(weight=v, reduction=red)
+
+
 # ---------------------------------------------------------------------------
 # Optimiser and metrics (uncertainty_guided_trainer.py:81-123)
 # ---------------------------------------------------------------------------

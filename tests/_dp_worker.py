@@ -1,0 +1,54 @@
+"""One rank of the data-parallel GPU test (tests/test_gpu_dp.py): started as a fresh
+child process per rank (never exec'd from a GPU-initialised process), gloo backend,
+both ranks on cuda:0.  Runs ugpg's trainer exactly as a user would under torchrun:
+constructor (replica broadcast), load_stage_weights (rank 1 loads DIFFERENT weights,
+which the broadcast must overwrite), train_epoch on a global-batch DataLoader (each rank
+keeps its shard), then dumps gradients, parameters, buffers and the epoch tuple."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "ug-pg-unet_amd")]
+
+
+def main(outdir):
+    import torch
+    import torch.distributed as dist
+    from torch.utils.data import DataLoader, TensorDataset
+    from oracle import detgen as G
+    from oracle.make_goldens import G8 as c
+    from tests._parity import det_state, perturbed_state
+    rank = int(os.environ["RANK"])
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo")
+    torch.manual_seed(1000 + rank)               # replicas start different on purpose
+    import ugpg
+    tr = ugpg.UncertaintyGuidedProgressiveTrainer(3, 1, device="cuda", uncertainty_alpha=1.0)
+    p0 = {k: v.detach().cpu().clone() for k, v in tr.models[3].state_dict().items()}
+    stage = c["stage"]
+    state = det_state(stage, 3, 1, seed=c["w_seed"])
+    if rank != 0:
+        state = perturbed_state(state, 77, 1e-2)
+    ck = os.path.join(outdir, f"ck{rank}.pth")
+    torch.save({"model_state_dict": state}, ck)
+    tr.load_stage_weights(stage, ck)             # broadcast: rank 0's weights everywhere
+    tr.models[stage - 1].load_state_dict(det_state(stage - 1, 3, 1, seed=c["prev_seed"]))
+    tr.current_stage, tr.current_model = stage, tr.models[stage]
+    tr.setup_optimizer(stage)
+    x = G.randn(c["x_seed"], (c["B"], 3, c["res"], c["res"]), "x")
+    t = G.bernoulli(c["t_seed"], (c["B"], 1, c["res"], c["res"]), 0.5, "t")
+    tup = tr.train_epoch(DataLoader(TensorDataset(x, t), batch_size=c["B"]), stage)
+    torch.cuda.synchronize()
+    m = tr.models[stage]
+    torch.save({"tuple": tup,
+                "grads": {k: p.grad.detach().cpu() for k, p in m.named_parameters()},
+                "state": {k: v.detach().cpu() for k, v in m.state_dict().items()},
+                "ctor_s3": p0,
+                "ctor_s3_after": {k: v.detach().cpu() for k, v in tr.models[3].state_dict().items()}},
+               os.path.join(outdir, f"rank{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

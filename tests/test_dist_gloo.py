@@ -138,3 +138,94 @@ def test_overlap_reducer_buckets_sum_like_one_allreduce():
         for r in range(WORLD):
             got, want = torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True)
             assert torch.allclose(got, want, rtol=1e-6, atol=1e-6)
+
+
+def _replica_worker(rank, port, outdir):
+    """Trainer constructors under torch.distributed: every rank seeds differently (as
+    unseeded torchrun ranks would) and must still end with rank 0's weights."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "ug-pg-unet_amd")]
+    import torch.distributed as dist
+    from torch.utils.data import DataLoader, TensorDataset
+    from torch.utils.data.distributed import DistributedSampler
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    torch.set_num_threads(2)
+    torch.manual_seed(100 + rank)
+    import ugpg
+    from ugpg.dist import shard_batch
+    from ugpg.herlev import HerlevTrainer
+    tr = ugpg.UncertaintyGuidedProgressiveTrainer(3, 1, device="cpu")
+    ht = HerlevTrainer({"device": "cpu", "epochs_per_stage": 1, "num_classes": 7})
+    sums = {f"seg{s}": [float(p.double().sum()) for p in m.state_dict().values()
+                        if p.is_floating_point()] for s, m in tr.models.items()}
+    sums.update({f"herlev{s}": [float(p.double().sum()) for p in m.state_dict().values()
+                                if p.is_floating_point()] for s, m in ht.models.items()})
+    # batch sharding: contiguous equal shards, remainder dropped, tiny batch skipped,
+    # DistributedSampler batches pass through
+    ds = TensorDataset(torch.arange(5).float().view(5, 1), torch.arange(5).view(5, 1))
+    plain = DataLoader(ds, batch_size=5)
+    (x, y), = list(plain)
+    part = shard_batch(plain, x, y)
+    tiny = shard_batch(plain, x[:1], y[:1])
+    samp = DataLoader(ds, batch_size=2, sampler=DistributedSampler(ds, WORLD, rank, shuffle=False))
+    (xs, ys), *_ = list(samp)
+    through = shard_batch(samp, xs, ys)
+    torch.save({"sums": sums, "part": part[0].view(-1).tolist(), "tiny": tiny,
+                "through": torch.equal(through[0], xs)}, os.path.join(outdir, f"r{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_trainers_start_from_rank0_weights_and_shard_batches():
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_replica_worker, args=(_free_port(), d), nprocs=WORLD, join=True)
+        r = [torch.load(os.path.join(d, f"r{i}.pt"), weights_only=True) for i in range(WORLD)]
+    assert r[0]["sums"] == r[1]["sums"]
+    assert r[0]["part"] == [0.0, 1.0] and r[1]["part"] == [2.0, 3.0]
+    assert r[0]["tiny"] is None and r[1]["tiny"] is None
+    assert r[0]["through"] and r[1]["through"]
+
+
+def _mixed_worker(rank, port, outdir):
+    """allreduce_gradients over a Herlev-like layout: one flat run (the encoder) handed to
+    the OverlapReducer during the backward, plus loose tensors (the head) reduced after."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "ug-pg-unet_amd")]
+    import torch.distributed as dist
+    from ugpg.dist import allreduce_gradients, overlapped_allreduce, overlap_reducer
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    gen = torch.Generator().manual_seed(20 + rank)
+    sizes = [300, 5000, 33, 7]
+    flat = torch.randn(sum(sizes), generator=gen)
+    loose = [torch.randn(n, generator=gen) for n in (512, 256, 7)]
+    want = [t.clone() for t in [flat] + loose]
+    for t in want:
+        dist.all_reduce(t)
+    views, off = [], 0
+    for n in sizes:
+        views.append(flat[off:off + n])
+        off += n
+    params = [torch.nn.Parameter(torch.zeros(n)) for n in sizes + [512, 256, 7]]
+    for p, g in zip(params, views + loose):
+        p.grad = g
+    with overlapped_allreduce():
+        red = overlap_reducer()
+        red.bucket = 1000
+        red.begin(flat, views)
+        red.done(views[::-1])
+        red.flush()
+    assert allreduce_gradients(params, bucket_bytes=4096) == 1.0 / WORLD
+    torch.save(([flat] + loose, want), os.path.join(outdir, f"m{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_allreduce_flat_run_plus_loose_tensors():
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_mixed_worker, args=(_free_port(), d), nprocs=WORLD, join=True)
+        for r in range(WORLD):
+            got, want = torch.load(os.path.join(d, f"m{r}.pt"), weights_only=True)
+            for a, b in zip(got, want):
+                assert torch.allclose(a, b, rtol=1e-6, atol=1e-6)

@@ -68,3 +68,28 @@ def test_tester_end_to_end(dev, tmp_path):
     assert masks.shape == (4, 1, 50, 40)
     assert int((masks.cpu() != want_m).sum()) <= band * 4
     assert torch.allclose(conf.cpu(), probs.mean(dim=(1, 2, 3)), atol=1e-5)
+
+
+def test_predict_image_matches_reference_evaluator(dev):
+    """MoNuSegEvaluator.predict_image run for real by the golden generator (G10): the
+    same resized image tensor through ugpg's tester gives the reference's mask (nearest
+    resize back to 45x61) and confidence."""
+    import ugpg
+    from tests._parity import det_state
+    fx = np.load("tests/golden/g10_monuseg_eval.npz")
+    state = det_state(1, 3, 1, seed=140)
+    model = ugpg.PGUNet1(3, 1)
+    model.load_state_dict(state)
+    tester = ugpg.MoNuSegTester(model=model, device=dev)
+    x = torch.from_numpy(fx["predict_input"])[None]
+    masks, conf = tester.predict(x, out_size=(45, 61))
+    ref_logits = torch.from_numpy(fx["predict_logits"])
+    band = (ref_logits.abs() < 1e-4)
+    want = torch.from_numpy(fx["predict_mask"])
+    got = masks.cpu().squeeze()
+    # pixels whose source logit sits in the +-1e-4 tie band may flip
+    from oracle import ref_cpu as O
+    src_band, _ = O.predict_mask(band.float() * 10.0, (45, 61))
+    sure = src_band.squeeze() == 0
+    assert torch.equal(got[sure], want[sure])
+    assert abs(conf.item() - float(fx["predict_conf"])) <= 1e-6

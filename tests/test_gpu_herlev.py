@@ -133,3 +133,136 @@ def test_trainer_steps_stage4(dev):
     f, metrics = tr.uncertainty_guided_forward_pass(x, y, 4)
     assert set(metrics) == {"final_loss", "base_loss", "output", "uncertainty_weight_mean",
                             "uncertainty_weight_std"}
+
+
+def _reference_trainer(dev, K, cw, alpha, res4):
+    from ugpg.herlev import HerlevTrainer
+    return HerlevTrainer({"device": dev, "epochs_per_stage": 1, "num_classes": K,
+                          "class_weights": cw, "uncertainty_alpha": alpha, "weight_decay": 1e-4,
+                          "stage4_resolution": res4})
+
+
+def _check_grad_stats(m, fx, rtol=2e-3):
+    """Per-tensor gradient norm and sum against the reference's checksums."""
+    named = dict(m.named_parameters())
+    n = 0
+    for key in fx.files:
+        if not key.startswith("grad32/"):
+            continue
+        k = key[len("grad32/"):]
+        g = named[k].grad.detach().double().cpu()
+        norm, tot = fx[key][0], fx[key][1]
+        assert abs(g.norm().item() - norm) <= rtol * norm + 1e-6, (k, g.norm().item(), norm)
+        n += 1
+    assert n > 0
+
+
+def test_reference_trainer_step_224(dev):
+    """HerlevTrainer.uncertainty_guided_forward_pass at the reference's Stage-4 resolution
+    224, bs4, class weights, pinned by the reference trainer itself (G7b)."""
+    fx = np.load("tests/golden/g7b_herlev_trainer_step.npz")
+    tr = _reference_trainer(dev, K, fx["class_weights"].tolist(), 1.0, 224)
+    s4 = G.make_state(O.state_spec(4, 3, 1, key_prefix="unet.") + O.herlev_head_spec(512, K), 75)
+    s3 = G.make_state(O.state_spec(3, 3, 1, key_prefix="unet.") + O.herlev_head_spec(512, K), 76)
+    tr.models[4].load_state_dict(s4)
+    tr.models[3].load_state_dict(s3)
+    tr.models[4].train()
+    for mod in tr.models[4].modules():
+        if isinstance(mod, nn.Dropout):
+            mod.p = 0.0
+    x = G.randn(77, (4, 3, 224, 224), "x").to(dev)
+    y = G.randint(78, (4,), K, "y").to(dev)
+    final, met = tr.uncertainty_guided_forward_pass(x, y, 4)
+    final.backward()
+    want = fx["loss"]
+    got = [met["final_loss"], met["base_loss"], met["uncertainty_weight_mean"],
+           met["uncertainty_weight_std"]]
+    assert abs(got[0] - want[0]) <= 1e-5 * abs(want[0]) and abs(got[1] - want[1]) <= 1e-5 * abs(want[1])
+    assert abs(got[2] - want[2]) <= 1e-5 and abs(got[3] - want[3]) <= 1e-5, (got, want)
+    assert (met["output"].detach().cpu() - torch.from_numpy(fx["logits"])).abs().max().item() <= 1e-3
+    _check_grad_stats(tr.models[4], fx)
+
+
+def test_reference_binary_branch(dev):
+    """The reference's num_classes <= 2 branch (sigmoid uncertainty, broadcast weights), G7d."""
+    fx = np.load("tests/golden/g7d_herlev_binary.npz")
+    tr = _reference_trainer(dev, 2, None, 0.7, 64)
+    s4 = G.make_state(O.state_spec(4, 3, 1, key_prefix="unet.") + O.herlev_head_spec(512, 2), 85)
+    s3 = G.make_state(O.state_spec(3, 3, 1, key_prefix="unet.") + O.herlev_head_spec(512, 2), 86)
+    tr.models[4].load_state_dict(s4)
+    tr.models[3].load_state_dict(s3)
+    tr.models[4].train()
+    for mod in tr.models[4].modules():
+        if isinstance(mod, nn.Dropout):
+            mod.p = 0.0
+    x = G.randn(87, (2, 3, 64, 64), "x").to(dev)
+    y = G.randint(88, (2,), 2, "y").to(dev)
+    final, met = tr.uncertainty_guided_forward_pass(x, y, 4)
+    final.backward()
+    got = [met["final_loss"], met["base_loss"], met["uncertainty_weight_mean"],
+           met["uncertainty_weight_std"]]
+    assert np.allclose(got, fx["loss"], rtol=1e-5, atol=1e-6), (got, fx["loss"])
+    _check_grad_stats(tr.models[4], fx)
+
+
+def test_constructor_probe_matches_reference(dev):
+    """Constructed with the same seed and moved to the GPU, the model's state equals the
+    reference constructor's: initial weights (same RNG draws) and the BatchNorm running
+    statistics / num_batches_tracked left by its probe forward (G7c)."""
+    from ugpg.herlev import HerlevClassificationModel
+    fx = np.load("tests/golden/g7c_herlev_ctor.npz")
+    torch.manual_seed(5)
+    m = HerlevClassificationModel(stage=4, num_classes=K)
+    assert np.array_equal(torch.rand(4).numpy(), fx["rng_after"])
+    m = m.to(dev)
+    n = 0
+    for k, v in m.state_dict().items():
+        if f"buf/{k}" in fx.files:
+            want = fx[f"buf/{k}"]
+            if k.endswith("num_batches_tracked"):
+                assert int(v) == int(want), k
+            else:
+                err = np.abs(v.cpu().numpy() - want).max()
+                assert err <= 1e-5 * max(1.0, np.abs(want).max()), (k, err)
+            n += 1
+    assert n == len([f for f in fx.files if f.startswith("buf/")])
+
+
+@pytest.mark.parametrize("res", [224, 256])
+def test_config4_bs16_parity(dev, res):
+    """BASELINE config 4 at its size: Stage-4 Herlev classifier, bs16, 224^2 (the
+    reference trainer's Stage-4 resolution) and 256^2, train mode (dropout off), UG CE
+    loss with class weights: logits, loss and every gradient vs the fp64 oracle (§8d rule)."""
+    from ugpg.herlev import _CEUGFn
+    B = 16
+    state = herlev_state(seed=90)
+    m = build(state, dev).train()
+    for mod in m.modules():
+        if isinstance(mod, nn.Dropout):
+            mod.p = 0.0
+    x = G.randn(91, (B, 3, res, res), "x")
+    y = G.randint(92, (B,), K, "y")
+    prev = G.randn(93, (B, K), "prev")
+    cw = torch.linspace(0.5, 2.0, K)
+    out = m(x.to(dev))
+    buf = torch.empty(5, device=dev)
+    final = _CEUGFn.apply(out, y.to(dev), prev.to(dev), cw.to(dev), 1.0, buf)
+    final.backward()
+    o32, f32, _, _, g32 = oracle(state, x, y, prev, cw)
+    _, f64, _, _, g64 = oracle(state, x, y, prev, cw, torch.float64)
+    assert (out.detach().cpu() - o32).abs().max().item() <= 1e-3
+    assert abs(buf[0].item() - f64.item()) <= 1e-5 * abs(f64.item())
+    floor = {k: (g32[k].double() - g64[k]).abs().max().item() for k in g32}
+    for s, rel in ((7, 1e-7), (10, 1e-6), (12, 5e-6)):
+        _, _, _, _, gp = oracle(perturbed_state(state, s, rel), x, y, prev, cw)
+        for k in floor:
+            floor[k] = max(floor[k], (gp[k].double() - g64[k]).abs().max().item())
+    named = dict(m.named_parameters())
+    bad, ratios = [], []
+    for k in g32:
+        ok, err, bound = grad_check(k, named[k].grad, g32[k], g64[k], floor[k])
+        ratios.append((err / bound, k))
+        if not ok:
+            bad.append(f"{k}: {err:.3e} > {bound:.3e}")
+    print(f"herlev {res}: gradient headroom (err/bound) worst 3 {sorted(ratios, reverse=True)[:3]}")
+    assert not bad, "\n".join(bad)

@@ -109,6 +109,36 @@ def test_ug_loss_alpha_sweep_golden(dev):
         assert abs(f.item() - fin) <= 1e-5 * abs(fin) and abs(b - base) <= 1e-5 * abs(base)
 
 
+def test_ug_loss_reductions_golden(dev):
+    """apply_uncertainty_weighted_loss honours the criterion's reduction and
+    per-channel pos_weight/weight exactly as the reference (G3b), and its gradient
+    w.r.t. the logits matches the oracle's autograd of the same expression."""
+    from tests.test_oracle_golden import _g3b_inputs
+    from ugpg.loss import UncertaintyGuidedLoss
+    fx = np.load("tests/golden/g3b_loss_reduction.npz")
+    out, t, u, out2, t2, u2 = _g3b_inputs()
+    L = UncertaintyGuidedLoss(dev)
+    cases = [(O.loss_case_name(r, p, uu, a), O.loss_case_criterion(r, p),
+              O.loss_case_criterion(r, p, dev), out, t, u if uu else None, a)
+             for r, p, uu, a in O.LOSS_CASES]
+    cases += [(f"c2,red={r},{k},u={int(uu)}", O.loss_case_criterion_c2(r, k),
+               O.loss_case_criterion_c2(r, k, dev), out2, t2, u2 if uu else None, 1.5)
+              for r, k in O.LOSS_CASES_C2 for uu in (False, True)]
+    for name, crit_cpu, crit, o, tt, uu, a in cases:
+        xo = o.clone().requires_grad_(True)
+        f_ref, _ = O.weighted_loss(crit_cpu(xo, tt), uu, a)
+        f_ref.backward()
+        xd = o.to(dev).requires_grad_(True)
+        f, b = L.apply_uncertainty_weighted_loss(crit, xd, tt.to(dev),
+                                                 None if uu is None else uu.to(dev), a)
+        f.backward()
+        fin, base = fx[name]
+        assert abs(f.item() - fin) <= 1e-5 * abs(fin), (name, f.item(), fin)
+        assert abs(b - base) <= 1e-5 * abs(base), (name, b, base)
+        g, gr = xd.grad.cpu(), xo.grad
+        assert (g - gr).abs().max().item() <= 1e-5 * gr.abs().max().item() + 1e-12, name
+
+
 def test_trainer_epoch_golden(dev):
     """trainer.train_epoch on a 1-batch loader == the reference's 6-tuple (G6)."""
     import json

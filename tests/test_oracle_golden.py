@@ -71,6 +71,46 @@ def test_g3_weighted_loss():
         assert near(f.item(), fin) and near(b, base)
 
 
+def _g3b_inputs():
+    out = G.randn(30, (2, 1, 64, 64), "logits")
+    t = G.bernoulli(31, (2, 1, 64, 64), 0.3, "t")
+    u = torch.from_numpy(G.uniform(32, 2 * 64 * 64, "u").reshape(2, 1, 64, 64)).float()
+    out2 = G.randn(33, (2, 2, 32, 32), "logits2")
+    t2 = G.bernoulli(34, (2, 2, 32, 32), 0.3, "t2")
+    u2 = torch.from_numpy(G.uniform(35, 2 * 32 * 32, "u2").reshape(2, 1, 32, 32)).float()
+    return out, t, u, out2, t2, u2
+
+
+def test_g3b_weighted_loss_reductions():
+    """The reference's weighting for reduction='mean'/'sum' criteria (scalar pixel loss
+    broadcast against 1+aU) and 2-channel criteria with per-channel pos_weight/weight."""
+    fx = np.load(GOLD + "g3b_loss_reduction.npz")
+    out, t, u, out2, t2, u2 = _g3b_inputs()
+    n = 0
+    for red, pw, use_u, a in O.LOSS_CASES:
+        f, b = O.weighted_loss(O.loss_case_criterion(red, pw)(out, t), u if use_u else None, a)
+        assert near([f.item(), b], fx[O.loss_case_name(red, pw, use_u, a)]), (red, pw, use_u, a)
+        n += 1
+    for red, kind in O.LOSS_CASES_C2:
+        for use_u in (False, True):
+            f, b = O.weighted_loss(O.loss_case_criterion_c2(red, kind)(out2, t2),
+                                   u2 if use_u else None, 1.5)
+            assert near([f.item(), b], fx[f"c2,red={red},{kind},u={int(use_u)}"])
+            n += 1
+    assert n == len(fx.files)
+
+
+def test_g4_logits256_train_mode():
+    """The reference's PGUNet4 train-mode logits at 256^2 (bs1) -- the only full-size
+    network pin besides the U map."""
+    fx = np.load(GOLD + "g4_pgunet4.npz")
+    state = det_state(4, 3, 1)
+    x256 = G.randn(41, (1, 3, 256, 256), "x256")
+    with torch.no_grad():
+        o = O.pgunet_forward(4, {k: v.clone() for k, v in state.items()}, x256, training=True)
+    assert near(o.numpy(), fx["logits256"], 1e-5, 1e-5)
+
+
 def test_g4_pgunet4_small():
     fx = np.load(GOLD + "g4_pgunet4.npz")
     state = det_state(4, 3, 1)
@@ -135,3 +175,96 @@ def test_g7_herlev():
     for k in keys:
         if P[k].grad is not None:
             assert near(stats(k, P[k].grad), fx[f"grad32/{k}"], 1e-3, 1e-5 if is_prebn_bias(k) else 1e-8), k
+
+
+def test_g7b_herlev_trainer_step():
+    """The oracle's Herlev step equals the reference HerlevTrainer's own forward pass
+    (train_herlev.py:216-296, stage 4 at 224^2, class weights, dropout off)."""
+    fx = np.load(GOLD + "g7b_herlev_trainer_step.npz")
+    K, cw = 7, torch.from_numpy(fx["class_weights"])
+    s4 = G.make_state(O.state_spec(4, 3, 1, key_prefix="unet.") + O.herlev_head_spec(512, K), 75)
+    x = G.randn(77, (4, 3, 224, 224), "x")
+    y = G.randint(78, (4,), K, "y")
+    assert torch.equal(y, torch.from_numpy(fx["y"]))
+    P = {k: v.clone() for k, v in s4.items()}
+    keys = param_keys(P)
+    for k in keys:
+        P[k].requires_grad_(True)
+    out = O.herlev_forward(4, P, x, training=True)
+    f, b, w = O.herlev_ug_loss(out, y, torch.from_numpy(fx["prev_logits"]), 1.0, K, cw)
+    f.backward()
+    assert near(out.detach().numpy(), fx["logits"], 1e-5, 1e-6)
+    assert near([f.item(), b.item(), w.mean().item(), w.std().item()], fx["loss"])
+    for k in keys:
+        if P[k].grad is not None:
+            assert near(stats(k, P[k].grad), fx[f"grad32/{k}"], 1e-3, 1e-5 if is_prebn_bias(k) else 1e-8), k
+
+
+def test_g7c_herlev_constructor_rng_parity():
+    """ugpg.HerlevClassificationModel draws the reference's probe image at the same point
+    of construction: same RNG position afterwards, same initial weights (train_herlev.py:
+    48-77).  The probe's BatchNorm update itself runs on the GPU (test_gpu_herlev.py)."""
+    from ugpg.herlev import HerlevClassificationModel
+    fx = np.load(GOLD + "g7c_herlev_ctor.npz")
+    torch.manual_seed(5)
+    m = HerlevClassificationModel(stage=4, num_classes=7)
+    assert np.array_equal(torch.rand(4).numpy(), fx["rng_after"])
+    for k, v in m.state_dict().items():
+        if f"sum/{k}" in fx.files:
+            # identical weights; the float64 sum's last bits depend on the thread count
+            assert near(v.double().sum().item(), float(fx[f"sum/{k}"]), 1e-12, 1e-12), k
+
+
+def test_g8_dp_shard_semantics_oracle():
+    """Mean of per-shard local-BN gradients (the DP step) from the oracle == the
+    reference's (G8)."""
+    from oracle.make_goldens import G8 as c
+    fx = np.load(GOLD + "g8_dp_shards.npz")
+    state = det_state(c["stage"], 3, 1, seed=c["w_seed"])
+    prev = det_state(c["stage"] - 1, 3, 1, seed=c["prev_seed"])
+    x = G.randn(c["x_seed"], (c["B"], 3, c["res"], c["res"]), "x")
+    t = G.bernoulli(c["t_seed"], (c["B"], 1, c["res"], c["res"]), 0.5, "t")
+    per = c["B"] // c["shards"]
+    gs = []
+    for r in range(c["shards"]):
+        xs, ts = x[r * per:(r + 1) * per], t[r * per:(r + 1) * per]
+        u = O.uncertainty_map(1, prev, xs, 32, 64)
+        _, _, _, g, _ = oracle_run(c["stage"], state, xs, ts, umap=u)
+        gs.append(g)
+    for k in param_keys(state):
+        avg = sum(g[k] for g in gs) / c["shards"]
+        assert near(stats(k, avg), fx[f"avg_grad/{k}"], 1e-3, 1e-5 if is_prebn_bias(k) else 1e-8), k
+
+
+def test_g9_rng_stream_parity():
+    """Building ugpg's ProgressiveUNet / trainer / transfer_weights consumes the global RNG
+    exactly like the reference (DataLoader shuffles and augmentation seeds stay in step)."""
+    import ugpg
+    gold = json.load(open(GOLD + "g9_rng.json"))
+    torch.manual_seed(0)
+    ugpg.ProgressiveUNet(3, 1)
+    assert torch.rand(4).tolist() == gold["after_progressive_unet"]
+    torch.manual_seed(1)
+    tr = ugpg.UncertaintyGuidedProgressiveTrainer(3, 1, device="cpu")
+    assert torch.rand(4).tolist() == gold["after_trainer_ctor"]
+    tr.transfer_weights(1, 2)
+    assert torch.rand(4).tolist() == gold["after_transfer_1_2"]
+
+
+def test_g10_monuseg_evaluator_metrics():
+    """MoNuSegEvaluator.calculate_metrics run for real (cv2 stubbed when generating):
+    the oracle restatement and ugpg's host API reproduce it exactly (float32)."""
+    from ugpg.evaluation import calculate_metrics
+    fx = np.load(GOLD + "g10_monuseg_eval.npz")
+    keys = ("iou", "dice", "accuracy", "precision", "recall", "specificity")
+    names = [k.split("/", 1)[1] for k in fx.files if k.startswith("metrics/")]
+    assert len(names) == 8
+    for n in names:
+        want = fx[f"metrics/{n}"]
+        for impl in (O.calculate_metrics, calculate_metrics):
+            got = impl(fx[f"pred/{n}"], fx[f"gt/{n}"])
+            assert [np.float32(got[k]) for k in keys] == [np.float32(v) for v in want], (n, impl)
+    # predict_image's mask rule on the reference's own logits
+    m, probs = O.predict_mask(torch.from_numpy(fx["predict_logits"]), (45, 61))
+    assert np.array_equal(m.squeeze().numpy(), fx["predict_mask"])
+    assert probs.mean().item() == float(fx["predict_conf"])

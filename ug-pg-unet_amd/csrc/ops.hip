@@ -810,6 +810,46 @@ __global__ void predict_mask_kernel(const float* x, int B, int H, int W, float* 
     }
 }
 
+// ---- data-parallel metrics (SURVEY §5 "metrics all-reduced under DP")
+// A rank's metrics buffer m[0..n) holds per-rank means (bit i of avg_mask), counts
+// (summed as is) and one (mean, unbiased std) pair at [ip, ip+1) over n_stat values.
+// pack -> double sums[n + 2] (the pair as n*mean and M2 + n*mean^2, then n_stat and a
+// rank count of 1); after a SUM all-reduce, unpack writes the global metrics back.
+__global__ void metrics_pack_kernel(const float* m, int n, int ip, double n_stat, double* sums) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        double v = m[i];
+        if (ip >= 0 && i == ip) {
+            v = n_stat * (double)m[ip];
+        } else if (ip >= 0 && i == ip + 1) {
+            const double mu = m[ip], sd = m[ip + 1];
+            v = (n_stat > 1 ? sd * sd * (n_stat - 1) : 0.0) + n_stat * mu * mu;
+        }
+        sums[i] = v;
+    }
+    if (threadIdx.x == 0) {
+        sums[n] = n_stat;
+        sums[n + 1] = 1.0;
+    }
+}
+
+__global__ void metrics_unpack_kernel(const double* sums, int n, int ip, unsigned avg_mask,
+                                      float* m) {
+    const double ranks = sums[n + 1], N = sums[n];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        double v = sums[i];
+        if (ip >= 0 && i == ip) {
+            v = N > 0 ? sums[ip] / N : 0.0;
+        } else if (ip >= 0 && i == ip + 1) {
+            const double mu = N > 0 ? sums[ip] / N : 0.0;
+            const double M2 = sums[ip + 1] - N * mu * mu;
+            v = N > 1 ? sqrt(fmax(M2, 0.0) / (N - 1)) : 0.0;
+        } else if (i < 32 && ((avg_mask >> i) & 1u)) {
+            v /= ranks;
+        }
+        m[i] = (float)v;
+    }
+}
+
 __global__ void __launch_bounds__(256) mean_std_part_kernel(const float* x, int64_t n,
                                                             int64_t per, double* part) {
     const int64_t p0 = blockIdx.x * per, p1 = min(n, p0 + per);
@@ -1275,6 +1315,22 @@ extern "C" int ugpg_predict_mask(const float* x, int B, int H, int W, float* mas
     hipLaunchKernelGGL(predict_mask_kernel, dim3(stream_grid((int64_t)B * Ho * Wo)), dim3(256), 0,
                        as_stream(stream), x, B, H, W, mask, Ho, Wo);
     return check_launch("predict_mask");
+}
+
+extern "C" int ugpg_metrics_pack(const float* m, int n, int ip, double n_stat, double* sums,
+                                 void* stream) {
+    UGPG_REQUIRE(m && sums && n > 0 && n <= 32 && ip < n - 1 && n_stat >= 0, "metrics_pack");
+    hipLaunchKernelGGL(metrics_pack_kernel, dim3(1), dim3(64), 0, as_stream(stream), m, n, ip,
+                       n_stat, sums);
+    return check_launch("metrics_pack");
+}
+
+extern "C" int ugpg_metrics_unpack(const double* sums, int n, int ip, unsigned avg_mask, float* m,
+                                   void* stream) {
+    UGPG_REQUIRE(m && sums && n > 0 && n <= 32 && ip < n - 1, "metrics_unpack");
+    hipLaunchKernelGGL(metrics_unpack_kernel, dim3(1), dim3(64), 0, as_stream(stream), sums, n,
+                       ip, avg_mask, m);
+    return check_launch("metrics_unpack");
 }
 
 extern "C" size_t ugpg_mean_std_workspace(int64_t n) {

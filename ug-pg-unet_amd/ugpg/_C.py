@@ -80,6 +80,8 @@ SIGNATURES = {
     "ugpg_predict_mask": (_i, [_p, _i, _i, _i, _p, _i, _i, _p]),
     "ugpg_mean_std_workspace": (_sz, [_i64]),
     "ugpg_mean_std": (_i, [_p, _i64, _p, _p, _sz, _p]),
+    "ugpg_metrics_pack": (_i, [_p, _i, _i, C.c_double, _p, _p]),
+    "ugpg_metrics_unpack": (_i, [_p, _i, _i, C.c_uint, _p, _p]),
     "ugpg_rmsprop_step": (_i, [_p, _p, _p, _i64, _f, _f, _f, _f, _f, _p]),
     "ugpg_avgpool_fwd": (_i, [Src, _i, _i, _p, _p]),
     "ugpg_avgpool_bwd": (_i, [_p, _i, _i, _i, _p, _i, _p]),

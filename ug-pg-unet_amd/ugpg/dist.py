@@ -153,27 +153,59 @@ def overlap_reducer() -> OverlapReducer | None:
     return _REDUCER
 
 
+def _runs(grads):
+    """Split `grads` (in order) into maximal back-to-back runs of one storage."""
+    runs, cur = [], []
+    for g in grads:
+        if cur and contiguous_run(cur + [g]) is None:
+            runs.append(cur)
+            cur = []
+        cur.append(g)
+    if cur:
+        runs.append(cur)
+    return runs
+
+
+def _allreduce_runs(grads, bucket_bytes):
+    """One SUM all-reduce per flat run (bucketed); loose tensors (a run of one, e.g.
+    the Herlev head's weights) are packed into one staging buffer and reduced together."""
+    loose = []
+    step = max(1, bucket_bytes // 4)
+    for run in _runs(grads):
+        flat = contiguous_run(run) if len(run) > 1 else None
+        if flat is None:
+            loose.extend(run)
+            continue
+        base, _, n = flat
+        for off in range(0, n, step):
+            dist.all_reduce(base[off:off + step])
+    if loose:
+        stage = torch.cat([g.reshape(-1) for g in loose])
+        dist.all_reduce(stage)
+        off = 0
+        for g in loose:
+            g.copy_(stage[off:off + g.numel()].view_as(g))
+            off += g.numel()
+
+
 def allreduce_gradients(params, bucket_bytes: int = 64 << 20):
-    """Sum gradients over ranks.  If the backward already issued them through the
-    OverlapReducer, only wait for those buckets; else one call when the grads form
-    a single flat run (the normal ugpg layout), otherwise per-tensor calls.
+    """Sum gradients over ranks.  Gradients the backward already handed to the
+    OverlapReducer are only waited for; the rest go out as one call per flat run
+    (the normal ugpg layout is a single run) plus one call for loose tensors.
     Returns the scale (1/world_size) the optimizer must apply."""
     _, ws = world()
     grads = [p.grad for p in params if p.grad is not None]
     if ws <= 1 or not grads:
         return 1.0
     red = _REDUCER
-    if red is not None and red.pending_for(grads):
-        return red.wait()
-    run = contiguous_run(grads)
-    if run is not None:
-        base, _, n = run
-        step = max(1, bucket_bytes // 4)
-        for off in range(0, n, step):
-            dist.all_reduce(base[off:off + step])
-    else:
-        for g in grads:
-            dist.all_reduce(g)
+    pending = red is not None and red.flat is not None
+    if pending:
+        ptr = red.flat.untyped_storage().data_ptr()
+        grads = [g for g in grads if g.untyped_storage().data_ptr() != ptr]
+    if grads:
+        _allreduce_runs(grads, bucket_bytes)
+    if pending:
+        red.wait()
     return 1.0 / ws
 
 
@@ -184,6 +216,58 @@ def broadcast_parameters(module: torch.nn.Module, src: int = 0):
         return
     for t in list(module.parameters()) + list(module.buffers()):
         dist.broadcast(t.data, src)
+
+
+def broadcast_buffers(module: torch.nn.Module, src: int = 0):
+    """BatchNorm running statistics and num_batches_tracked from rank `src` (SURVEY §8e:
+    local BN in the step; replicas agree at validation, stage end and checkpoints)."""
+    _, ws = world()
+    if ws <= 1:
+        return
+    for t in module.buffers():
+        dist.broadcast(t.data, src)
+
+
+def allreduce_metrics(mbuf, ip: int, n_stat: float, avg_mask: int):
+    """Turn this rank's device metrics buffer into the global-batch metrics in place:
+    per-rank means (bits of avg_mask) are averaged (equal shards), counts summed, and
+    the (mean, unbiased std) pair at [ip, ip+1) pooled over all ranks' n_stat values.
+    One float64 SUM all-reduce of n+2 values (libugpg metrics_pack/unpack kernels)."""
+    _, ws = world()
+    if ws <= 1:
+        return mbuf
+    from . import ops
+    sums = ops.metrics_pack(mbuf, ip, n_stat)
+    dist.all_reduce(sums)
+    return ops.metrics_unpack(sums, mbuf, ip, avg_mask)
+
+
+def _has_distributed_sampler(loader) -> bool:
+    from torch.utils.data.distributed import DistributedSampler
+    for attr in ("sampler", "batch_sampler"):
+        s = getattr(loader, attr, None)
+        if isinstance(s, DistributedSampler) or isinstance(getattr(s, "sampler", None),
+                                                           DistributedSampler):
+            return True
+    return False
+
+
+def shard_batch(loader, *tensors):
+    """This rank's contiguous equal shard of a global batch drawn from `loader`.
+
+    With a DistributedSampler the loader already yields per-rank batches, so they pass
+    through.  Otherwise every rank draws the same global batch (same seed) and keeps
+    rows [r*b, (r+1)*b), b = len // world_size; a remainder that does not divide is
+    dropped (DistributedSampler(drop_last=True) semantics), and a batch smaller than
+    the world size yields None on every rank (skipped consistently)."""
+    rank, ws = world()
+    if ws <= 1 or _has_distributed_sampler(loader):
+        return tensors
+    n = tensors[0].shape[0]
+    per = n // ws
+    if per == 0:
+        return None
+    return tuple(t[rank * per:(rank + 1) * per] for t in tensors)
 
 
 def max_over_ranks(value: float, device=None) -> float:

@@ -93,7 +93,13 @@ class _PooledFeaturesFn(torch.autograd.Function):
         B, H, W, C = ctx.act_shape
         da = torch.empty(B, H, W, C, dtype=torch.float32, device=dfeat.device)
         ops.avgpool_bwd(dfeat.contiguous(), H, W, da)
-        dx = ctx.graph.backward(ctx.state, grads, dout_act=da, need_dx=need[1])
+        red = overlap_reducer()
+        if red is not None and grads:
+            red.begin(_flat_of(views), list(grads.values()))
+        dx = ctx.graph.backward(ctx.state, grads, dout_act=da, need_dx=need[1],
+                                on_done=red.done if red is not None and grads else None)
+        if red is not None and grads:
+            red.flush()
         ctx.state = None
         return (None, dx, *views)
 

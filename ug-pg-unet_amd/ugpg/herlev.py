@@ -8,10 +8,14 @@ the head (Dropout -> Linear 512 -> ReLU -> Dropout -> Linear 256 -> ReLU ->
 Dropout -> Linear K) runs on ugpg linear/dropout kernels.  state_dict keys are the
 reference's (`unet.*`, `classifier.{3,6,9}.*`).
 
-Difference to the reference, documented in DESIGN.md: the reference constructor
-runs a probe forward on a random image only to read the feature width (always
-512 for these encoders) -- which also nudges BatchNorm running statistics and
-consumes the global RNG.  ugpg sets the width statically and does not probe.
+Constructor side effect: the reference runs a probe forward of the encoder on
+``torch.randn(1, 3, res, res)`` to read the feature width (train_herlev.py:59-63).
+That draws from the global RNG and, the module being in train mode, moves every
+encoder BatchNorm's running statistics once (num_batches_tracked = 1).  ugpg draws
+the same probe image at the same point of construction (so the RNG stream and the
+classifier's initial weights equal the reference's) and runs the probe on the GPU
+encoder the first time the model is moved to a ROCm device -- the state_dict of a
+constructed-and-moved model therefore matches the reference's.
 """
 from __future__ import annotations
 
@@ -22,13 +26,16 @@ from datetime import datetime
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from . import functional as Fn
 from . import ops
 from .flat import ensure_flat
 from .loss import UncertaintyGuidedLoss
+from .dist import (allreduce_gradients, allreduce_metrics, broadcast_buffers,
+                   broadcast_parameters, overlapped_allreduce, shard_batch, world)
 from .optim import Adam
-from .unet import STAGE_CLASSES, _LAYOUT
+from .unet import STAGE_CLASSES, STAGE_RESOLUTIONS, _LAYOUT
 
 FEATURE_DIM = 512  # output width of inc (stage 1) / down3 (stages 2-4)
 
@@ -104,6 +111,9 @@ class HerlevClassificationModel(nn.Module):
             if "model_state_dict" in sd:
                 sd = sd["model_state_dict"]
             self.unet.load_state_dict(sd)
+        # the reference's feature-width probe: same RNG draw, same point (train_herlev.py:59-63)
+        res = STAGE_RESOLUTIONS[stage]
+        self._probe = torch.randn(1, 3, res, res)
         self.classifier = nn.Sequential(
             nn.AdaptiveAvgPool2d(1), nn.Flatten(), nn.Dropout(0.5), nn.Linear(FEATURE_DIM, 512),
             nn.ReLU(), nn.Dropout(0.3), nn.Linear(512, 256), nn.ReLU(), nn.Dropout(0.2),
@@ -111,6 +121,31 @@ class HerlevClassificationModel(nn.Module):
         if pretrained_unet_path:
             self._freeze_encoder()
         self._enc = None
+
+    def _apply(self, fn, *args, **kwargs):
+        out = super()._apply(fn, *args, **kwargs)
+        probe = self.__dict__.get("_probe")
+        if probe is not None and next(self.unet.parameters()).is_cuda:
+            self._probe = None
+            self._run_probe(probe)
+        return out
+
+    def load_state_dict(self, state_dict, strict=True, assign=False):
+        # the reference probes before any load, so a load that sets every encoder
+        # buffer supersedes the probe's BatchNorm update
+        if all(f"unet.{k}" in state_dict for k, _ in self.unet.named_buffers()):
+            self._probe = None
+        return super().load_state_dict(state_dict, strict=strict, assign=assign)
+
+    def _run_probe(self, probe):
+        """Encoder forward in train mode (a freshly built module's mode) on the probe
+        image, no grad: BatchNorm statistics move as in the reference's constructor."""
+        was = self.unet.training
+        self.unet.train(True)
+        with torch.no_grad():
+            dev = next(self.unet.parameters()).device
+            self._extract_features(probe.to(dev))
+        self.unet.train(was)
 
     def _freeze_encoder(self):
         for p in self.unet.parameters():
@@ -170,6 +205,9 @@ class HerlevTrainer:
         self.history = {k: [] for k in ("train_loss", "val_loss", "train_acc", "val_acc",
                                         "uncertainty_weights_mean", "uncertainty_weights_std",
                                         "base_loss", "stage_transitions")}
+        if world()[1] > 1:  # data parallel: every replica starts from rank 0's weights
+            for m in self.models.values():
+                broadcast_parameters(m)
 
     def setup_loss_function(self):
         cw = self.config.get("class_weights")
@@ -203,11 +241,33 @@ class HerlevTrainer:
             with torch.no_grad():
                 prev = pm(ops.resize_nchw(data.float().contiguous(), r, r, ops.RESIZE_BILINEAR))
         if self.config["num_classes"] <= 2:
-            raise NotImplementedError("binary Herlev heads are not supported (the reference's "
-                                      "binary branch mis-broadcasts the sample weights)")
+            return self._forward_binary(output, target, prev)
         out = torch.empty(5, dtype=torch.float32, device=output.device)
         final = _CEUGFn.apply(output, target.contiguous(), prev, self.class_weights,
                               float(self.uncertainty_alpha), out)
+        return output, final, out
+
+    def _forward_binary(self, output, target, prev):
+        """The reference's num_classes <= 2 branch (train_herlev.py:258-261, 266-285):
+        U = 1 - 2|sigmoid(prev) - 0.5| per logit, weights 1 + alpha*U.squeeze(), per-sample
+        CE times the weights under torch broadcasting, mean.  The logits are (B, <=2), so
+        this tail runs as torch device ops with the reference's exact expression --
+        including its broadcast (an error for 2 logits unless B <= 2, as in the
+        reference).  Same 5-float metrics buffer as the fused multi-class kernel."""
+        base = self.criterion(output, target)
+        if prev is None:
+            final, w = base, None
+        else:
+            u = 1.0 - 2.0 * torch.abs(torch.sigmoid(prev) - 0.5)
+            w = 1.0 + self.uncertainty_alpha * u.squeeze()
+            if w.dim() == 0:
+                w = w.unsqueeze(0)
+            final = torch.mean(F.cross_entropy(output, target, reduction="none") * w.detach())
+        zero = torch.zeros((), device=output.device)
+        correct = output.argmax(dim=1).eq(target.view(-1)).sum().float()
+        out = torch.stack([final.detach(), base.detach(),
+                           w.mean() if w is not None else zero,
+                           w.std() if w is not None else zero, correct]).float()
         return output, final, out
 
     def uncertainty_guided_forward_pass(self, data, target, stage):
@@ -222,33 +282,48 @@ class HerlevTrainer:
         opt = self.optimizers[stage]
         opt.zero_grad()
         _, final, out = self._forward_device(data, target, stage)
-        final.backward()
-        from .dist import allreduce_gradients
+        with overlapped_allreduce():  # encoder gradient buckets go out during the backward
+            final.backward()
         opt.grad_scale = allreduce_gradients([p for g in opt.param_groups for p in g["params"]])
         opt.step()
+        self._reduce_metrics(out, data.shape[0], stage)
         return out
+
+    @staticmethod
+    def _reduce_metrics(out, batch, stage):
+        """Data parallel: [final, base] averaged over ranks, the weight mean/std pooled
+        over the global batch, the correct count summed (one all-reduce)."""
+        allreduce_metrics(out, 2, batch if stage > 1 else 0, 0b11)
 
     def _epoch(self, dataloader, stage, train):
         model = self.models[stage]
         model.train(train)
         if stage > 1:
             self.models[stage - 1].eval()
-        tot, correct, total = [0.0] * 4, 0, 0
+        rank, ws = world()
+        if not train and ws > 1:
+            broadcast_buffers(model)  # every rank validates rank 0's BatchNorm state
+        tot, correct, total, skipped = [0.0] * 4, 0, 0, 0
         for data, target in dataloader:
-            data = data.to(self.device, non_blocking=True).float()
-            target = target.to(self.device, non_blocking=True)
+            part = shard_batch(dataloader, data, target)
+            if part is None:
+                skipped += 1
+                continue
+            data = part[0].to(self.device, non_blocking=True).float()
+            target = part[1].to(self.device, non_blocking=True)
             if train:
                 out = self.train_step(data, target, stage)
             else:
                 with torch.no_grad():
                     _, _, out = self._forward_device(data, target, stage)
+                    self._reduce_metrics(out, data.shape[0], stage)
             v = out.tolist()
             tot = [a + b for a, b in zip(tot, (v[0], v[1], v[2] if stage > 1 else 0.0,
                                                v[3] if stage > 1 else 0.0))]
-            correct += int(v[4])
-            total += target.shape[0]
-        n = len(dataloader)
-        return tot[0] / n, tot[1] / n, 100.0 * correct / total, tot[2] / n, tot[3] / n
+            correct += int(round(v[4]))
+            total += target.shape[0] * ws
+        n = max(len(dataloader) - skipped, 1)
+        return tot[0] / n, tot[1] / n, 100.0 * correct / max(total, 1), tot[2] / n, tot[3] / n
 
     def train_epoch(self, dataloader, stage):
         return self._epoch(dataloader, stage, True)
@@ -264,7 +339,6 @@ class HerlevTrainer:
         improves, early stop after `early_stopping_patience` (15) epochs without one,
         and the history JSON at the end.  Checkpoints carry the reference's keys."""
         os.makedirs(save_dir, exist_ok=True)
-        from .dist import world
         rank, _ = world()
         for stage in self.config["stages"]:
             print(f"\n{'=' * 60}")
@@ -310,6 +384,7 @@ class HerlevTrainer:
                 if stale >= self.config.get("early_stopping_patience", 15):
                     print(f"Early stopping after {stale} epochs without improvement")
                     break
+            broadcast_buffers(self.models[stage])  # the next stage's U producer: one BN state
             self.history["stage_transitions"].append(
                 {"stage": stage, "completed_at": datetime.now().isoformat(),
                  "best_val_acc": best_val_acc, "best_val_loss": best_val_loss})

@@ -21,11 +21,32 @@ def _pos_weight_tensor(loss_fn, like):
     pw = getattr(loss_fn, "pos_weight", None)
     if pw is None:
         return None
-    if pw.numel() != 1:
-        raise NotImplementedError("ugpg: only a scalar pos_weight is supported")
     if pw.device != like.device or pw.dtype != torch.float32:
         pw = pw.to(device=like.device, dtype=torch.float32)
     return pw.contiguous()
+
+
+def _fusable_bce(loss_fn, output, target, u):
+    """The fused kernel computes BCE-with-logits(pos_weight) per element with a
+    scalar pos_weight and reduction='none', weighted and averaged in one pass."""
+    if not isinstance(loss_fn, nn.BCEWithLogitsLoss) or loss_fn.weight is not None:
+        return False
+    if loss_fn.reduction != "none" or output.shape != target.shape:
+        return False
+    pw = getattr(loss_fn, "pos_weight", None)
+    if pw is not None and pw.numel() != 1:
+        return False
+    return _kernel_layout(output, u)
+
+
+def _kernel_layout(pixel, u):
+    """(B, c, *spatial) element map with U either absent or (B, 1|c, *spatial)."""
+    if pixel.dim() < 2 or pixel.numel() == 0:
+        return False
+    if u is None:
+        return True
+    return (u.dim() == pixel.dim() and u.shape[0] == pixel.shape[0]
+            and u.shape[2:] == pixel.shape[2:] and u.shape[1] in (1, pixel.shape[1]))
 
 
 class _UGBCEFn(torch.autograd.Function):
@@ -68,18 +89,37 @@ class _WeightedMeanFn(torch.autograd.Function):
 
 def weighted_loss_tensors(loss_fn, output, target, uncertainty_map=None, alpha=1.0, out=None):
     """Device-side (final_loss, base_loss) -- no host synchronisation.  `out`: optional
-    2-float device buffer receiving [final, base] (BCE path)."""
+    2-float device buffer receiving [final, base] (fused BCE path).
+
+    Semantics are the reference's (UG_unet.py:78-94) for any criterion:
+    ``pixel = loss_fn(output, target)``; ``final = mean(pixel * (1 + alpha*U))`` (plain
+    ``mean(pixel)`` without U); ``base = mean(pixel)``.  With ``reduction='mean'|'sum'``
+    the criterion already returns a scalar s, so final = s * mean(1 + alpha*U)."""
     u = None
     if uncertainty_map is not None:
         u = uncertainty_map.detach().contiguous().float()
         alpha_eff = float(alpha)
     else:
         alpha_eff = 0.0
-    if isinstance(loss_fn, nn.BCEWithLogitsLoss) and loss_fn.weight is None:
+    if _fusable_bce(loss_fn, output, target, u):
         pw = _pos_weight_tensor(loss_fn, output)
         return _UGBCEFn.apply(output, target, u, pw, alpha_eff, out)
     pixel_loss = loss_fn(output, target)
-    return _WeightedMeanFn.apply(pixel_loss, u, alpha_eff)
+    if pixel_loss.dim() == 0:
+        # reduced criterion: torch.mean(s * w) == s * mean(w), w = 1 + alpha*U
+        base = pixel_loss.detach()
+        if u is None:
+            return pixel_loss, base
+        w_mean = 1.0 + alpha_eff * ops.mean_std(u)[0]
+        return pixel_loss * w_mean, base
+    if _kernel_layout(pixel_loss, u):
+        return _WeightedMeanFn.apply(pixel_loss, u, alpha_eff)
+    # any other broadcast between the criterion's output and U: the reference's
+    # elementwise expression, evaluated by torch on the device
+    base = torch.mean(pixel_loss.detach())
+    if u is None:
+        return torch.mean(pixel_loss), base
+    return torch.mean(pixel_loss * (1.0 + alpha_eff * u)), base
 
 
 class UncertaintyGuidedLoss:

@@ -491,6 +491,20 @@ def predict_mask(logits, size):
     return out
 
 
+def metrics_pack(m, ip, n_stat):
+    """-> float64 device tensor of n+2 sums for a SUM all-reduce (see include/ugpg.h)."""
+    sums = torch.empty(m.numel() + 2, dtype=torch.float64, device=m.device)
+    check(lib.ugpg_metrics_pack(_f32(m), m.numel(), int(ip), float(n_stat), ptr(sums), stream()),
+          "metrics_pack")
+    return sums
+
+
+def metrics_unpack(sums, m, ip, avg_mask):
+    check(lib.ugpg_metrics_unpack(ptr(sums), m.numel(), int(ip), int(avg_mask), _f32(m), stream()),
+          "metrics_unpack")
+    return m
+
+
 def mean_std(x, out=None):
     x = x.contiguous()
     out = empty(2, like=x) if out is None else out

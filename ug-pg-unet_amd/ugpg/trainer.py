@@ -19,10 +19,11 @@ import torch
 import torch.nn as nn
 
 from . import ops
-from .dist import allreduce_gradients, overlapped_allreduce, world
+from .dist import (allreduce_gradients, allreduce_metrics, broadcast_buffers,
+                   broadcast_parameters, overlapped_allreduce, shard_batch, world)
 from .loss import UncertaintyGuidedLoss, weighted_loss_tensors
 from .optim import RMSprop
-from .unet import PGUNet1, PGUNet2, PGUNet3, PGUNet4, transfer_state
+from .unet import PGUNet1, PGUNet2, PGUNet3, PGUNet4, ProgressiveUNet
 
 try:  # plotting is optional, as in the reference
     import matplotlib
@@ -78,6 +79,18 @@ class UncertaintyGuidedProgressiveTrainer:
         self.history = {k: [] for k in ("train_loss", "val_loss", "train_dice", "val_dice",
                                         "uncertainty_weights_mean", "uncertainty_weights_std",
                                         "base_loss", "stage_transitions")}
+        self.sync_replicas()
+
+    # ------------------------------------------------------------ data parallel
+    def sync_replicas(self, stages=None, buffers_only=False):
+        """Under torch.distributed (one process per GPU) make every rank's stage models
+        equal to rank 0's: parameters and buffers at construction / after loading
+        weights, BatchNorm buffers before validation and at stage end.
+        A no-op in a single process."""
+        if world()[1] <= 1:
+            return
+        for s in (stages or sorted(self.models)):
+            (broadcast_buffers if buffers_only else broadcast_parameters)(self.models[s])
 
     # ------------------------------------------------------------ components
     def setup_optimizer(self, stage):
@@ -106,9 +119,12 @@ class UncertaintyGuidedProgressiveTrainer:
         print(f"Transferring weights from stage {prev_stage} to stage {new_stage}")
         prev_dict = self.models[prev_stage].state_dict()
         new_dict = self.models[new_stage].state_dict()
-        new_state, copied = transfer_state(prev_dict, new_dict)
-        print(f"transfer_weights(stage={new_stage}): copied {len(copied)} keys "
-              f"(examples: {copied[:5]})")
+        # the reference builds a throwaway ProgressiveUNet here (uncertainty_guided_trainer.py:
+        # 136); building ours on the host draws the same default-init random numbers, so the
+        # global RNG -- DataLoader shuffles, augmentation seeds -- stays in step with it
+        progressive_unet = ProgressiveUNet(self.in_channels, self.num_classes)
+        new_state = progressive_unet.transfer_weights(prev_dict, new_dict, new_stage)
+        del progressive_unet
         self.models[new_stage].load_state_dict(new_state)
         print(f"Weight transfer completed for stage {new_stage}")
 
@@ -156,7 +172,14 @@ class UncertaintyGuidedProgressiveTrainer:
             [p for g in self.optimizer.param_groups for p in g["params"]])
         self.optimizer.step()
         self._metrics_device(output, target, umap, mbuf)
+        self._reduce_metrics(mbuf, umap)
         return mbuf
+
+    @staticmethod
+    def _reduce_metrics(mbuf, umap):
+        """Data parallel: [final, base, dice, acc] averaged over ranks (equal shards),
+        the wrong-pixel count summed, the U mean/std pooled over the global batch."""
+        allreduce_metrics(mbuf, 5, umap.numel() if umap is not None else 0, 0b1111)
 
     def uncertainty_guided_forward_pass(self, data, target, stage):
         mbuf = torch.zeros(8, dtype=torch.float32, device=data.device)
@@ -188,9 +211,17 @@ class UncertaintyGuidedProgressiveTrainer:
                 print(f"Stage {stage}, Batch {batch_idx}, Loss: {v[0]:.4f}, Base_Loss: {v[1]:.4f}, "
                       f"Dice: {v[2]:.4f}, Acc: {acc:.4f}{extra}")
 
+        _, ws = world()
+        if not train:
+            self.sync_replicas([stage], buffers_only=True)
         pending = None  # batch k is read back after batch k+1 is enqueued
+        skipped = 0
         for batch_idx, (data, target) in enumerate(dataloader):
-            data, target = self._resize_batch(data, target, res)
+            part = shard_batch(dataloader, data, target)  # this rank's rows (DP)
+            if part is None:
+                skipped += 1
+                continue
+            data, target = self._resize_batch(*part, res)
             if train:
                 mbuf = self.train_step(data, target, stage)
             else:
@@ -198,14 +229,15 @@ class UncertaintyGuidedProgressiveTrainer:
                 with torch.no_grad():
                     output, umap, _, _ = self._forward_device(data, target, stage, mbuf)
                     self._metrics_device(output, target, umap, mbuf)
-            cur = (batch_idx, data.shape[0] * res * res, MetricsReadback(mbuf))
+                    self._reduce_metrics(mbuf, umap)
+            cur = (batch_idx, data.shape[0] * ws * res * res, MetricsReadback(mbuf))
             if pending is not None:
                 consume(*pending)
             pending = cur
         if pending is not None:
             consume(*pending)
-        num = len(dataloader)
-        avg = tot / num
+        num = len(dataloader) - skipped
+        avg = tot / max(num, 1)
         kind = "training" if train else "validation"
         print(f"Stage {stage} {kind} epoch completed. Batches processed: {num}")
         return tuple(float(a) for a in avg)
@@ -247,6 +279,8 @@ class UncertaintyGuidedProgressiveTrainer:
                 print(f"Stage {stage}, Epoch {epoch + 1}/{epochs} ({time.time() - t0:.2f}s)")
                 print(f"Train - Loss: {tr[0]:.4f}, Base: {tr[1]:.4f}, Dice: {tr[2]:.4f}, Acc: {tr[3]:.4f}")
                 print(f"Val   - Loss: {va[0]:.4f}, Base: {va[1]:.4f}, Dice: {va[2]:.4f}, Acc: {va[3]:.4f}")
+                # validation used rank 0's BatchNorm buffers on every rank, so the
+                # checkpoint decision below is the same everywhere
                 if va[2] > best:
                     best = va[2]
                     if rank == 0:
@@ -257,6 +291,8 @@ class UncertaintyGuidedProgressiveTrainer:
                                     "uncertainty_alpha": self.uncertainty_alpha,
                                     "history": self.history},
                                    save_path / f"ug_pgunet_stage{stage}_best.pth")
+            # the finished stage becomes the next stage's U-map producer: one BN state
+            self.sync_replicas([stage], buffers_only=True)
         print("Uncertainty-guided progressive training completed!")
         if rank == 0:
             self.save_training_plots(save_path)
@@ -289,6 +325,7 @@ class UncertaintyGuidedProgressiveTrainer:
     def load_stage_weights(self, stage, checkpoint_path):
         ck = torch.load(checkpoint_path, map_location=self.device, weights_only=True)
         self.models[stage].load_state_dict(ck["model_state_dict"] if "model_state_dict" in ck else ck)
+        self.sync_replicas([stage])
         print(f"Loaded weights for stage {stage} from {checkpoint_path}")
 
     def save_uncertainty_analysis(self, data_loader, stage, save_path):
