@@ -96,11 +96,20 @@ def test_config2_bs16_step_parity(dev):
     print("bs16 gradient headroom err/bound: worst", [(round(r, 3), k) for r, k in ratios[:5]],
           "median", round(float(np.median([r for r, _ in ratios])), 4))
     assert not bad, "gradient parity failures:\n" + "\n".join(bad[:20])
-    # post-RMSprop parameters vs the reference's torch.optim.RMSprop step
-    for k in param_keys(state):
+    # post-RMSprop parameters: exactly torch's RMSprop rule on the HIP gradients, and the
+    # reference's post-step checksums up to the first step's sign flips (RMSprop's first
+    # update is ~10 lr * sign(g) whatever |g|, so a noise-level gradient element whose
+    # sign differs moves by 2e-3: norm tolerance 1e-4 relative)
+    keys = param_keys(state)
+    P = {k: state[k].clone() for k in keys}
+    O.rmsprop_step(P, {k: grads[k] for k in keys}, {k: torch.zeros_like(P[k]) for k in keys}, 1e-4)
+    for k in keys:
+        p = sd[k].detach().cpu()
+        assert (p - P[k]).abs().max().item() <= 1e-6 * max(1.0, P[k].abs().max().item()), k
+        if is_prebn_bias(k):
+            continue  # gradient is pure rounding noise (true value 0): every sign is arbitrary
         want = fx[f"post/{k}"]
-        p = sd[k].detach().double().cpu()
-        assert abs(p.norm().item() - want[0]) <= 1e-6 * want[0] + 1e-7, k
+        assert abs(p.double().norm().item() - want[0]) <= 1e-4 * want[0] + 1e-6, k
 
 
 def test_config3_bf16_bs16_step(dev):

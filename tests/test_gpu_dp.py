@@ -15,8 +15,8 @@ import torch
 
 from oracle import detgen as G
 from oracle import ref_cpu as O
-from tests._parity import det_state, grad_check, oracle_run, param_keys, FLOOR_PERTURBATIONS, \
-    perturbed_state
+from tests._parity import (FLOOR_PERTURBATIONS, det_state, grad_check, is_prebn_bias,
+                           oracle_run, param_keys, perturbed_state)
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -64,8 +64,8 @@ def test_dp_two_ranks_match_shard_mean(tmp_path):
     # replicas: constructor broadcast, load_stage_weights broadcast, identical step
     for k, v in res[0]["ctor_s3_after"].items():
         assert torch.equal(v, res[1]["ctor_s3_after"][k]), k
-    assert not all(torch.equal(v, res[1]["ctor_s3"][k]) for k, v in res[0]["ctor_s3"].items()
-                   if v.is_floating_point()), "ranks should have started from different weights"
+    for k, v in res[0]["ctor_s3"].items():     # right after the constructor already
+        assert torch.equal(v, res[1]["ctor_s3"][k]), k
     for k, v in res[0]["state"].items():
         if not O._is_buffer(k):
             assert torch.equal(v, res[1]["state"][k]), f"replicas diverged: {k}"
@@ -97,6 +97,10 @@ def test_dp_two_ranks_match_shard_mean(tmp_path):
     print("DP gradient headroom (err/bound), worst 5:", sorted(worst, reverse=True)[:5])
     assert not bad, "\n".join(bad[:20])
     # one RMSprop step on the averaged gradient: parameter checksums
+    # (RMSprop's first update is ~10 lr * sign(g): noise-level sign flips move an element
+    # by 2e-3, hence the 1e-4 relative norm tolerance; the rule itself is exact elsewhere)
     for k in param_keys(state):
+        if is_prebn_bias(k):
+            continue  # noise-level gradient (true value 0): its RMSprop signs are arbitrary
         p = res[0]["state"][k].double()
-        assert abs(p.norm().item() - fx[f"post/{k}"][0]) <= 1e-5 * fx[f"post/{k}"][0] + 1e-6, k
+        assert abs(p.norm().item() - fx[f"post/{k}"][0]) <= 1e-4 * fx[f"post/{k}"][0] + 1e-6, k

@@ -619,7 +619,12 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
     // spare slot NHALO; plane pitch 348 = 4 (mod 8) for the 32x32 fragment pattern, 352
     // = 0 (mod 16) for the 16x16 one (ds_read_b128 lane groups, MI355X_MICROARCH.md §LDS)
     constexpr int NHP = M16 ? (NHALO + 1 + 15) / 16 * 16 : NHALO + 1 + (11 - NHALO % 8) % 8;
-    constexpr int A_ITEMS = NHALO * 2;                      // (pixel, channel half)
+    // (halo pixel, channel half) items: lane group i of 16 takes 16 consecutive pixels of
+    // one half (i & 1), so each 8-lane group of a halo ds_write_b128 stores 128 contiguous
+    // bytes of one plane -- conflict-free (the two halves of a pixel sit 352 vectors apart,
+    // i.e. on the same banks; pairing them in one 8-lane group was a 2-way conflict on
+    // every halo store: 0.35 conflict cycles per LDS instruction, profiles/r1i)
+    constexpr int A_ITEMS = (NHALO + 15) / 16 * 32;         // 704 / 672 incl. idle lanes
     constexpr int A_PER = (A_ITEMS + 255) / 256;            // 3
     constexpr int A_VECS = 2 * NP * NHP;
     constexpr int R_VEC = NP * 2 * 3 * BN;                  // one kernel row of weights
@@ -666,6 +671,8 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
         // coefficients) three steps ahead, written (activated, split) into A buffer s & 1
         // during phases 0-1 of step s-1.  Weight rows: LDS-DMA, see below.
         const int lt = tid - 256;
+        const int hhl = (lt >> 4) & 1;  // channel half of this lane (same for all its items)
+        auto item_px = [](int idx) { return (idx >> 5) * 16 + (idx & 15); };
         f32x4 ra[2][A_PER][2];
         unsigned avalid[2] = {0u, 0u};
         Act4 r0[2], r1[2];
@@ -699,9 +706,8 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
         int hy[A_PER], hx[A_PER];
 #pragma unroll
         for (int v = 0; v < A_PER; ++v) {
-            const int idx = lt + v * 256;
-            const int hp = idx < A_ITEMS ? idx >> 1 : 0;
-            hy[v] = idx < A_ITEMS ? hp / HWD : -(1 << 20);  // never inside the image
+            const int hp = item_px(lt + v * 256);
+            hy[v] = hp < NHALO ? hp / HWD : -(1 << 20);  // never inside the image
             hx[v] = hp % HWD;
         }
         auto load_halo = [&](const Cur& q, auto S) {
@@ -720,8 +726,8 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
             const float* shp = aon ? sh : g_act_zeros;
             lo[st] = aon ? 0.f : -INFINITY;
             // an 8-channel source is zero-extended to the 16-channel chunk
-            const bool cok = cb + (lt & 1) * 8 < Cs;
-            const int cc = cb + (cok ? (lt & 1) * 8 : 0);
+            const bool cok = cb + hhl * 8 < Cs;
+            const int cc = cb + (cok ? hhl * 8 : 0);
             r0[st].s = gld16(scp + cc);
             r0[st].h = gld16(shp + cc);
             r1[st].s = gld16(scp + cc + 4);
@@ -745,8 +751,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
             u32x4* As = smem + (k & 1) * A_VECS;
 #pragma unroll
             for (int v = v0; v < v1; ++v) {
-                const int idx = lt + v * 256;
-                const int hp = idx >> 1, hh = idx & 1;
+                const int hp = item_px(lt + v * 256), hh = hhl;
                 const f32x4 lo4 = act_floor4(ra[st][v][0], r0[st], lo[st]),
                             hi4 = act_floor4(ra[st][v][1], r1[st], lo[st]);
                 const bool ok = (avalid[st] >> v) & 1u;
@@ -755,7 +760,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
                                  ok ? hi4.z : 0.f, ok ? hi4.w : 0.f};
                 u32x4 pc[NP];
                 split_n<NP>(x, pc);
-                const int hl = idx < A_ITEMS ? (hp / HWD) * HS + hp % HWD : NHALO;
+                const int hl = hp < NHALO ? (hp / HWD) * HS + hp % HWD : NHALO;
 #pragma unroll
                 for (int q = 0; q < NP; ++q) As[(q * 2 + hh) * NHP + hl] = pc[q];
             }
