@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=16, help="images per GPU")
     ap.add_argument("--res", type=int, default=256)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-steps", type=int, default=5)
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--secondary-steps", type=int, default=5,
                     help="steps of the secondary line (S4 fwd+bwd without the uncertainty "
@@ -55,26 +55,61 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(batch, res, steps, threads):
-    """Time the CPU oracle's UG step (bounded sample) on this host."""
+def cpu_cores():
+    """Physical cores this process can use: the affinity mask's cores (logical CPUs / SMT
+    width), capped by the cgroup CPU quota (a container's share of the host)."""
+    logical = len(os.sched_getaffinity(0))
+    try:
+        sib = open("/sys/devices/system/cpu/cpu0/topology/thread_siblings_list").read().strip()
+        smt = 0
+        for part in sib.split(","):
+            a, _, b = part.partition("-")
+            smt += int(b) - int(a) + 1 if b else 1
+    except (OSError, ValueError):
+        smt = 1
+    cores = max(1, logical // max(smt, 1))
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            cores = min(cores, max(1, int(quota) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return cores
+
+
+def cpu_baseline(batch, res, steps, thread_counts):
+    """Time the CPU oracle's UG step (the reference's torch CPU ops, same order) on this
+    host: for each thread count, 1 warm-up step then the median of `steps` timed steps
+    (SURVEY.md §8d protocol).  Progress goes to stderr (a long silent phase reads as hung)."""
     import torch
     from oracle import detgen as G
     from oracle import ref_cpu as O
-    torch.set_num_threads(threads)
-    cur = G.make_state(O.state_spec(4, 3, 1), 0)
+    cur0 = G.make_state(O.state_spec(4, 3, 1), 0)
     prev = G.make_state(O.state_spec(3, 3, 1), 1)
-    sq = {k: torch.zeros_like(v) for k, v in cur.items() if v.is_floating_point() and not O._is_buffer(k)}
     x = G.randn(1, (batch, 3, res, res), "x")
     t = G.bernoulli(2, (batch, 1, res, res), 0.5, "t")
-    O.ug_train_step(4, cur, prev, x, t, sq, 1e-4)  # warm-up
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        O.ug_train_step(4, cur, prev, x, t, sq, 1e-4)
-    dt = time.perf_counter() - t0
-    return {"value": round(batch * steps / dt, 4), "unit": "images/sec", "cores": threads,
-            "kind": "port",
-            "sample": f"{steps} oracle UG steps (bs{batch} {res}^2, S4 fwd+bwd + S3 U-map + RMSprop) "
-                      f"after 1 warm-up, torch CPU fp32, {threads} threads"}
+    rates = {}
+    for threads in thread_counts:
+        torch.set_num_threads(threads)
+        cur = {k: v.clone() for k, v in cur0.items()}
+        sq = {k: torch.zeros_like(v) for k, v in cur.items()
+              if v.is_floating_point() and not O._is_buffer(k)}
+        O.ug_train_step(4, cur, prev, x, t, sq, 1e-4)  # warm-up
+        times = []
+        for i in range(steps):
+            t0 = time.perf_counter()
+            O.ug_train_step(4, cur, prev, x, t, sq, 1e-4)
+            times.append(time.perf_counter() - t0)
+            print(f"cpu baseline: {threads} threads, step {i + 1}/{steps}: {times[-1]:.2f} s",
+                  file=sys.stderr, flush=True)
+        times.sort()
+        rates[threads] = round(batch / times[len(times) // 2], 4)
+    top = max(thread_counts)
+    return {"value": rates[top], "unit": "images/sec", "cores": top, "kind": "port",
+            "by_cores": {str(k): v for k, v in rates.items()},
+            "sample": f"oracle UG step (bs{batch} {res}^2: S4 fwd+bwd + S3 U-map + RMSprop), "
+                      f"torch CPU fp32, median of {steps} steps after 1 warm-up, at "
+                      f"{' and '.join(str(k) for k in thread_counts)} threads (= physical cores)"}
 
 
 def pmc_traffic(family):
@@ -100,7 +135,7 @@ def main():
     import torch.distributed as dist
     import ugpg
     from ugpg import ops
-    from ugpg.dist import broadcast_parameters, init_from_env, max_over_ranks
+    from ugpg.dist import init_from_env, max_over_ranks
     from ugpg.trainer import MetricsReadback
 
     ops.set_conv_math(args.conv_math)
@@ -117,9 +152,7 @@ def main():
     tr = ugpg.UncertaintyGuidedProgressiveTrainer(3, 1, device=dev, uncertainty_alpha=1.0)
     tr.current_stage = 4
     tr.current_model = tr.models[4]
-    tr.setup_optimizer(4)
-    for s in (3, 4):
-        broadcast_parameters(tr.models[s])
+    tr.setup_optimizer(4)  # (the trainer constructor already made the replicas equal)
     B, R = args.batch, args.res
     g = torch.Generator().manual_seed(100 + rank)
     x = torch.randn(B, 3, R, R, generator=g).to(dev)
@@ -238,8 +271,9 @@ def main():
         "secondary": secondary,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-        result["cpu_baseline"] = cpu_baseline(B, R, args.cpu_steps, threads)
+        phys = cpu_cores()
+        counts = sorted({phys, min(8, phys)})
+        result["cpu_baseline"] = cpu_baseline(B, R, args.cpu_steps, counts)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -31,6 +31,7 @@ extern "C" {
 #define UGPG_ERR_INVALID (-1)     /* bad argument / unsupported shape */
 #define UGPG_ERR_LAUNCH (-2)      /* hipGetLastError after a launch */
 #define UGPG_ERR_WORKSPACE (-3)   /* workspace too small */
+#define UGPG_ERR_COMM (-4)        /* RCCL / device error in a ugpg_comm_* call */
 
 const char* ugpg_version(void);
 const char* ugpg_last_error(void);
@@ -251,6 +252,31 @@ int ugpg_predict_mask(const float* logits, int B, int H, int W, float* mask, int
 size_t ugpg_mean_std_workspace(int64_t n);
 int ugpg_mean_std(const float* x, int64_t n, float* out, void* ws, size_t ws_bytes,
                   void* stream);
+
+/* ---- RCCL communicator (the reference has no collectives -- this is the
+ * data-parallel exchange the build adds: gradient all-reduce, replica broadcast).
+ * Rendezvous: rank 0 calls ugpg_comm_unique_id and passes the ugpg_comm_id_bytes() bytes
+ * to every rank out of band; each rank calls ugpg_comm_init with its own device.  The
+ * collectives are stream-ordered on `stream` (hipStream_t), in place when send == recv,
+ * never synchronise the host and allocate nothing.  The handle is the only global state
+ * of the library; destroy it on every rank. */
+typedef struct ugpg_comm* ugpg_comm_t;
+#define UGPG_DT_F32 0
+#define UGPG_DT_BF16 1
+#define UGPG_DT_F64 2
+#define UGPG_DT_I64 3
+#define UGPG_OP_SUM 0
+#define UGPG_OP_AVG 1
+#define UGPG_OP_MAX 2
+size_t ugpg_comm_id_bytes(void);
+int ugpg_comm_unique_id(unsigned char* out, size_t n);
+int ugpg_comm_init(ugpg_comm_t* comm, int nranks, int rank, const unsigned char* id,
+                   size_t id_bytes, int device);
+int ugpg_comm_allreduce(ugpg_comm_t comm, const void* send, void* recv, size_t count, int dtype,
+                        int op, void* stream);
+int ugpg_comm_broadcast(ugpg_comm_t comm, const void* send, void* recv, size_t count, int dtype,
+                        int root, void* stream);
+int ugpg_comm_destroy(ugpg_comm_t comm);
 
 /* ---- data-parallel metrics exchange (metrics all-reduced under DP; the
  * reference is single-process, its per-batch metrics are uncertainty_guided_trainer.py:

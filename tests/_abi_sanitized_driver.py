@@ -1,0 +1,62 @@
+"""Run under the ASan runtime against the host-only sanitized libugpg (tests/test_abi.py):
+every C-ABI entry is called with null pointers and out-of-range sizes and must refuse with a
+negative status and a message, never crash or touch memory it was not given.  No GPU."""
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "ug-pg-unet_amd")]
+
+from ugpg import _C  # noqa: E402  (UGPG_LIB points at the sanitized build)
+
+
+def bad_value(t):
+    if t in (C.c_int, C.c_int64):
+        return -1
+    if t in (C.c_size_t, C.c_uint, C.c_uint64):
+        return 0
+    if t in (C.c_float, C.c_double):
+        return float("nan")
+    if t is C.c_char_p:
+        return None
+    if isinstance(t, type) and issubclass(t, C.Structure):
+        return t()  # all-zero descriptor by value (null pointers, zero sizes)
+    return None  # pointers, including POINTER(struct)
+
+
+def main():
+    lib = _C.lib.load()
+    assert _C.version().startswith("ugpg ")
+    checked = 0
+    for name, (res, args) in _C.SIGNATURES.items():
+        if name in ("ugpg_version", "ugpg_last_error", "ugpg_comm_id_bytes"):
+            getattr(lib, name)()
+            continue
+        if res is not C.c_int or name in ("ugpg_conv3x3_fwd_ntiles",):  # size/count queries
+            getattr(lib, name)(*[bad_value(a) for a in args])
+            continue
+        rc = getattr(lib, name)(*[bad_value(a) for a in args])
+        if name == "ugpg_comm_destroy":  # destroy(NULL) is a no-op, like free
+            assert rc == 0
+            continue
+        msg = lib.ugpg_last_error()
+        assert rc < 0, f"{name} accepted invalid arguments (rc {rc})"
+        assert msg, f"{name}: no error message"
+        checked += 1
+    # a few targeted cases around the accepted range
+    assert lib.ugpg_set_tuning(b"no_such_knob", 1) < 0
+    buf = (C.c_ubyte * 8)()
+    assert lib.ugpg_comm_unique_id(buf, 8) < 0 and b"comm_unique_id" in lib.ugpg_last_error()
+    assert lib.ugpg_comm_destroy(None) == 0
+    x = (C.c_float * 40)()
+    assert lib.ugpg_metrics_pack(x, 40, -1, 1.0, None, None) < 0       # n > 32
+    assert lib.ugpg_metrics_unpack(None, 8, 5, 0xF, x, None) < 0
+    long_name = b"k" * 5000                                                   # message buffer bound
+    lib.ugpg_set_tuning(long_name, 1)
+    assert len(lib.ugpg_last_error()) < 5000
+    print(f"sanitized ABI driver: {checked} entries refused invalid arguments")
+
+
+if __name__ == "__main__":
+    main()

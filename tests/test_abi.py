@@ -57,3 +57,29 @@ def test_ops_refuse_cpu_tensors():
     from ugpg import ops
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         ops.mean_std(torch.ones(8))
+
+
+def test_host_side_under_asan_ubsan():
+    """the C-ABI's host side (argument validation, error strings, plan and
+    workspace arithmetic, communicator bookkeeping) built with AddressSanitizer and
+    UndefinedBehaviorSanitizer on the host only (-Xarch_host) and driven with invalid
+    arguments through every entry (tests/_abi_sanitized_driver.py), ASan runtime preloaded."""
+    import glob
+    import importlib.util
+    import os
+    import sys
+    spec = importlib.util.spec_from_file_location("ugpg_build", ROOT / "ug-pg-unet_amd" / "build.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    lib = mod.build_sanitized()
+    syms = subprocess.run(["nm", "-D", str(lib)], capture_output=True, text=True, check=True).stdout
+    assert "__asan_init" in syms and "__ubsan_handle" in syms, "sanitizers not linked in"
+    rt = glob.glob("/opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so")
+    assert rt, "ASan runtime not found"
+    env = dict(os.environ, LD_PRELOAD=rt[0], UGPG_LIB=str(lib),
+               ASAN_OPTIONS="detect_leaks=0:halt_on_error=1",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    r = subprocess.run([sys.executable, str(ROOT / "tests" / "_abi_sanitized_driver.py")],
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "entries refused invalid arguments" in r.stdout

@@ -75,7 +75,8 @@ def build(force: bool = False, verbose: bool = True, defines=(), out: Path | Non
     LIB_ = lib
     if force or not LIB_.exists() or LIB_.stat().st_mtime < newest:
         tmp = LIB_.with_suffix(".so.tmp")
-        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp)]
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp),
+               "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr}")
@@ -83,6 +84,44 @@ def build(force: bool = False, verbose: bool = True, defines=(), out: Path | Non
     if verbose:
         print(f"built {LIB_} ({LIB_.stat().st_size / 1e6:.1f} MB)")
     return LIB_
+
+
+SAN_FLAGS = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined"]
+
+
+def build_sanitized(out: Path | None = None, verbose: bool = False) -> Path:
+    """ASan + UBSan on the HOST side of the C-ABI (argument validation, error plumbing,
+    plan/workspace arithmetic, the communicator's host code): the usual gfx950 build with
+    each -fsanitize= behind -Xarch_host, device code untouched.  For CPU tests of the host
+    paths (tests/test_abi.py, loaded with the ASan runtime preloaded); never used on a GPU."""
+    bdir = BUILD / "asan"
+    bdir.mkdir(parents=True, exist_ok=True)
+    lib = Path(out) if out else bdir / "libugpg_asan.so"
+
+    def one(src):
+        obj = bdir / (src.stem + ".o")
+        if not obj.exists() or obj.stat().st_mtime < max(src.stat().st_mtime, _newest_header()):
+            cmd = [_hipcc(), "-O1", "-g", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}",
+                   "-fno-omit-frame-pointer", *PER_FILE.get(src.name, []), *SAN_FLAGS, "-c",
+                   str(src), "-o", str(obj)]
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"sanitized hipcc failed for {src.name}:\n{r.stderr}")
+        return obj
+
+    srcs = _sources()
+    with cf.ThreadPoolExecutor(max_workers=max(1, min(len(srcs), int(os.environ.get("MAX_JOBS", "8"))))) as ex:
+        objs = list(ex.map(one, srcs))
+    if not lib.exists() or lib.stat().st_mtime < max(o.stat().st_mtime for o in objs):
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-shared-libsan", *SAN_FLAGS,
+               *map(str, objs), "-o", str(lib), "-L/opt/rocm/lib", "-lrccl",
+               "-Wl,-rpath,/opt/rocm/lib"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"sanitized link failed:\n{r.stderr}")
+    if verbose:
+        print(f"built {lib}")
+    return lib
 
 
 if __name__ == "__main__":

@@ -80,6 +80,12 @@ SIGNATURES = {
     "ugpg_predict_mask": (_i, [_p, _i, _i, _i, _p, _i, _i, _p]),
     "ugpg_mean_std_workspace": (_sz, [_i64]),
     "ugpg_mean_std": (_i, [_p, _i64, _p, _p, _sz, _p]),
+    "ugpg_comm_id_bytes": (_sz, []),
+    "ugpg_comm_unique_id": (_i, [_p, _sz]),
+    "ugpg_comm_init": (_i, [C.POINTER(_p), _i, _i, _p, _sz, _i]),
+    "ugpg_comm_allreduce": (_i, [_p, _p, _p, _sz, _i, _i, _p]),
+    "ugpg_comm_broadcast": (_i, [_p, _p, _p, _sz, _i, _i, _p]),
+    "ugpg_comm_destroy": (_i, [_p]),
     "ugpg_metrics_pack": (_i, [_p, _i, _i, C.c_double, _p, _p]),
     "ugpg_metrics_unpack": (_i, [_p, _i, _i, C.c_uint, _p, _p]),
     "ugpg_rmsprop_step": (_i, [_p, _p, _p, _i64, _f, _f, _f, _f, _f, _p]),

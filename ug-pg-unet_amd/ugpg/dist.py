@@ -81,7 +81,7 @@ class OverlapReducer:
     def _issue(self, lo, hi):
         while hi > lo:
             a = max(lo, hi - self.bucket)
-            self.works.append(dist.all_reduce(self.flat[a:hi], async_op=True))
+            self.works.append(_all_reduce_async(self.flat[a:hi]))
             hi = a
         return lo
 
@@ -153,6 +153,118 @@ def overlap_reducer() -> OverlapReducer | None:
     return _REDUCER
 
 
+_DT = {torch.float32: 0, torch.bfloat16: 1, torch.float64: 2, torch.int64: 3}
+_OPS = {"sum": 0, "avg": 1, "max": 2}
+
+
+class Communicator:
+    """libugpg's own RCCL communicator (C-ABI ugpg_comm_*, include/ugpg.h) for one process
+    per GPU.  Rendezvous: rank 0's unique id travels through the torch.distributed store
+    (or is passed in).  Collectives run on the caller's current HIP stream, in place.
+
+    torch.distributed's "nccl" backend is RCCL too; this handle is the same exchange at the
+    C-ABI boundary, for callers that bind libugpg without torch.  Select it
+    for the trainer's gradient all-reduce with UGPG_COMM=native."""
+
+    def __init__(self, rank=None, world_size=None, device=None, unique_id: bytes | None = None):
+        import ctypes
+        from ._C import check, lib
+        r, ws = world()
+        self.rank = r if rank is None else rank
+        self.world_size = ws if world_size is None else world_size
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        n = lib.ugpg_comm_id_bytes()
+        if unique_id is None:
+            buf = (ctypes.c_ubyte * n)()
+            if self.rank == 0:
+                check(lib.ugpg_comm_unique_id(buf, n), "comm_unique_id")
+            if self.world_size > 1:
+                obj = [bytes(buf) if self.rank == 0 else None]
+                dist.broadcast_object_list(obj, src=0)
+                unique_id = obj[0]
+            else:
+                unique_id = bytes(buf)
+        idbuf = (ctypes.c_ubyte * n).from_buffer_copy(unique_id[:n])
+        self._h = ctypes.c_void_p()
+        check(lib.ugpg_comm_init(ctypes.byref(self._h), self.world_size, self.rank, idbuf, n,
+                                 self.device), "comm_init")
+
+    def _stream(self):
+        return torch.cuda.current_stream().cuda_stream
+
+    def all_reduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        from ._C import check, lib
+        if not t.is_cuda or not t.is_contiguous():
+            raise RuntimeError("ugpg Communicator: contiguous ROCm tensors only")
+        check(lib.ugpg_comm_allreduce(self._h, t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype],
+                                      _OPS[op], self._stream()), "comm_allreduce")
+        return t
+
+    def broadcast(self, t: torch.Tensor, root: int = 0) -> torch.Tensor:
+        from ._C import check, lib
+        if not t.is_cuda or not t.is_contiguous():
+            raise RuntimeError("ugpg Communicator: contiguous ROCm tensors only")
+        check(lib.ugpg_comm_broadcast(self._h, t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype],
+                                      root, self._stream()), "comm_broadcast")
+        return t
+
+    def close(self):
+        from ._C import check, lib
+        if self._h:
+            check(lib.ugpg_comm_destroy(self._h), "comm_destroy")
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_COMM: Communicator | None = None
+
+
+def native_comm() -> Communicator | None:
+    """The process-wide libugpg communicator when UGPG_COMM=native (data parallel only)."""
+    global _COMM
+    if os.environ.get("UGPG_COMM", "torch") != "native" or world()[1] <= 1:
+        return None
+    if _COMM is None:
+        _COMM = Communicator()
+    return _COMM
+
+
+class _NativeWork:
+    """async handle of a bucket reduced by the native communicator on a side stream"""
+
+    def __init__(self, comm, t, stream):
+        cur = torch.cuda.current_stream()
+        stream.wait_stream(cur)
+        with torch.cuda.stream(stream):
+            comm.all_reduce(t)
+            self.done = torch.cuda.Event()
+            self.done.record(stream)
+        t.record_stream(stream)
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.done)
+
+
+_SIDE = None
+
+
+def _all_reduce_async(t):
+    """SUM all-reduce of a gradient bucket: RCCL through torch.distributed (async work), or
+    libugpg's communicator on a side stream (UGPG_COMM=native)."""
+    global _SIDE
+    comm = native_comm() if t.is_cuda else None
+    if comm is None:
+        return dist.all_reduce(t, async_op=True)
+    if _SIDE is None:
+        _SIDE = torch.cuda.Stream(device=t.device)
+    return _NativeWork(comm, t, _SIDE)
+
+
 def _runs(grads):
     """Split `grads` (in order) into maximal back-to-back runs of one storage."""
     runs, cur = [], []
@@ -178,7 +290,7 @@ def _allreduce_runs(grads, bucket_bytes):
             continue
         base, _, n = flat
         for off in range(0, n, step):
-            dist.all_reduce(base[off:off + step])
+            _all_reduce_async(base[off:off + step]).wait()
     if loose:
         stage = torch.cat([g.reshape(-1) for g in loose])
         dist.all_reduce(stage)
