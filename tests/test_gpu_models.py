@@ -365,3 +365,49 @@ def test_ug_training_trajectory_dice_parity(dev):
     lref = max(abs(a[0] - o[0]) / abs(o[0]) for a, o in zip(o32[1:], o64[1:]))
     assert lhip <= 2 * lref + 1e-3, (lhip, lref)
     print(f"max |Dice - fp64 oracle| over steps 2-10: HIP {dev_hip:.4f}, reference fp32 {dev_ref:.4f}")
+
+
+def test_weight_pack_cache_reuse_and_invalidation(dev):
+    """Packed weights persist on the parameters and are reused while a weight is unchanged
+    (the frozen uncertainty-map stage), and are rebuilt after every kind of write: an
+    RMSprop step (raw-pointer kernel), load_state_dict, a broadcast-style raw write."""
+    import ugpg
+    from ugpg import ops
+    state = det_state(3, 3, 1)
+    m = build(3, 1, state, dev).eval()
+    x = G.randn(5, (2, 3, 128, 128), "x").to(dev)
+    w = m.inc.conv.conv_op[3].weight
+    with torch.no_grad():
+        o1 = m(x)
+    first = {k: v[1] for k, v in w._ugpg_packs.items()}
+    with torch.no_grad():
+        o2 = m(x)
+    assert all(w._ugpg_packs[k][1] is v for k, v in first.items()), "pack not reused"
+    assert torch.equal(o1, o2)
+
+    def fresh_logits():
+        f = build(3, 1, {k: v.detach().cpu() for k, v in m.state_dict().items()}, dev).eval()
+        with torch.no_grad():
+            return f(x)
+
+    # optimizer step: new weights must be repacked
+    m.train()
+    opt = ugpg.RMSprop(m.parameters(), lr=1e-3)
+    m(x).sum().backward()
+    opt.step()
+    m.eval()
+    with torch.no_grad():
+        o3 = m(x)
+    assert not any(w._ugpg_packs[k][1] is v for k, v in first.items()), "stale pack after step"
+    assert torch.equal(o3, fresh_logits()) and not torch.equal(o3, o1)
+    # load_state_dict
+    m.load_state_dict(state)
+    with torch.no_grad():
+        assert torch.equal(m(x), o1)
+    # raw write announced with weights_written
+    with torch.no_grad():
+        w.data.mul_(1.5)  # .data: no version bump by itself
+    ops.weights_written([w])
+    with torch.no_grad():
+        o4 = m(x)
+    assert torch.equal(o4, fresh_logits())

@@ -40,5 +40,37 @@ def main():
         print(f"bilinear_bwd {2 * h}->{h} C{c}: {us:7.1f} us  {gb:6.0f} GB/s", flush=True)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and (len(sys.argv) < 2 or sys.argv[1] != "bn"):
     main()
+
+
+def bn_main(knobs):
+    """BatchNorm+ReLU backward (reduce, finalize, apply) at the 8 Stage-4 layer shapes;
+    `knobs`: list of (name, {tuning key: value}) to A/B in one process."""
+    from ugpg._C import lib
+    dev = torch.device("cuda:0")
+    B = 16
+    tot = {}
+    for (h, c) in [(256, 64), (128, 128), (64, 256), (32, 512), (16, 512), (32, 256), (64, 128),
+                   (128, 64)]:
+        y = torch.randn(B, h, h, c, device=dev)
+        da = torch.randn_like(y)
+        dy = torch.empty_like(y)
+        mean, invstd = torch.randn(c, device=dev) * 0.1, torch.rand(c, device=dev) + 0.5
+        scale, shift = torch.rand(c, device=dev) + 0.5, torch.randn(c, device=dev) * 0.1
+        dg, dbt, dbias = (torch.empty(c, device=dev) for _ in range(3))
+        line = []
+        for name, kv in knobs:
+            for k, v in kv.items():
+                lib.ugpg_set_tuning(k.encode(), v)
+            us = timeit(lambda: ops.bn_relu_bwd(da, y, mean, invstd, scale, shift, dy, dg, dbt, dbias))
+            gb = 5 * y.numel() * 4 / (us * 1e-6) / 1e9
+            tot[name] = tot.get(name, 0.0) + 2 * us
+            line.append(f"{name} {us:6.1f} us {gb:5.0f} GB/s")
+        print(f"bn_bwd {h}^2 C{c}: " + " | ".join(line), flush=True)
+    print("bn_bwd per step (x2 per shape): " + " ".join(f"{k}={v:.0f}us" for k, v in tot.items()))
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "bn":
+    bn_main([("old", {"bn_bwd_blocks": 1024, "bn_bwd_ppt": 32}), ("new", {"bn_bwd_blocks": 2048, "bn_bwd_ppt": 4}),
+             ("p8", {"bn_bwd_blocks": 2048, "bn_bwd_ppt": 8}), ("b4096", {"bn_bwd_blocks": 4096, "bn_bwd_ppt": 2})])

@@ -7,6 +7,8 @@
 // the numerically stable two-pass result, deterministic for a fixed tiling.
 // The normalisation itself is never materialised: consumers apply
 // relu(scale*y + shift) while loading (ugpg_src_t).
+#include <numeric>
+
 #include "common.h"
 
 namespace ugpg {
@@ -183,20 +185,24 @@ __global__ void bn_bwd_finalize_kernel(const float* part, int nblk, int C, int64
     }
 }
 
-__global__ void bn_bwd_apply_kernel(const float* da, const float* __restrict__ y, int64_t npix,
-                                    int C, const float* mean, const float* invstd,
-                                    const float* scale, const float* shift, const float* coef,
-                                    float* dy) {
+// dy = scale * (g - mean(g) - xhat * mean(g*xhat)), g = [scale*y + shift > 0] * da.
+// The grid stride is a multiple of C/4 (2048 x 256 threads, C <= 1024), so each thread
+// keeps one 4-channel group: its per-channel coefficients are loaded once, and four
+// float4 pairs are in flight per thread.
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const float* da, const float* __restrict__ y,
+                                                           int64_t npix, int C, const float* mean,
+                                                           const float* invstd, const float* scale,
+                                                           const float* shift, const float* coef,
+                                                           float* dy) {
     const int64_t n4 = npix * C / 4;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i0 >= n4) return;
     auto ld4 = [](const float* p, int c) { return *reinterpret_cast<const f32x4*>(p + c); };
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const int c = (int)((i * 4) % C);
-        const f32x4 d = reinterpret_cast<const f32x4*>(da)[i];
-        const f32x4 v = reinterpret_cast<const f32x4*>(y)[i];
-        // per-channel parameters as 16-byte loads (C % 4 == 0, 16-byte aligned arrays)
-        const f32x4 sc = ld4(scale, c), sh = ld4(shift, c), mu = ld4(mean, c),
-                    is = ld4(invstd, c), k0 = ld4(coef, c), k1 = ld4(coef, C + c);
+    const int c = (int)((i0 * 4) % C);  // fixed: stride * 4 is a multiple of C
+    const f32x4 sc = ld4(scale, c), sh = ld4(shift, c), mu = ld4(mean, c), is = ld4(invstd, c),
+                k0 = ld4(coef, c), k1 = ld4(coef, C + c);
+    auto one = [&](f32x4 d, f32x4 v) {
         f32x4 o;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -204,8 +210,23 @@ __global__ void bn_bwd_apply_kernel(const float* da, const float* __restrict__ y
             const float xh = (v[k] - mu[k]) * is[k];
             o[k] = (g - k0[k] - xh * k1[k]) * sc[k];
         }
-        reinterpret_cast<f32x4*>(dy)[i] = o;
+        return o;
+    };
+    const f32x4* D = reinterpret_cast<const f32x4*>(da);
+    const f32x4* Y = reinterpret_cast<const f32x4*>(y);
+    f32x4* O = reinterpret_cast<f32x4*>(dy);
+    int64_t i = i0;
+    for (; i + 3 * stride < n4; i += 4 * stride) {
+        f32x4 d[4], v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            d[u] = D[i + u * stride];
+            v[u] = Y[i + u * stride];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) O[i + u * stride] = one(d[u], v[u]);
     }
+    for (; i < n4; i += stride) O[i] = one(D[i], Y[i]);
 }
 
 __global__ void bn_relu_apply_kernel(const float* x, const float* sc, const float* sh,
@@ -218,15 +239,22 @@ __global__ void bn_relu_apply_kernel(const float* x, const float* sc, const floa
     }
 }
 
+int g_bn_bwd_blocks = 2048;  // tuning knobs "bn_bwd_blocks" / "bn_bwd_ppt" (A/B timing)
+int g_bn_bwd_ppt = 8;
 namespace {
 struct BwdPlan {
     int nblk;
     int64_t ppb;
 };
-BwdPlan bwd_plan(int64_t npix) {
+// Reduce blocks: as many as keep >= ppt pixels per thread (a block covers 256 / (C/4)
+// pixels per pass), at most g_bn_bwd_blocks: the narrow-pixel, wide-channel layers
+// (C = 512 at 32^2 / 16^2) need many blocks for enough loads in flight -- the former
+// npix/64 rule gave them 1 block per CU (latency-bound, SQ_WAIT_ANY 0.93).
+BwdPlan bwd_plan(int64_t npix, int C) {
     BwdPlan p;
-    int64_t nb = cdiv(npix, 64);
-    if (nb > 1024) nb = 1024;
+    const int slots = 256 / (C / 4 > 0 ? C / 4 : 1);
+    int64_t nb = npix / ((int64_t)slots * (g_bn_bwd_ppt > 0 ? g_bn_bwd_ppt : 1));
+    if (nb > g_bn_bwd_blocks) nb = g_bn_bwd_blocks;
     if (nb < 1) nb = 1;
     p.ppb = cdiv(npix, nb);
     p.nblk = (int)cdiv(npix, p.ppb);
@@ -265,7 +293,7 @@ extern "C" int ugpg_bn_eval_params(const float* gamma, const float* beta, const 
 }
 
 extern "C" size_t ugpg_bn_relu_bwd_workspace(int64_t npix, int C) {
-    BwdPlan p = bwd_plan(npix);
+    BwdPlan p = bwd_plan(npix, C);
     return ((size_t)3 * C * p.nblk + (size_t)2 * C) * sizeof(float);
 }
 
@@ -283,7 +311,7 @@ extern "C" int ugpg_bn_relu_bwd(const float* da, const float* y, int64_t npix, i
         set_error("bn_relu_bwd: workspace %zu < %zu", ws_bytes, need);
         return UGPG_ERR_WORKSPACE;
     }
-    BwdPlan p = bwd_plan(npix);
+    BwdPlan p = bwd_plan(npix, C);
     float* part = static_cast<float*>(ws);
     float* coef = part + (size_t)3 * C * p.nblk;
     hipStream_t st = as_stream(stream);
@@ -293,7 +321,10 @@ extern "C" int ugpg_bn_relu_bwd(const float* da, const float* y, int64_t npix, i
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, part, p.nblk, C, npix,
                        scale, dgamma, dbeta, dbias, acc, coef);
     if (int e = check_launch("bn_bwd_finalize")) return e;
-    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(stream_grid(npix * C / 4)), dim3(256), 0, st, da,
+    // the apply kernel keeps one channel group per thread: grid * 1024 must be a multiple of C
+    const unsigned q = (unsigned)(C / std::gcd(1024, C));
+    const unsigned ga = (stream_grid(npix * C / 4) + q - 1) / q * q;
+    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ga), dim3(256), 0, st, da,
                        y, npix, C, mean, invstd, scale, shift, coef, dy);
     return check_launch("bn_bwd_apply");
 }

@@ -611,6 +611,10 @@ void launch_fwd(const ConvFwdArgs& a, hipStream_t st) {
 
 using namespace ugpg;
 
+namespace ugpg {
+extern int g_bn_bwd_blocks, g_bn_bwd_ppt, g_x6_cw;
+}
+
 extern "C" int ugpg_set_tuning(const char* key, int value) {
     if (key && std::string(key) == "fwd_cfg") {
         g_force_fwd_cfg = value;
@@ -622,6 +626,18 @@ extern "C" int ugpg_set_tuning(const char* key, int value) {
     }
     if (key && std::string(key) == "x6_wgrad") {
         g_x6_wgrad = value;
+        return UGPG_OK;
+    }
+    if (key && std::string(key) == "x6_cw" && (value == 4 || value == 8)) {
+        g_x6_cw = value;
+        return UGPG_OK;
+    }
+    if (key && std::string(key) == "bn_bwd_blocks" && value > 0) {
+        g_bn_bwd_blocks = value;
+        return UGPG_OK;
+    }
+    if (key && std::string(key) == "bn_bwd_ppt" && value > 0) {
+        g_bn_bwd_ppt = value;
         return UGPG_OK;
     }
     if (key && std::string(key) == "x6_probe") {  // timing diagnostics; results are wrong

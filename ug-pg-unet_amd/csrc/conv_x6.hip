@@ -454,11 +454,13 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
 // (g, l) holds channels 4g..4g+3 of pixel l -> one 16-byte store per tile.  BatchNorm
 // partials as x6_epilogue_wave (slot 2*tile + wm), reduced over the pixel lanes of
 // each DPP row.
-template <int TH, int TW>
-__device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a, f32x4 (&acc)[8][2], int tile,
-                                                  int b, int ty0, int tx0, int n0, int wm, int wn) {
+template <int TH, int TW, int NWM = 2>
+__device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a, f32x4 (&acc)[16 / NWM][2],
+                                                  int tile, int b, int ty0, int tx0, int n0, int wm,
+                                                  int wn) {
     static_assert(TH * TW == 256 && (TW == 32 || TW == 16), "256-pixel tiles");
-    constexpr int WR = TH / 2;  // image rows of one wave
+    constexpr int WR = TH / NWM;  // image rows of one wave (NWM pixel groups per tile)
+    constexpr int MTW = 16 / NWM;  // m-tiles of one wave
     auto prow = [](int mt) { return TW == 32 ? mt >> 1 : mt; };
     auto pcol = [](int mt) { return TW == 32 ? (mt & 1) * 16 : 0; };
     const int lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
@@ -491,7 +493,7 @@ __device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a, f32x4 (&
     auto store_tiles = [&](auto accumulate) {
         constexpr bool ACC = decltype(accumulate)::value;
 #pragma unroll
-        for (int mt = 0; mt < 8; ++mt) {
+        for (int mt = 0; mt < MTW; ++mt) {
             const int py = wm * WR + prow(mt), px = pcol(mt) + l16;
             if (py >= vh) break;  // uniform
             const bool ok = px < vw;
@@ -504,7 +506,11 @@ __device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a, f32x4 (&
 #pragma unroll
                 for (int i = 0; i < 4; ++i) v[i] = acc[mt][nt][i] + bv[nt][i];
                 acc[mt][nt] = v;
+#ifdef X6Q_NOSTORE  // diagnostic build: no output stores (results are wrong)
+                if (ok && v[0] == 12345.f) {
+#else
                 if (ok) {
+#endif
                     f32x4* q = reinterpret_cast<f32x4*>(p + 16 * nt);
                     if constexpr (ACC) {
                         const f32x4 o = *q;
@@ -537,7 +543,7 @@ __device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a, f32x4 (&
         q[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
-    for (int mt = 0; mt < 8; ++mt) {
+    for (int mt = 0; mt < MTW; ++mt) {
         if (wm * WR + prow(mt) >= vh) break;  // uniform
         if (pcol(mt) + l16 < vw) {
 #pragma unroll
@@ -564,7 +570,8 @@ __device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a, f32x4 (&
                 sv = psum[t >> 2][t & 3];
                 qv = q[t >> 2][t & 3];
             }
-        const size_t n = n0 + c0 + 16 * nt + i, S = 2 * (size_t)a.ntiles, slot = 2 * (size_t)tile + wm;
+        const size_t n = n0 + c0 + 16 * nt + i, S = NWM * (size_t)a.ntiles,
+                     slot = NWM * (size_t)tile + wm;
         a.stats[(0 * (size_t)a.Cout + n) * S + slot] = cnt;
         a.stats[(1 * (size_t)a.Cout + n) * S + slot] = sv;
         a.stats[(2 * (size_t)a.Cout + n) * S + slot] = qv;
@@ -608,10 +615,14 @@ extern "C" int ugpg_debug_clock(double* mhz) {
     return n;
 }
 #endif
-template <int NP, bool M16, int TWT = 32>
-__global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) {
+// NCW = compute waves: 4 (one per SIMD) or 8 (two per SIMD, 16x16x32 form only: while one
+// waits on an LDS read or a barrier the other issues MFMAs; each covers a quarter of the
+// item's pixels, so a tile has NCW/2 BatchNorm stat slots)
+template <int NP, bool M16, int TWT = 32, int NCW = 4>
+__global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) {
     static_assert(!M16 || NP == 3, "the 16x16x32 form pairs the split-bf16 products");
     static_assert(TWT == 32 || (M16 && TWT == 16), "16-wide tiles only in the 16x16x32 form");
+    static_assert(NCW == 4 || (NCW == 8 && M16), "two compute waves per SIMD: 16x16x32 form only");
     // 256-pixel items: 8 x 32 (images >= 32 wide) or 16 x 16 (16-31 wide, 16x16x32 form)
     constexpr int TW = TWT, TH = 256 / TWT, BN = 64, BKC = 16, MT = 4;
     constexpr int HWD = TW + 2, HS = HWD;
@@ -636,7 +647,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
     u32x4* const dummy = smem + 2 * A_VECS + NSLOT * R_STR;  // writes of idle lanes
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const bool loader = wave >= 4;
+    const bool loader = wave >= NCW;
     const int NB = a.Cout / BN;
     const int nitems = a.ntiles * NB;
     const int nslots = gridDim.x >> 3;
@@ -670,7 +681,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
         // Halo of step s: loaded into register set s & 1 (f32, with its activation
         // coefficients) three steps ahead, written (activated, split) into A buffer s & 1
         // during phases 0-1 of step s-1.  Weight rows: LDS-DMA, see below.
-        const int lt = tid - 256;
+        const int lt = tid - NCW * 64;
         const int hhl = (lt >> 4) & 1;  // channel half of this lane (same for all its items)
         auto item_px = [](int idx) { return (idx >> 5) * 16 + (idx & 15); };
         f32x4 ra[2][A_PER][2];
@@ -859,7 +870,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
         vm_wait<0>();  // no load outlives the workgroup (nothing may run before this wait:
                        // the last loads' destination registers are dead to the compiler)
 #ifdef X6R_STAMP
-        if (tid == 256 && blockIdx.x < 1024) {
+        if (tid == NCW * 64 && blockIdx.x < 1024) {
             g_clk[8 * blockIdx.x] = __builtin_amdgcn_s_memtime() - st_t0;
             for (int q = 0; q < 3; ++q) {
                 g_clk[8 * blockIdx.x + 1 + q] = st_vm[q];
@@ -881,24 +892,26 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
         // accumulators; the next unit's A fragments and, spread over the tap, the next
         // tap's six W fragments are read while it runs.
         const int g = lane >> 4, l16 = lane & 15;
-        // m-tile mt of a wave = 16 pixels: row mt/2, columns 16(mt&1).. (8 x 32 tiles) or
-        // row mt (16 x 16 tiles); a wave covers TH/2 image rows
-        const int a01 = g * NHP + wm * (TH / 2) * HS + l16;
-        const int a02 = ((g >> 1) * 4 + (g & 1)) * NHP + wm * (TH / 2) * HS + l16;
+        // NWM pixel groups per tile: a wave covers TH/NWM image rows = MTW m-tiles of 16
+        // pixels (row mt/2, columns 16(mt&1).. for 8 x 32 tiles; row mt for 16 x 16 tiles)
+        constexpr int NWM = NCW / 2, MTW = 16 / NWM, URT = MTW / 2, UPS = 9 * URT;
+        constexpr int WPU = (6 + URT - 1) / URT;  // next tap's W fragments read per unit
+        const int a01 = g * NHP + wm * (TH / NWM) * HS + l16;
+        const int a02 = ((g >> 1) * 4 + (g & 1)) * NHP + wm * (TH / NWM) * HS + l16;
         const int bo = (g & 1) * 3 * BN + wn * 32 + l16;
         const int wq[3] = {bo + 4 * 3 * BN * (g < 2 ? 1 : 0), bo + 2 * 3 * BN, bo};  // W20, W11, W00
-        f32x4 acc[8][2];
+        f32x4 acc[MTW][2];
 #pragma unroll
-        for (int mt = 0; mt < 8; ++mt)
+        for (int mt = 0; mt < MTW; ++mt)
 #pragma unroll
             for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #ifndef X6Q_DEPTH
 #define X6Q_DEPTH 1
 #endif
-        constexpr int DA = X6Q_DEPTH;  // A fragments are read DA units ahead (36 % (DA+1) == 0)
-        static_assert(36 % (DA + 1) == 0, "unit ring must divide a step");
+        constexpr int DA = X6Q_DEPTH;  // A fragments are read DA units ahead
+        static_assert(UPS % (DA + 1) == 0, "unit ring must divide a step");
         u32x4 fa[DA + 1][2][2];  // [unit % (DA+1)][m-tile of the pair][A02, A01]
-        u32x4 fw[3][3][2];     // [tap % 3 (9 taps per step)][W20, W11, W00][nt]
+        u32x4 fw[2][3][2];     // [tap & 1][W20, W11, W00][nt]
         auto lda = [&](const u32x4* As, int t, int r, u32x4 (&f)[2][2]) {
             const int ky = t / 3, kx = t % 3;
 #pragma unroll
@@ -919,7 +932,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
         int cc = 0, item = item0;
         Pos cp = pos_of(item0);
 #pragma unroll
-        for (int uu = 0; uu < DA; ++uu) lda(smem, uu / 4, uu % 4, fa[uu]);
+        for (int uu = 0; uu < DA; ++uu) lda(smem, uu / URT, uu % URT, fa[uu]);
 #pragma unroll
         for (int e = 0; e < 6; ++e) ldw(Bring, 0, e, fw[0]);
         for (int k = 0; k < total; ++k) {
@@ -930,18 +943,22 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
                 const int tn = t + 1 < 9 ? t + 1 : 0;  // next tap (of this step or the next)
                 const u32x4* Bn = Bring + ((3 * k + (t + 1) / 3) % NSLOT) * R_STR;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int u = t * 4 + r;
-                    // next unit's A fragments, then (units 0-2 of the tap) next tap's W
+                for (int r = 0; r < URT; ++r) {
+                    const int u = t * URT + r;
+                    // next unit's A fragments, then (spread over the tap) next tap's W
                     const int un = u + DA;
-                    if (un < 36) lda(Ac, un / 4, un % 4, fa[un % (DA + 1)]);
-                    else lda(An, (un - 36) / 4, (un - 36) % 4, fa[un % (DA + 1)]);
-                    if (r < 3) {
-                        ldw(Bn, tn % 3, 2 * r, fw[(t + 1) % 3]);
-                        ldw(Bn, tn % 3, 2 * r + 1, fw[(t + 1) % 3]);
-                    }
+                    if (un < UPS) lda(Ac, un / URT, un % URT, fa[un % (DA + 1)]);
+                    else lda(An, (un - UPS) / URT, (un - UPS) % URT, fa[un % (DA + 1)]);
+                    constexpr int NWR = 0;
+                    int nw = NWR;
+#pragma unroll
+                    for (int j = 0; j < WPU; ++j)
+                        if (r * WPU + j < 6) {
+                            ldw(Bn, tn % 3, r * WPU + j, fw[(t + 1) & 1]);
+                            ++nw;
+                        }
                     const u32x4(&A)[2][2] = fa[u % (DA + 1)];
-                    const u32x4(&W)[3][2] = fw[t % 3];
+                    const u32x4(&W)[3][2] = fw[t & 1];
 #pragma unroll
                     for (int e = 0; e < 3; ++e)
 #pragma unroll
@@ -953,19 +970,20 @@ __global__ void __launch_bounds__(512, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) 
 #pragma unroll
                     for (int i = 0; i < 12; ++i) {
                         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-                        if (i < (r < 3 ? 6 : 4)) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                        if (i < 4 + nw) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 }
                 if (t % 3 == 2) read_barrier();
             }
             if (++cc == nchunk) {
-                x6q_epilogue_wave<TH, TW>(a, acc, cp.tile, cp.b, cp.ty0, cp.tx0, cp.nb * BN, wm, wn);
+                x6q_epilogue_wave<TH, TW, NWM>(a, acc, cp.tile, cp.b, cp.ty0, cp.tx0, cp.nb * BN, wm,
+                                               wn);
                 cc = 0;
                 item += nslots;
                 if (item < iend) cp = pos_of(item);
 #pragma unroll
-                for (int mt = 0; mt < 8; ++mt)
+                for (int mt = 0; mt < MTW; ++mt)
 #pragma unroll
                     for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
             }
@@ -1691,7 +1709,14 @@ int fwd_x6_tile_w(int W, int np) { return W >= 32 ? 32 : 16; }
 int fwd_x6_tile_h(int W, int np) {
     return use_x6r(W, np) ? (W >= 32 ? 8 : 16) : (W >= 32 ? 4 : 8);
 }
-int fwd_x6_stat_slots(int ntiles, int W, int np) { return use_x6r(W, np) ? 2 * ntiles : ntiles; }
+#ifndef X6R_CW_DEFAULT
+#define X6R_CW_DEFAULT 4
+#endif
+int g_x6_cw = X6R_CW_DEFAULT;  // tuning knob "x6_cw": compute waves of the 16x16x32 persistent form
+static int x6r_cw(int np) { return np == 3 && g_x6_pipe >= 2 && g_x6_cw == 8 ? 8 : 4; }
+int fwd_x6_stat_slots(int ntiles, int W, int np) {
+    return use_x6r(W, np) ? x6r_cw(np) / 2 * ntiles : ntiles;
+}
 
 // tuning knob "x6_pipe": conv3x3_fwd_x6r_kernel for images >= 32 wide with 16x16x32
 // tiles (2, default) or 32x32x16 tiles (1); 3 = as 2 plus 16x16-pixel items for images
@@ -1707,8 +1732,15 @@ void launch_fwd_x6(const ConvFwdArgs& a_in, int np, hipStream_t st) {
         // walking a strided share of its XCD's contiguous item range
         int64_t g = std::min<int64_t>(cu_count(st), (items + 7) / 8 * 8);
         g = std::max<int64_t>(8, g / 8 * 8);
-        if (np == 3 && g_x6_pipe >= 2 && a.W < 32)
+        const bool cw8 = x6r_cw(np) == 8;
+        if (np == 3 && g_x6_pipe >= 2 && a.W < 32 && cw8)
+            hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<3, true, 16, 8>), dim3((unsigned)g), dim3(768),
+                               0, st, a);
+        else if (np == 3 && g_x6_pipe >= 2 && a.W < 32)
             hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<3, true, 16>), dim3((unsigned)g), dim3(512),
+                               0, st, a);
+        else if (np == 3 && g_x6_pipe >= 2 && cw8)
+            hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<3, true, 32, 8>), dim3((unsigned)g), dim3(768),
                                0, st, a);
         else if (np == 3 && g_x6_pipe >= 2)
             hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<3, true>), dim3((unsigned)g), dim3(512), 0,

@@ -326,8 +326,11 @@ def broadcast_parameters(module: torch.nn.Module, src: int = 0):
     _, ws = world()
     if ws <= 1:
         return
-    for t in list(module.parameters()) + list(module.buffers()):
+    params = list(module.parameters())
+    for t in params + list(module.buffers()):
         dist.broadcast(t.data, src)
+    from . import ops
+    ops.weights_written(params)  # written behind autograd's back: cached packs are stale
 
 
 def broadcast_buffers(module: torch.nn.Module, src: int = 0):

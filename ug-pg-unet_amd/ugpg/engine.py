@@ -169,7 +169,7 @@ class UNetGraph:
         specs = []
         for blk in self.blocks:
             (c1, _), (c2, _) = _conv_bn(blk.mod.conv_op)
-            w1, w2 = c1.weight.detach(), c2.weight.detach()
+            w1, w2 = c1.weight, c2.weight  # parameters: packs are cached on them
             cin = cpad if blk.kind == "inc" else w1.shape[1]
             specs += [(w1, ops.conv_pack_k(cin), 0), (w2, ops.conv_pack_k(w2.shape[1]), 0)]
             if save:
@@ -185,8 +185,8 @@ class UNetGraph:
         packs = ops.prepack(self._pack_specs(ceil_to(x.shape[1], 8), save))
         with ops.prepacked(packs):
             logits, state = self._forward(x, save)
-        if save:
-            state["packs"] = packs
+        if save:  # the backward needs only the data-gradient (mode 1) packs
+            state["packs"] = {k: v for k, v in packs.items() if k[4] == 1}
         return logits, state
 
     def _forward(self, x, save: bool):

@@ -134,14 +134,25 @@ def _pack_key(w, cin_pad, mode):
     return (w.data_ptr(), w._version, tuple(w.shape), int(cin_pad), int(mode), _conv_math)
 
 
+def _cache_key(cin_pad, mode):
+    return (int(cin_pad), int(mode), _conv_math)
+
+
 def prepack(specs):
-    """Pack many (weight, cin_pad, mode) in one launch (split-bf16 formats only);
-    returns {key: packed} for pack_conv3x3 to consult while the table is active."""
+    """Pack many (parameter, cin_pad, mode) in one launch (split-bf16 formats only);
+    returns {key: packed} for pack_conv3x3 to consult while the table is active.
+
+    Packs persist on the parameter (``_ugpg_packs``), keyed by its storage address and
+    version counter: a weight that has not changed since its last pack -- the frozen
+    previous stage that produces the uncertainty map -- is not repacked every step.
+    Every writer of parameters bumps the version (ugpg's optimizers, broadcasts,
+    load_state_dict), so a stale pack is never used."""
     table = {}
     if _conv_math not in ("x6", "bf16") or not specs or not _PREPACK_ON:
         return table
     items, outs = [], []
-    for w, cin_pad, mode in specs:
+    for p, cin_pad, mode in specs:
+        w = p.detach()
         cout, cin = w.shape[0], w.shape[1]
         fmt = conv_weight_format(cout, cin_pad) if mode == 0 else conv_weight_format(cin_pad, cout)
         if fmt != _MATH_FMT[_conv_math] or not w.is_contiguous() or w.dtype != F32:
@@ -149,10 +160,16 @@ def prepack(specs):
         key = _pack_key(w, cin_pad, mode)
         if key in table:
             continue
+        cache = p.__dict__.setdefault("_ugpg_packs", {}) if isinstance(p, torch.nn.Parameter) else {}
+        hit = cache.get(_cache_key(cin_pad, mode))
+        if hit is not None and hit[0] == key:
+            table[key] = hit[1]
+            continue
         out = torch.empty(lib.ugpg_pack_conv3x3_bytes(cout, cin_pad, fmt), dtype=torch.uint8,
                           device=w.device)
         out.ugpg_fmt = fmt
         table[key] = out
+        cache[_cache_key(cin_pad, mode)] = (key, out)
         items.append(PackItem(ptr(w), ptr(out), cout, cin, int(cin_pad), int(mode)))
         outs.append(out)
     if items:
@@ -160,6 +177,13 @@ def prepack(specs):
         check(lib.ugpg_pack_conv3x3_batch(arr, len(items), _MATH_FMT[_conv_math], stream()),
               "pack_conv3x3_batch")
     return table
+
+
+def weights_written(params):
+    """Record an in-place write to `params` that bypassed autograd (raw-pointer kernels,
+    collectives): bump their version counters so cached packs are not reused."""
+    from torch.autograd.graph import increment_version
+    increment_version([p for p in params])
 
 
 class prepacked:

@@ -72,6 +72,7 @@ class RMSprop(Optimizer):
                     g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
                     ops.rmsprop_step(p.data, g, self.state[p]["square_avg"], lr, a, eps, wd,
                                      self.grad_scale)
+            ops.weights_written(params)  # the kernels wrote through raw pointers
         return loss
 
 
@@ -134,4 +135,5 @@ class Adam(Optimizer):
                     g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
                     ops.adam_step(p.data, g, st["exp_avg"], st["exp_avg_sq"], lr, b1, b2, eps, wd,
                                   int(st["step"]), self.grad_scale)
+            ops.weights_written(params)  # the kernels wrote through raw pointers
         return loss
