@@ -188,6 +188,11 @@ int ugpg_bilinear_nhwc_bwd(const float* dout, int B, int Ho, int Wo, int C, floa
  *  mode 2: U = 1 - 2|bilinear(sigmoid(in)) - 0.5|  (uncertainty map, UG_unet.py:45-57) */
 int ugpg_resize_nchw(const float* in, int B, int C, int Hi, int Wi, float* out, int Ho, int Wo,
                      int mode, void* stream);
+/* gradient of ugpg_resize_nchw mode 0 w.r.t. its input (autograd of F.interpolate(bilinear,
+ * align_corners=True), ProgressiveUNet.forward UG_unet.py:418-424): din (B,C,Hi,Wi) from
+ * dout (B,C,Ho,Wo), gather form, deterministic */
+int ugpg_resize_nchw_bwd(const float* dout, int B, int C, int Ho, int Wo, float* din, int Hi,
+                         int Wi, void* stream);
 /* NCHW <-> NHWC (with zero channel padding to Cpad) */
 int ugpg_nchw_to_nhwc(const float* in, int B, int C, int H, int W, float* out, int Cpad,
                       void* stream);

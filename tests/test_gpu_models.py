@@ -8,6 +8,7 @@ import torch
 from oracle import detgen as G
 from oracle import ref_cpu as O
 from tests._parity import (det_state, grad_check, is_prebn_bias, noise_floor, oracle_run,
+                           perturbed_state,
                            param_keys)
 
 pytestmark = pytest.mark.gpu
@@ -411,3 +412,41 @@ def test_weight_pack_cache_reuse_and_invalidation(dev):
     with torch.no_grad():
         o4 = m(x)
     assert torch.equal(o4, fresh_logits())
+
+
+def test_progressive_unet_forward_with_input_gradient(dev):
+    """ProgressiveUNet.forward resizes its input to the stage resolution (UG_unet.py:413-426);
+    logits and the gradient w.r.t. the ORIGINAL-size input (through the resize and the
+    network's data gradient) vs the oracle (F.interpolate + pgunet_forward on the CPU)."""
+    import torch.nn.functional as F
+    import ugpg
+    stage = 2
+    pu = ugpg.ProgressiveUNet(3, 1)
+    pu.set_stage(stage)
+    state = det_state(stage, 3, 1)
+    pu.stages[stage].load_state_dict(state)
+    pu = pu.to(dev).train()
+    x = G.randn(7, (2, 3, 96, 80), "x")
+    w = G.randn(8, (2, 1, 64, 64), "w")
+
+    def oracle(dtype, st):
+        xx = x.to(dtype).clone().requires_grad_(True)
+        P = {k: (v.to(dtype) if v.is_floating_point() else v.clone()) for k, v in st.items()}
+        out = O.pgunet_forward(stage, P, F.interpolate(xx, size=(64, 64), mode="bilinear",
+                                                       align_corners=True), training=True)
+        (out * w.to(dtype)).sum().backward()
+        return out.detach(), xx.grad
+
+    xd = x.to(dev).requires_grad_(True)
+    out = pu(xd)
+    (out * w.to(dev)).sum().backward()
+    o32, g32 = oracle(torch.float32, state)
+    _, g64 = oracle(torch.float64, state)
+    assert out.shape == (2, 1, 64, 64)
+    assert (out.detach().cpu() - o32).abs().max().item() <= 1e-3
+    floor = (g32.double() - g64).abs().max().item()
+    for s, rel in ((7, 1e-7), (10, 1e-6), (12, 5e-6)):
+        _, gp = oracle(torch.float32, perturbed_state(state, s, rel))
+        floor = max(floor, (gp.double() - g64).abs().max().item())
+    err = (xd.grad.cpu().double() - g64).abs().max().item()
+    assert err <= 3 * floor + 1e-6 * g64.abs().max().item(), (err, floor)

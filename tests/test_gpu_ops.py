@@ -478,3 +478,19 @@ def test_pack_batch_matches_single_packs(dev, conv_math):
             assert ops.pack_conv3x3(w, k, m) is not table.get(ops._pack_key(w, k, m), None)
     finally:
         ops.set_conv_math(old)
+
+
+@pytest.mark.parametrize("hi,wi,ho,wo", [(96, 80, 64, 64), (32, 32, 256, 256), (256, 256, 128, 128),
+                                         (17, 29, 40, 33), (64, 64, 64, 64)])
+def test_resize_bilinear_backward(dev, hi, wi, ho, wo):
+    """Input gradient of the align-corners resize (ProgressiveUNet.forward's F.interpolate)
+    vs torch autograd of F.interpolate in fp32 on the CPU: the same fp32 source-index and
+    weight arithmetic (an fp64 reference computes different weights: src = o*(in-1)/(out-1)
+    carries ~1e-5 of fp32 rounding at o ~ 127), summed in a different order."""
+    from ugpg import ops
+    x = torch.randn(2, 3, hi, wi, requires_grad=True)
+    g = torch.randn(2, 3, ho, wo)
+    torch.nn.functional.interpolate(x, size=(ho, wo), mode="bilinear", align_corners=True).backward(g)
+    got = ops.resize_nchw_bwd(g.to(dev), hi, wi).cpu().double()
+    ref = x.grad.double()
+    assert (got - ref).abs().max().item() <= 1e-5 * max(1.0, ref.abs().max().item())

@@ -911,7 +911,7 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
         constexpr int DA = X6Q_DEPTH;  // A fragments are read DA units ahead
         static_assert(UPS % (DA + 1) == 0, "unit ring must divide a step");
         u32x4 fa[DA + 1][2][2];  // [unit % (DA+1)][m-tile of the pair][A02, A01]
-        u32x4 fw[2][3][2];     // [tap & 1][W20, W11, W00][nt]
+        u32x4 fw[3][3][2];     // [tap % 3 (9 taps per step)][W20, W11, W00][nt]
         auto lda = [&](const u32x4* As, int t, int r, u32x4 (&f)[2][2]) {
             const int ky = t / 3, kx = t % 3;
 #pragma unroll
@@ -954,11 +954,11 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
 #pragma unroll
                     for (int j = 0; j < WPU; ++j)
                         if (r * WPU + j < 6) {
-                            ldw(Bn, tn % 3, r * WPU + j, fw[(t + 1) & 1]);
+                            ldw(Bn, tn % 3, r * WPU + j, fw[(t + 1) % 3]);
                             ++nw;
                         }
                     const u32x4(&A)[2][2] = fa[u % (DA + 1)];
-                    const u32x4(&W)[3][2] = fw[t & 1];
+                    const u32x4(&W)[3][2] = fw[t % 3];
 #pragma unroll
                     for (int e = 0; e < 3; ++e)
 #pragma unroll

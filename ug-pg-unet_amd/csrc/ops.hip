@@ -303,6 +303,38 @@ __global__ void resize_nchw_kernel(const float* in, int BC, int Hi, int Wi, floa
     }
 }
 
+// gradient of resize_nchw mode 0 (bilinear, align_corners=True; ProgressiveUNet.forward's
+// input resize, UG_unet.py:418-424): gather form -- each input pixel sums w_y * w_x * dy
+// over the outputs whose interpolation reads it (the same index/weight arithmetic as the
+// forward), deterministic, no atomics.
+__global__ void resize_nchw_bwd_kernel(const float* dout, int BC, int Ho, int Wo, float* din,
+                                       int Hi, int Wi) {
+    const int64_t total = (int64_t)BC * Hi * Wi;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int x = (int)(i % Wi);
+        const int64_t r = i / Wi;
+        const int y = (int)(r % Hi);
+        const int64_t bc = r / Hi;
+        const float* g = dout + bc * Ho * Wo;
+        int ylo, yhi, xlo, xhi;
+        ac_range_tight(y, Hi, Ho, ylo, yhi);
+        ac_range_tight(x, Wi, Wo, xlo, xhi);
+        float acc = 0.f;
+        for (int oy = ylo; oy <= yhi; ++oy) {
+            const float wy = ac_weight(oy, y, Hi, Ho);
+            if (wy == 0.f) continue;
+            float row = 0.f;
+            for (int ox = xlo; ox <= xhi; ++ox) {
+                const float wx = ac_weight(ox, x, Wi, Wo);
+                if (wx != 0.f) row = fmaf(wx, g[(size_t)oy * Wo + ox], row);
+            }
+            acc = fmaf(wy, row, acc);
+        }
+        din[i] = acc;
+    }
+}
+
 __global__ void nchw_to_nhwc_kernel(const float* in, int B, int C, int HW, float* out, int Cp) {
     const int64_t total = (int64_t)B * HW * Cp;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
@@ -1116,6 +1148,16 @@ extern "C" int ugpg_resize_nchw(const float* in, int B, int C, int Hi, int Wi, f
     hipLaunchKernelGGL(resize_nchw_kernel, dim3(stream_grid(total)), dim3(256), 0,
                        as_stream(stream), in, B * C, Hi, Wi, out, Ho, Wo, mode);
     return check_launch("resize_nchw");
+}
+
+extern "C" int ugpg_resize_nchw_bwd(const float* dout, int B, int C, int Ho, int Wo, float* din,
+                                    int Hi, int Wi, void* stream) {
+    UGPG_REQUIRE(dout && din && B > 0 && C > 0 && Ho > 0 && Wo > 0 && Hi > 0 && Wi > 0,
+                 "resize_nchw_bwd");
+    const int64_t total = (int64_t)B * C * Hi * Wi;
+    hipLaunchKernelGGL(resize_nchw_bwd_kernel, dim3(stream_grid(total)), dim3(256), 0,
+                       as_stream(stream), dout, B * C, Ho, Wo, din, Hi, Wi);
+    return check_launch("resize_nchw_bwd");
 }
 
 extern "C" int ugpg_nchw_to_nhwc(const float* in, int B, int C, int H, int W, float* out, int Cp,

@@ -61,6 +61,7 @@ SIGNATURES = {
     "ugpg_bilinear_nhwc_fwd": (_i, [Src, _i, _i, _i, _p, _i, _i, _p]),
     "ugpg_bilinear_nhwc_bwd": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _i, _p]),
     "ugpg_resize_nchw": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _i, _p]),
+    "ugpg_resize_nchw_bwd": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _p]),
     "ugpg_nchw_to_nhwc": (_i, [_p, _i, _i, _i, _i, _p, _i, _p]),
     "ugpg_nhwc_to_nchw": (_i, [_p, _i, _i, _i, _i, _i, _p, _i, _p]),
     "ugpg_head_fwd": (_i, [Src, _i64, _p, _p, _i, _p, _p]),
@@ -123,6 +124,11 @@ class _Lib:
                 fn.restype = res
                 fn.argtypes = args
             self._lib = lib
+            # UGPG_TUNE="key=value,...": kernel tuning knobs (ugpg_set_tuning) for A/B runs
+            for kv in filter(None, os.environ.get("UGPG_TUNE", "").split(",")):
+                k, _, v = kv.partition("=")
+                if lib.ugpg_set_tuning(k.strip().encode(), int(v)) != 0:
+                    raise ValueError(f"UGPG_TUNE: {lib.ugpg_last_error().decode()}")
         return self._lib
 
     def __getattr__(self, name):

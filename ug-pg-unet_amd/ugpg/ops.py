@@ -368,6 +368,15 @@ def resize_nchw(x, Ho, Wo, mode):
     return out
 
 
+def resize_nchw_bwd(dout, Hi, Wi):
+    """Input gradient of resize_nchw(..., RESIZE_BILINEAR)."""
+    B, C, Ho, Wo = dout.shape
+    din = empty(B, C, Hi, Wi, like=dout)
+    check(lib.ugpg_resize_nchw_bwd(_f32(dout.contiguous()), B, C, Ho, Wo, ptr(din), Hi, Wi,
+                                   stream()), "resize_nchw_bwd")
+    return din
+
+
 def nchw_to_nhwc(x, cpad):
     x = x.contiguous()
     B, c, H, W = x.shape

@@ -100,12 +100,26 @@ class PGUNet4(_PGUNetBase):
 STAGE_CLASSES = {1: PGUNet1, 2: PGUNet2, 3: PGUNet3, 4: PGUNet4}
 
 
+class _ResizeFn(torch.autograd.Function):
+    """Bilinear align-corners resize with its gather-form input gradient."""
+
+    @staticmethod
+    def forward(ctx, x, res):
+        ctx.hw = x.shape[-2:]
+        return ops.resize_nchw(x.detach().float().contiguous(), res, res, ops.RESIZE_BILINEAR)
+
+    @staticmethod
+    def backward(ctx, dout):
+        return ops.resize_nchw_bwd(dout.contiguous(), *ctx.hw), None
+
+
 def resize_input(x, res):
-    """F.interpolate(x, size=(res,res), bilinear, align_corners=True) on the GPU."""
+    """F.interpolate(x, size=(res,res), bilinear, align_corners=True) on the GPU, with
+    its gradient when the input requires one (UG_unet.py:418-424)."""
     if x.shape[-2:] == (res, res):
         return x
     if x.requires_grad and torch.is_grad_enabled():
-        raise NotImplementedError("ugpg: gradients through the input resize are not supported")
+        return _ResizeFn.apply(x, res)
     return ops.resize_nchw(x.detach().float(), res, res, ops.RESIZE_BILINEAR)
 
 
