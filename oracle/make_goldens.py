@@ -24,6 +24,7 @@ Fixture map:
   g8_dp_shards.npz        DP semantics: mean of 2 per-shard local-BN gradients, step, 6-tuple
   g9_rng.json             RNG positions after ProgressiveUNet / trainer ctor / transfer
   g10_monuseg_eval.npz    MoNuSegEvaluator.calculate_metrics and predict_image, run for real
+  g11_checkpoint_interop.json  checkpoints round-trip reference <-> ugpg (asserted when generated)
   g4b_pgunet4_bs16.npz    config 2 at bs16 x 256^2: checksums, fp32 noise floors
 """
 from __future__ import annotations
@@ -697,6 +698,81 @@ def g10(RU):
     save_npz("g10_monuseg_eval.npz", **fx)
 
 
+def g11(RU):
+    """Checkpoint interop in both directions, asserted here with the real
+    reference code (files in a temporary directory, nothing committed but the summary):
+    the reference trainer's best-checkpoint dict (uncertainty_guided_trainer.py:382-393)
+    loads into ugpg's trainer (load_stage_weights) and MoNuSegTester; ugpg-written dict and
+    raw state_dict checkpoints load into the reference's MoNuSegEvaluator.load_model
+    (test_monuseg.py:120-162) and its trainer's load_stage_weights (:469-473)."""
+    import tempfile
+    import types
+    import uncertainty_guided_trainer as RT  # noqa: E402
+    from torch.utils.data import DataLoader, TensorDataset
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "ug-pg-unet_amd"))
+    import ugpg  # noqa: E402
+    from ugpg.evaluation import MoNuSegTester
+    for mod, attrs in (("cv2", {}), ("monuseg_dataset", {"MoNuSegDataset": object}),
+                       ("preprocessing_utils", {"xml_to_mask": None})):
+        if mod not in sys.modules:
+            m = types.ModuleType(mod)
+            for a, v in attrs.items():
+                setattr(m, a, v)
+            sys.modules[mod] = m
+    mp = os.path.join(REF, "MoNuSegImprove")
+    if mp not in sys.path:
+        sys.path.insert(0, mp)
+    import test_monuseg as TM  # noqa: E402
+    out = {}
+    with tempfile.TemporaryDirectory() as d:
+        # reference -> ugpg: a real best-checkpoint from the reference's driver (stage 1)
+        torch.manual_seed(0)
+        tr = RT.UncertaintyGuidedProgressiveTrainer(3, 1, device="cpu")
+        tr.stage_configs[1]["epochs_per_stage"] = 1
+        x = G.randn(111, (4, 3, 32, 32), "x")
+        t = G.bernoulli(112, (4, 1, 32, 32), 0.4, "t")
+        loader = DataLoader(TensorDataset(x, t), batch_size=2)
+        tr.train_progressive(loader, loader, max_stages=1, save_dir=d)
+        ck = Path(d) / "ug_pgunet_stage1_best.pth"
+        assert ck.exists()
+        want = tr.models[1].state_dict()
+        mine = ugpg.UncertaintyGuidedProgressiveTrainer(3, 1, device="cpu")
+        mine.load_stage_weights(1, str(ck))
+        for k, v in mine.models[1].state_dict().items():
+            assert torch.equal(v, want[k]), k
+        tester = MoNuSegTester(str(ck), device="cpu")
+        assert tester.stage == 1 and all(torch.equal(v, want[k]) for k, v in
+                                         tester.model.state_dict().items())
+        keys = sorted(torch.load(ck, weights_only=True).keys())
+        out["reference_checkpoint_keys"] = keys
+        # ugpg -> reference: ugpg's checkpoint dict (trainer.train_progressive's format) and a
+        # raw state_dict (train_aug_monuseg.py:258-260)
+        torch.manual_seed(3)
+        m4 = ugpg.PGUNet4(3, 1)
+        opt = ugpg.RMSprop(m4.parameters(), lr=1e-4, weight_decay=1e-4)
+        ck2 = Path(d) / "ugpg_stage4.pth"
+        torch.save({"stage": 4, "epoch": 0, "model_state_dict": m4.state_dict(),
+                    "optimizer_state_dict": opt.state_dict(), "val_dice": 0.5, "train_dice": 0.5,
+                    "uncertainty_alpha": 1.0, "history": mine.history}, ck2)
+        ev = object.__new__(TM.MoNuSegEvaluator)
+        ev.device = "cpu"
+        ref_model = ev.load_model(str(ck2))
+        assert all(torch.equal(v, m4.state_dict()[k]) for k, v in ref_model.state_dict().items())
+        ck3 = Path(d) / "ugpg_raw.pth"
+        torch.save(m4.state_dict(), ck3)
+        ref_model = ev.load_model(str(ck3))
+        assert all(torch.equal(v, m4.state_dict()[k]) for k, v in ref_model.state_dict().items())
+        rt = RT.UncertaintyGuidedProgressiveTrainer(3, 1, device="cpu")
+        rt.load_stage_weights(4, str(ck2))
+        assert all(torch.equal(v, m4.state_dict()[k]) for k, v in rt.models[4].state_dict().items())
+        out["ugpg_to_reference"] = ["MoNuSegEvaluator.load_model(dict)", "MoNuSegEvaluator.load_model(raw)",
+                                    "UncertaintyGuidedProgressiveTrainer.load_stage_weights"]
+        out["reference_to_ugpg"] = ["UncertaintyGuidedProgressiveTrainer.load_stage_weights",
+                                    "MoNuSegTester"]
+    (OUT / "g11_checkpoint_interop.json").write_text(json.dumps(out, indent=1))
+    print("wrote g11_checkpoint_interop.json")
+
+
 def g0(RU):
     """state_dict keys/shapes/dtypes of every reference model (checkpoint format)."""
     out = {}
@@ -737,6 +813,7 @@ def main():
     g8(RU)
     g9(RU)
     g10(RU)
+    g11(RU)
     g4b(RU)
 
 

@@ -612,7 +612,7 @@ void launch_fwd(const ConvFwdArgs& a, hipStream_t st) {
 using namespace ugpg;
 
 namespace ugpg {
-extern int g_bn_bwd_blocks, g_bn_bwd_ppt, g_x6_cw;
+extern int g_bn_bwd_blocks, g_bn_bwd_ppt, g_x6_cw, g_x6_order;
 }
 
 extern "C" int ugpg_set_tuning(const char* key, int value) {
@@ -626,6 +626,10 @@ extern "C" int ugpg_set_tuning(const char* key, int value) {
     }
     if (key && std::string(key) == "x6_wgrad") {
         g_x6_wgrad = value;
+        return UGPG_OK;
+    }
+    if (key && std::string(key) == "x6_order" && (value == 0 || value == 1)) {
+        g_x6_order = value;
         return UGPG_OK;
     }
     if (key && std::string(key) == "x6_cw" && (value == 4 || value == 8)) {
@@ -689,6 +693,7 @@ extern "C" int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream) {
     }
     ConvFwdArgs a;
     a.probe = 0;
+    a.order = 0;
     a.src0 = p->src[0].data;
     a.sc0 = p->src[0].scale;
     a.sh0 = p->src[0].shift;

@@ -25,6 +25,8 @@ struct ConvFwdArgs {
     int B, H, W, Cin, Cout;
     int tiles_x, tiles_y, ntiles;
     int probe;  // diagnostics only (tuning knob "x6_probe"): bit0 skip prefetch, bit1 skip staging
+    int order;  // persistent x6r item order: 0 = tile-major (it = tile*NB + nb), 1 = column-
+                // block-major (it = nb*ntiles + tile: an XCD's range shares one weight slab)
 };
 
 // Output pixel (row*TW + col inside the tile) of GEMM row m.  PERM16 is the

@@ -667,8 +667,8 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
     };
     auto pos_of = [&](int it) {
         Pos p;
-        p.nb = it % NB;
-        p.tile = it / NB;
+        p.nb = a.order ? it / a.ntiles : it % NB;
+        p.tile = a.order ? it % a.ntiles : it / NB;
         p.b = p.tile / tpi;
         const int trem = p.tile % tpi;
         p.ty0 = (trem / a.tiles_x) * TH;
@@ -699,7 +699,7 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
             q.s = min(s, last);
             q.c = q.s % nchunk;
             q.itm = item0 + (q.s / nchunk) * nslots;
-            q.nb = q.itm % NB;
+            q.nb = a.order ? q.itm / a.ntiles : q.itm % NB;
             q.p = pos_of(q.itm);
             return q;
         };
@@ -709,7 +709,7 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
             if (++q.c == nchunk) {
                 q.c = 0;
                 q.itm += nslots;
-                q.nb = q.itm % NB;
+                q.nb = a.order ? q.itm / a.ntiles : q.itm % NB;
                 q.p = pos_of(q.itm);
             }
         };
@@ -1723,9 +1723,15 @@ int fwd_x6_stat_slots(int ntiles, int W, int np) {
 // 16-31 wide; 0 = conv3x3_fwd_x6_kernel everywhere
 int g_x6_probe = 0;  // "x6_probe": timing diagnostics (see ugpg_set_tuning)
 
+#ifndef X6R_ORDER_DEFAULT
+#define X6R_ORDER_DEFAULT 0
+#endif
+int g_x6_order = X6R_ORDER_DEFAULT;  // tuning knob "x6_order" (ConvFwdArgs::order)
+
 void launch_fwd_x6(const ConvFwdArgs& a_in, int np, hipStream_t st) {
     ConvFwdArgs a = a_in;
     a.probe = g_x6_probe;
+    a.order = g_x6_order;
     const int64_t items = (int64_t)a.ntiles * (a.Cout / 64);
     if (use_x6r(a.W, np)) {
         // persistent: one workgroup per CU (a multiple of 8: blockIdx % 8 = XCD), each
