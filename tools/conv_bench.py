@@ -54,7 +54,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--cfgs", default="-1", help="fp32 tile configs (-1 = heuristic)")
     ap.add_argument("--maths", default="x6,f32")
-    ap.add_argument("--pipes", default="2", help="x6 forward forms to time (x6_pipe knob)")
+    ap.add_argument("--pipes", default="4", help="x6 forward forms to time (x6_pipe knob)")
     ap.add_argument("--wgrad", action="store_true")
     ap.add_argument("--layers", default="", help="comma-separated layer names (default: all)")
     ap.add_argument("--libs", default="", help="comma-separated libugpg builds to compare")
@@ -129,7 +129,7 @@ def main():
                 except RuntimeError as e:
                     res[k].append(float("nan"))
         lib.ugpg_set_tuning(b"fwd_cfg", -1)
-        lib.ugpg_set_tuning(b"x6_pipe", 2)
+        lib.ugpg_set_tuning(b"x6_pipe", 4)
         ops.set_conv_math("x6")
         rows[name] = {k: (min(v), flops / (min(v) * 1e-3) / 1e12) for k, v in res.items()}
         print(name, " ".join(f"{k}={v[0]:.3f}ms/{v[1]:.0f}TF" for k, v in rows[name].items()),

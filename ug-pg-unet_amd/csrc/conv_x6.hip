@@ -455,12 +455,14 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
 // partials as x6_epilogue_wave (slot 2*tile + wm), reduced over the pixel lanes of
 // each DPP row.
 template <int TH, int TW, int NWM = 2>
-__device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a, f32x4 (&acc)[16 / NWM][2],
+__device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a,
+                                                  f32x4 (&acc)[TH * TW / 16 / NWM][2],
                                                   int tile, int b, int ty0, int tx0, int n0, int wm,
                                                   int wn) {
-    static_assert(TH * TW == 256 && (TW == 32 || TW == 16), "256-pixel tiles");
+    static_assert((TH * TW == 256 || TH * TW == 128) && (TW == 32 || TW == 16),
+                  "256- or 128-pixel tiles");
     constexpr int WR = TH / NWM;  // image rows of one wave (NWM pixel groups per tile)
-    constexpr int MTW = 16 / NWM;  // m-tiles of one wave
+    constexpr int MTW = TH * TW / 16 / NWM;  // m-tiles of one wave
     auto prow = [](int mt) { return TW == 32 ? mt >> 1 : mt; };
     auto pcol = [](int mt) { return TW == 32 ? (mt & 1) * 16 : 0; };
     const int lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
@@ -618,13 +620,17 @@ extern "C" int ugpg_debug_clock(double* mhz) {
 // NCW = compute waves: 4 (one per SIMD) or 8 (two per SIMD, 16x16x32 form only: while one
 // waits on an LDS read or a barrier the other issues MFMAs; each covers a quarter of the
 // item's pixels, so a tile has NCW/2 BatchNorm stat slots)
-template <int NP, bool M16, int TWT = 32, int NCW = 4>
+// THT: tile height; 256 / TWT (256-pixel items) by default, 8 with TWT = 16 for 128-pixel
+// items (8 x 16) on 16-wide images, whose 256-pixel items would leave half of the CUs idle
+// at bs16 (64 images' worth of 16 x 16 tiles x 8 column blocks = 128 items).
+template <int NP, bool M16, int TWT = 32, int NCW = 4, int THT = 256 / TWT>
 __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) {
     static_assert(!M16 || NP == 3, "the 16x16x32 form pairs the split-bf16 products");
     static_assert(TWT == 32 || (M16 && TWT == 16), "16-wide tiles only in the 16x16x32 form");
+    static_assert(THT * TWT == 256 || (M16 && THT * TWT == 128), "256- or 128-pixel items");
     static_assert(NCW == 4 || (NCW == 8 && M16), "two compute waves per SIMD: 16x16x32 form only");
     // 256-pixel items: 8 x 32 (images >= 32 wide) or 16 x 16 (16-31 wide, 16x16x32 form)
-    constexpr int TW = TWT, TH = 256 / TWT, BN = 64, BKC = 16, MT = 4;
+    constexpr int TW = TWT, TH = THT, BN = 64, BKC = 16, MT = 4;
     constexpr int HWD = TW + 2, HS = HWD;
     constexpr int NHALO = (TH + 2) * HWD;                   // 340 / 324 halo pixels
     // spare slot NHALO; plane pitch 348 = 4 (mod 8) for the 32x32 fragment pattern, 352
@@ -894,7 +900,8 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
         const int g = lane >> 4, l16 = lane & 15;
         // NWM pixel groups per tile: a wave covers TH/NWM image rows = MTW m-tiles of 16
         // pixels (row mt/2, columns 16(mt&1).. for 8 x 32 tiles; row mt for 16 x 16 tiles)
-        constexpr int NWM = NCW / 2, MTW = 16 / NWM, URT = MTW / 2, UPS = 9 * URT;
+        constexpr int NWM = NCW / 2, MTW = TH * TW / 16 / NWM, URT = MTW / 2, UPS = 9 * URT;
+        static_assert(URT >= 1, "a wave needs at least one m-tile pair");
         constexpr int WPU = (6 + URT - 1) / URT;  // next tap's W fragments read per unit
         const int a01 = g * NHP + wm * (TH / NWM) * HS + l16;
         const int a02 = ((g >> 1) * 4 + (g & 1)) * NHP + wm * (TH / NWM) * HS + l16;
@@ -908,7 +915,8 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
 #ifndef X6Q_DEPTH
 #define X6Q_DEPTH 1
 #endif
-        constexpr int DA = X6Q_DEPTH;  // A fragments are read DA units ahead
+        // A fragments are read DA units ahead (a ring of DA+1 must divide the step's units)
+        constexpr int DA = UPS % (X6Q_DEPTH + 1) == 0 ? X6Q_DEPTH : 2;
         static_assert(UPS % (DA + 1) == 0, "unit ring must divide a step");
         u32x4 fa[DA + 1][2][2];  // [unit % (DA+1)][m-tile of the pair][A02, A01]
         u32x4 fw[3][3][2];     // [tap % 3 (9 taps per step)][W20, W11, W00][nt]
@@ -1696,18 +1704,24 @@ __global__ void pack_x6_batch_kernel(PackBatch pb, int np) {
         pack_x6_elem(it.w, static_cast<__bf16*>(it.wpk), it.Cin, K, it.mode, np, e);
 }
 
-int g_x6_pipe = 2;   // tuning knob "x6_pipe" (see launch_fwd_x6)
+#ifndef X6_PIPE_DEFAULT
+#define X6_PIPE_DEFAULT 4
+#endif
+int g_x6_pipe = X6_PIPE_DEFAULT;   // tuning knob "x6_pipe" (see launch_fwd_x6)
 // persistent form for this image width / piece count: 8x32 items for W >= 32; with
 // x6_pipe = 3 also 16x16 items for 16 <= W < 32 (16x16x32 split-bf16 form only).  Not
 // the default: at bs16 the 16-wide layers have 64-128 such items for 256 CUs and the
 // single-stage kernel's 128-pixel tiles fill the chip better (0.120 vs 0.124 ms,
 // down4 of S4).
+// x6_pipe = 4: 8 x 16-pixel (128-pixel) items for 16 <= W < 32, so that bs16's 16-wide
+// layers have 256 items for 256 CUs.
 static bool use_x6r(int W, int np) {
-    return g_x6_pipe && (W >= 32 || (g_x6_pipe == 3 && np == 3 && W >= 16));
+    return g_x6_pipe && (W >= 32 || (g_x6_pipe >= 3 && np == 3 && W >= 16));
 }
 int fwd_x6_tile_w(int W, int np) { return W >= 32 ? 32 : 16; }
 int fwd_x6_tile_h(int W, int np) {
-    return use_x6r(W, np) ? (W >= 32 ? 8 : 16) : (W >= 32 ? 4 : 8);
+    if (use_x6r(W, np)) return W >= 32 ? 8 : (g_x6_pipe == 4 ? 8 : 16);
+    return W >= 32 ? 4 : 8;
 }
 #ifndef X6R_CW_DEFAULT
 #define X6R_CW_DEFAULT 4
@@ -1719,8 +1733,10 @@ int fwd_x6_stat_slots(int ntiles, int W, int np) {
 }
 
 // tuning knob "x6_pipe": conv3x3_fwd_x6r_kernel for images >= 32 wide with 16x16x32
-// tiles (2, default) or 32x32x16 tiles (1); 3 = as 2 plus 16x16-pixel items for images
-// 16-31 wide; 0 = conv3x3_fwd_x6_kernel everywhere
+// tiles (2) or 32x32x16 tiles (1); 3 = as 2 plus 16x16-pixel items for images 16-31
+// wide; 4 (default) = as 2 plus 8x16-pixel items for images 16-31 wide (bs16's 16-wide
+// layers: 256 items for 256 CUs, 152-166 -> 216-223 TF/s vs the single-stage kernel);
+// 0 = conv3x3_fwd_x6_kernel everywhere
 int g_x6_probe = 0;  // "x6_probe": timing diagnostics (see ugpg_set_tuning)
 
 #ifndef X6R_ORDER_DEFAULT
@@ -1739,7 +1755,13 @@ void launch_fwd_x6(const ConvFwdArgs& a_in, int np, hipStream_t st) {
         int64_t g = std::min<int64_t>(cu_count(st), (items + 7) / 8 * 8);
         g = std::max<int64_t>(8, g / 8 * 8);
         const bool cw8 = x6r_cw(np) == 8;
-        if (np == 3 && g_x6_pipe >= 2 && a.W < 32 && cw8)
+        if (np == 3 && g_x6_pipe == 4 && a.W < 32 && cw8)
+            hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<3, true, 16, 8, 8>), dim3((unsigned)g),
+                               dim3(768), 0, st, a);
+        else if (np == 3 && g_x6_pipe == 4 && a.W < 32)
+            hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<3, true, 16, 4, 8>), dim3((unsigned)g),
+                               dim3(512), 0, st, a);
+        else if (np == 3 && g_x6_pipe >= 2 && a.W < 32 && cw8)
             hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<3, true, 16, 8>), dim3((unsigned)g), dim3(768),
                                0, st, a);
         else if (np == 3 && g_x6_pipe >= 2 && a.W < 32)
