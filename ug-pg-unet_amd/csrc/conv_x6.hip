@@ -1291,8 +1291,13 @@ __global__ void __launch_bounds__(256, 2) conv3x3_wgrad_x6_kernel(WgradArgs a) {
 template <int NP>
 constexpr int wrec() { return NP == 3 ? WX_REC : 192; }
 
-template <int TH, int TW, int NP>
+// M16: the compute waves run v_mfma_f32_16x16x32_bf16 with the split-bf16 products paired
+// along k, as the forward's x6r form (3 MFMAs per 16 x 16 tile and tap instead of 6 half-
+// size products): k groups 0,1 of both operands carry the 16 pixels of one piece, groups
+// 2,3 of another, so dy01.x10 = a0b1 + a1b0, dy01.x01 = a0b0 + a1b1, dy02.x20 = a0b2 + a2b0.
+template <int TH, int TW, int NP, bool M16 = false>
 __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) {
+    static_assert(!M16 || NP == 3, "the paired 16x16x32 form needs the three pieces");
     constexpr int REC = wrec<NP>();
     static_assert(TW == 16, "one 16-pixel row per MFMA k-step");
     constexpr int P = TH * TW, HWD = TW + 2, NHALO = (TH + 2) * HWD;
@@ -1524,6 +1529,110 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
 
     // ---------------------------------------------------------------- compute waves
     const int wm = wave >> 1, wn = wave & 1;
+    if constexpr (M16) {
+        const int li = lane & 15, g = lane >> 4;
+        // transposed reads: 16-lane group g takes pixels 8(g&1) + (li>>2) (+4 for the
+        // second read), channels 4(li&3)..+3 of a 16-channel tile; lane li receives the
+        // 8 pixels of channel li = its row (co) or column (ci) of the 16 x 16 tile
+        const int pix_in = 8 * (g & 1) + (li >> 2);
+        const int s0 = g < 2 ? 0 : 1, s2 = g < 2 ? 0 : 2;  // piece of A01 / A02 (and B01)
+        const int s10 = g < 2 ? 1 : 0, s20 = g < 2 ? 2 : 0;  // piece of B10 / B20
+        f32x4 acc[9][2][2];
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt) acc[t][mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        Cur cc;
+        item_range(item0, cc);
+        lds_barrier();  // step 0 staged
+        for (int k = 0; k < total; ++k) {
+            const char* dys = smem + (k & 1) * RECS * REC;
+            const char* abase = dys + pix_in * REC + (wm * 32 + 4 * (li & 3)) * 2;
+            const char* bbase = dys + P * REC + pix_in * REC + (wn * 32 + 4 * (li & 3)) * 2;
+            auto trpair = [](const char* p) {
+                const u32x2 lo = ds_read_tr(p), hi = ds_read_tr(p + 4 * REC);
+                return u32x4{lo.x, lo.y, hi.x, hi.y};
+            };
+            auto lda = [&](int ks, u32x4 (&af)[2][2]) {  // [co tile][A01, A02]
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt) {
+                    const char* pa = abase + ks * TW * REC + 32 * mt;
+                    af[mt][0] = trpair(pa + s0 * 128);
+                    af[mt][1] = trpair(pa + s2 * 128);
+                }
+            };
+            auto ldb = [&](int ks, int t, u32x4 (&bf)[2][3]) {  // [ci tile][B10, B01, B20]
+                const char* pb = bbase + ((ks + t / 3) * HWD + (t % 3)) * REC;
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt) {
+                    const char* q = pb + 32 * nt;
+                    bf[nt][0] = trpair(q + s10 * 128);
+                    bf[nt][1] = trpair(q + s0 * 128);
+                    bf[nt][2] = trpair(q + s20 * 128);
+                }
+            };
+            u32x4 afr[2][2][2], bfr[2][2][3];
+            lda(0, afr[0]);
+            ldb(0, 0, bfr[0]);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < 9 * TH; ++u) {
+                const int ks = u / 9, t = u % 9;
+                const bool more = u + 1 < 9 * TH, row = (u + 1) % 9 == 0;
+                if (more) {
+                    if (row) lda((u + 1) / 9, afr[((u + 1) / 9) & 1]);
+                    ldb((u + 1) / 9, (u + 1) % 9, bfr[(u + 1) & 1]);
+                }
+                const u32x4(&A)[2][2] = afr[ks & 1];
+                const u32x4(&B)[2][3] = bfr[u & 1];
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                    for (int nt = 0; nt < 2; ++nt) {
+                        f32x4 c = acc[t][mt][nt];
+                        c = mfma16x16(A[mt][0], B[nt][0], c);  // a0b1 + a1b0
+                        c = mfma16x16(A[mt][0], B[nt][1], c);  // a0b0 + a1b1
+                        c = mfma16x16(A[mt][1], B[nt][2], c);  // a0b2 + a2b0
+                        acc[t][mt][nt] = c;
+                    }
+                // the next tap's 12 reads (20 at a row change) between the 12 MFMAs
+#pragma unroll
+                for (int i = 0; i < 12; ++i) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    if (more) {
+                        if (row && i < 8) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                        else __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            read_barrier();
+            const bool item_end = cc.tile + 1 >= cc.tend;
+            if (item_end) {
+                const int nb = cc.item % NCO, rest = cc.item / NCO;
+                const int cb = rest % NCI, split = rest / NCI;
+#pragma unroll
+                for (int t = 0; t < 9; ++t)
+#pragma unroll
+                    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                        for (int nt = 0; nt < 2; ++nt) {
+                            const int ci = cb * 64 + wn * 32 + 16 * nt + li;
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) {
+                                const int co = nb * 64 + wm * 32 + 16 * mt + 4 * g + i;
+                                a.part[((size_t)(split * 9 + t) * a.Cout + co) * a.Cin + ci] =
+                                    acc[t][mt][nt][i];
+                            }
+                            acc[t][mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+                        }
+            }
+            advance(cc);
+        }
+        return;
+    }
     f32x16 acc[9];
 #pragma unroll
     for (int t = 0; t < 9; ++t)
@@ -1626,14 +1735,18 @@ void wgrad_x6w_plan(int ntiles, int Cout, int Cin, int cus, int& nsplit, int& tp
     nsplit = (int)cdiv(ntiles, tps);
 }
 
-int g_x6_wgrad = 1;  // tuning knob "x6_wgrad": 1 = persistent x6w kernel, 0 = one block per item
+int g_x6_wgrad = 1;  // tuning knob "x6_wgrad": 1 = persistent x6w kernel (32x32x16), 2 = its
+                     // paired 16x16x32 form, 0 = one block per item
 
 void launch_wgrad_x6(const WgradArgs& a, unsigned grid, int np, hipStream_t st) {
     if (g_x6_wgrad || np == 1) {  // (the per-item kernel has no single-piece form)
         const int64_t items = (int64_t)(a.Cout / 64) * (a.Cin / 64) * a.nsplit;
         int64_t g = std::min<int64_t>(cu_count(st), (items + 7) / 8 * 8);
         g = std::max<int64_t>(8, g / 8 * 8);
-        if (np == 3)
+        if (np == 3 && g_x6_wgrad == 2)
+            hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW, 3, true>), dim3((unsigned)g),
+                               dim3(512), 0, st, a);
+        else if (np == 3)
             hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW, 3>), dim3((unsigned)g), dim3(512), 0, st, a);
         else
             hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW, 1>), dim3((unsigned)g), dim3(512), 0, st, a);
