@@ -65,19 +65,22 @@ CONV_CASES = [
     (2, 20, 24, 64, 0, 64, True),      # 16x16-item persistent form: ragged rows and columns
     (1, 18, 17, 128, 64, 128, True),   # same, concat input, 2 partial tiles per side
     (1, 16, 16, 512, 512, 512, True),  # Up-shaped 16-wide concat: 4-way split-K forward/dgrad
+    (2, 45, 70, 8, 0, 64, False),      # image layer, ragged 8 x 32 tiles (direct fp32 kernel)
+    (3, 16, 40, 512, 0, 64, True),     # 16-high, 40-wide: 8 x 32 items, ragged columns
 ]
 BIG = {5, 6, 7}
 
 
 # x6 kernel forms: (x6_pipe, x6_wgrad) tuning knobs.  Default = persistent
-# warp-specialized forward/dgrad with 16x16x32 MFMA tiles and persistent wgrad; "x6w"
-# the forward/dgrad form with 32x32x16 tiles; "x6t" adds 16x16-pixel items for images
-# 16-31 wide; "x6s" one workgroup per tile/item.
-X6_FORMS = {"x6": (2, 1), "x6w": (1, 1), "x6t": (3, 1), "x6s": (0, 0)}
+# warp-specialized forward/dgrad with 16x16x32 MFMA tiles (8 x 16-pixel items for images
+# 16-31 wide) and persistent wgrad; "x6q" the same without the 16-wide items; "x6w" the
+# forward/dgrad form with 32x32x16 tiles; "x6t" 16x16-pixel items for images 16-31 wide;
+# "x6p" the paired 16x16x32 weight gradient; "x6s" one workgroup per tile/item.
+X6_FORMS = {"x6": (4, 1), "x6q": (2, 1), "x6w": (1, 1), "x6t": (3, 1), "x6p": (4, 2), "x6s": (0, 0)}
 X6_DEFAULT = X6_FORMS["x6"]
 
 
-@pytest.fixture(params=["x6", "x6w", "x6t", "x6s", "f32", "bf16"])
+@pytest.fixture(params=["x6", "x6q", "x6w", "x6t", "x6p", "x6s", "f32", "bf16"])
 def math(request):
     """Every conv arithmetic form: split-bf16 (default, every kernel form), fp32
     MFMA, and bf16 (BASELINE config 3: operands rounded to bf16, fp32 accumulation)."""

@@ -57,6 +57,7 @@ def main():
     ap.add_argument("--pipes", default="4", help="x6 forward forms to time (x6_pipe knob)")
     ap.add_argument("--wgrad", action="store_true")
     ap.add_argument("--layers", default="", help="comma-separated layer names (default: all)")
+    ap.add_argument("--nostats", action="store_true", help="forward without BatchNorm partials")
     ap.add_argument("--libs", default="", help="comma-separated libugpg builds to compare")
     a = ap.parse_args()
     libs = [(Path(p).stem, load_lib(p)) for p in a.libs.split(",")] if a.libs else [("", None)]
@@ -69,8 +70,11 @@ def main():
             continue
         cin = C0 + C1
         real_cin = 3 if cin == 8 else cin
-        srcs = [ops.Act(torch.randn(B, H, H, C0, device=dev),
-                        torch.rand(C0, device=dev) + 0.5, torch.randn(C0, device=dev) * 0.1)]
+        if cin == 8:  # the image layer reads the raw (channel-padded) image
+            srcs = [ops.Act(torch.randn(B, H, H, C0, device=dev))]
+        else:
+            srcs = [ops.Act(torch.randn(B, H, H, C0, device=dev),
+                            torch.rand(C0, device=dev) + 0.5, torch.randn(C0, device=dev) * 0.1)]
         if C1:
             srcs.append(ops.Act(torch.randn(B, H, H, C1, device=dev)))
         w = torch.randn(Cout, real_cin, 3, 3, device=dev) * 0.05
@@ -80,7 +84,7 @@ def main():
         fns = {}
         for m in a.maths.split(","):
             ops.set_conv_math(m)
-            wpk = ops.pack_conv3x3(w, cin, 0)
+            wpk = ops.pack_conv3x3(w, ops.conv_pack_k(cin), 0)
             wpk1 = ops.pack_conv3x3(w, real_cin, 1) if real_cin % 64 == 0 else None
             nt = ops.conv_ntiles(B, H, H, cin, Cout, wpk)
             st = torch.empty(3 * Cout * nt, device=dev)
@@ -92,7 +96,7 @@ def main():
                 def f(c=c, wpk=wpk, st=st, pipe=pipe):
                     lib.ugpg_set_tuning(b"fwd_cfg", c)
                     lib.ugpg_set_tuning(b"x6_pipe", pipe)
-                    ops.conv3x3_fwd(srcs, wpk, bias, Cout, [out], stats=st)
+                    ops.conv3x3_fwd(srcs, wpk, bias, Cout, [out], stats=None if a.nostats else st)
                 fns[f"fwd_{tag}"] = f
                 if wpk1 is not None:
                     dy = torch.randn(B, H, H, Cout, device=dev)

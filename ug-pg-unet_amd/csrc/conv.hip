@@ -612,7 +612,7 @@ void launch_fwd(const ConvFwdArgs& a, hipStream_t st) {
 using namespace ugpg;
 
 namespace ugpg {
-extern int g_bn_bwd_blocks, g_bn_bwd_ppt, g_x6_cw, g_x6_order;
+extern int g_bn_bwd_blocks, g_bn_bwd_ppt, g_x6_cw, g_x6_order, g_x6_img;
 }
 
 extern "C" int ugpg_set_tuning(const char* key, int value) {
@@ -626,6 +626,10 @@ extern "C" int ugpg_set_tuning(const char* key, int value) {
     }
     if (key && std::string(key) == "x6_wgrad") {
         g_x6_wgrad = value;
+        return UGPG_OK;
+    }
+    if (key && std::string(key) == "x6_img" && (value == 0 || value == 1)) {
+        g_x6_img = value;
         return UGPG_OK;
     }
     if (key && std::string(key) == "x6_order" && (value == 0 || value == 1)) {

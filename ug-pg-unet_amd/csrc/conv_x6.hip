@@ -1852,16 +1852,245 @@ int fwd_x6_stat_slots(int ntiles, int W, int np) {
 // 0 = conv3x3_fwd_x6_kernel everywhere
 int g_x6_probe = 0;  // "x6_probe": timing diagnostics (see ugpg_set_tuning)
 
+// ---------------------------------------------------------------------------
+// Image layer (inc.conv_op.0: a 3-channel image zero-extended to 8 channels, one
+// 16-channel K chunk, 64 outputs) as a direct fp32-FMA convolution.  Through x6r each
+// 256-pixel item is a single K chunk, so its pipeline prologue and epilogue dominate
+// (113-128 us at bs16 x 256^2 against 38 us of output stores).  The layer is bound by
+// store issue, so the mapping is chosen for the stores: 16 lanes hold one pixel's 64
+// channels (4 each), a wave's four 16-lane groups are four 16-pixel row segments, and
+// every store instruction writes four whole 256-B pixels.  A persistent workgroup
+// rebuilds the fp32 weights once from the split-bf16 pack (p0 + p1 + p2 == w exactly)
+// and finds the highest input channel with a nonzero weight (the zero padding is
+// skipped), then walks 8 x 32-pixel tiles, fetching the next tile's halo into
+// registers while the current one computes; the halo sits channel-planar in LDS so a
+// segment's 18 inputs are 4 ds_read_b128 + 1 ds_read_b64, reused over the 3 kx taps.
+// Products and sums in fp32 (the fp32-MFMA path's arithmetic class), as packed pairs.
+// Epilogue: bias, store, BatchNorm partials (count, sum, M2 about the slot mean) in
+// x6r's slot layout (NWM row groups per tile).
+template <int NWM, int PX>
+__global__ void __launch_bounds__(4096 / PX) conv3x3_img_fwd_kernel(ConvFwdArgs a) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    // PX pixels per thread: 16 lanes x (TW / PX) segments per tile row
+    constexpr int NT = 4096 / PX, NWV = NT / 64, RPW = 4 * PX / 32;  // rows per wave
+    constexpr int TH = 8, TW = 32, HWP = 36, HROWS = TH + 2, CIN = 8;
+    constexpr int NH = HROWS * (TW + 2) * 2;     // halo f32x4 pieces (2 per pixel)
+    constexpr int HPT = (NH + NT - 1) / NT;      // per thread
+    __shared__ float wsm[9 * CIN][64];           // [tap * 8 + ci][co]
+    __shared__ float xs[2][CIN][HROWS * HWP];    // channel-planar halo, double-buffered
+    __shared__ float wred[2][NWV][64];           // per-wave channel sums / M2 partials
+    __shared__ int nci_s;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tpi = a.tiles_x * a.tiles_y;
+    auto halo_fetch = [&](int tile, f32x4* r) {
+        const int b = tile / tpi, trem = tile % tpi;
+        const int ty0 = (trem / a.tiles_x) * TH, tx0 = (trem % a.tiles_x) * TW;
+#pragma unroll
+        for (int k = 0; k < HPT; ++k) {
+            const int e = tid + NT * k, hp = e >> 1, q = e & 1;
+            const int gy = ty0 - 1 + hp / (TW + 2), gx = tx0 - 1 + hp % (TW + 2);
+            r[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (e < NH && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W)
+                r[k] = *reinterpret_cast<const f32x4*>(
+                    a.src0 + ((size_t)(b * a.H + gy) * a.W + gx) * CIN + 4 * q);
+        }
+    };
+    auto halo_put = [&](int buf, const f32x4* r) {
+#pragma unroll
+        for (int k = 0; k < HPT; ++k) {
+            const int e = tid + NT * k, hp = e >> 1, q = e & 1;
+            const int o = (hp / (TW + 2)) * HWP + hp % (TW + 2);
+            if (e < NH)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) xs[buf][4 * q + i][o] = r[k][i];
+        }
+    };
+    if (blockIdx.x >= a.ntiles) return;
+    f32x4 hr[HPT];
+    halo_fetch(blockIdx.x, hr);
+    // weights: pack layout of pack_x6_elem (mode 0, K = 16, nb = 0)
+    const __bf16* wp = static_cast<const __bf16*>(a.wpk);
+    constexpr int plane = 3 * 64 * 8;
+    if (tid == 0) nci_s = 0;
+    __syncthreads();
+    int hi = 0;
+    {
+        // all 3 x 9 * 512 / NT loads issued before the first is used (one round trip)
+        constexpr int NE = 9 * CIN * 64 / NT;
+        __bf16 pc[NE][3];
+#pragma unroll
+        for (int k = 0; k < NE; ++k) {
+            const int e = tid + NT * k, ci = e & 7, co = (e >> 3) & 63, t = e >> 9;
+            const size_t base = (size_t)(t / 3) * 6 * plane + ((size_t)(t % 3) * 64 + co) * 8 + ci;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) pc[k][q] = wp[base + 2 * q * plane];
+        }
+#pragma unroll
+        for (int k = 0; k < NE; ++k) {
+            const int e = tid + NT * k, ci = e & 7, co = (e >> 3) & 63, t = e >> 9;
+            const float v = ((float)pc[k][0] + (float)pc[k][1]) + (float)pc[k][2];
+            wsm[t * CIN + ci][co] = v;
+            if (v != 0.f) hi = max(hi, ci + 1);
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) hi = max(hi, __shfl_xor(hi, o, 64));
+    if (lane == 0) atomicMax(&nci_s, hi);
+    halo_put(0, hr);
+    __syncthreads();
+    const int nci = nci_s;
+    // thread: channels 4*cq..+3 of the PX-pixel row segment (row, c0..c0+PX-1)
+    constexpr int SPR = TW / PX;  // segments per row
+    const int cq = lane & 15, seg = tid >> 4, row = seg / SPR, c0 = (seg % SPR) * PX;
+    constexpr int RPS = TH / NWM;  // rows per BN slot
+    constexpr int WPS = RPS / RPW; // waves per BN slot
+    int buf = 0;
+    for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x, buf ^= 1) {
+        const int nxt = tile + gridDim.x;
+        if (nxt < a.ntiles) halo_fetch(nxt, hr);
+        const int b = tile / tpi, trem = tile % tpi;
+        const int ty0 = (trem / a.tiles_x) * TH, tx0 = (trem % a.tiles_x) * TW;
+        f2 acc[PX][2];
+#pragma unroll
+        for (int p = 0; p < PX; ++p) acc[p][0] = acc[p][1] = f2{0.f, 0.f};
+        for (int ky = 0; ky < 3; ++ky) {
+            for (int ci = 0; ci < nci; ++ci) {
+                const float* xr = &xs[buf][ci][(row + ky) * HWP + c0];
+                float x[PX + 2];
+#pragma unroll
+                for (int k = 0; k < PX / 4; ++k) {
+                    const f32x4 v = *reinterpret_cast<const f32x4*>(xr + 4 * k);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) x[4 * k + i] = v[i];
+                }
+                {
+                    const f2 v = *reinterpret_cast<const f2*>(xr + PX);
+                    x[PX] = v.x;
+                    x[PX + 1] = v.y;
+                }
+#pragma unroll
+                for (int kx = 0; kx < 3; ++kx) {
+                    const f32x4 wv = *reinterpret_cast<const f32x4*>(&wsm[(3 * ky + kx) * CIN + ci][4 * cq]);
+                    const f2 w01 = f2{wv[0], wv[1]}, w23 = f2{wv[2], wv[3]};
+#pragma unroll
+                    for (int p = 0; p < PX; ++p) {
+                        const f2 xv = f2{x[p + kx], x[p + kx]};
+                        acc[p][0] = __builtin_elementwise_fma(xv, w01, acc[p][0]);
+                        acc[p][1] = __builtin_elementwise_fma(xv, w23, acc[p][1]);
+                    }
+                }
+            }
+        }
+        // bias, store (16 lanes = one whole pixel), per-thread sums over valid pixels
+        const int vh = min(TH, a.H - ty0), vw = min(TW, a.W - tx0);
+        const bool rok = row < vh;
+        f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+        if (a.bias)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) bv[i] = a.bias[4 * cq + i];
+        float* orow = a.out0 + ((size_t)(b * a.H + ty0 + row) * a.W + tx0 + c0) * 64 + 4 * cq;
+        float sj[4] = {0.f, 0.f, 0.f, 0.f};
+        float v[PX][4];
+#pragma unroll
+        for (int p = 0; p < PX; ++p) {
+            v[p][0] = acc[p][0].x + bv[0];
+            v[p][1] = acc[p][0].y + bv[1];
+            v[p][2] = acc[p][1].x + bv[2];
+            v[p][3] = acc[p][1].y + bv[3];
+            if (rok && c0 + p < vw) {
+#ifndef IMG_NOSTORE
+                *reinterpret_cast<f32x4*>(orow + (size_t)p * 64) = f32x4{v[p][0], v[p][1], v[p][2], v[p][3]};
+#endif
+#pragma unroll
+                for (int i = 0; i < 4; ++i) sj[i] += v[p][i];
+            }
+        }
+        if (nxt < a.ntiles) halo_put(buf ^ 1, hr);
+        if (a.stats != nullptr) {
+            // BatchNorm partials per (channel, slot): slot = NWM * tile + row group.
+            // wave sums: the 4 segments holding the same channels (lane bits 4, 5)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                sj[i] += __shfl_xor(sj[i], 16, 64);
+                sj[i] += __shfl_xor(sj[i], 32, 64);
+            }
+            if (lane < 16)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) wred[0][wave][4 * cq + i] = sj[i];
+            __syncthreads();
+            const int sl = row / RPS, w0 = sl * WPS;
+            const int rows = min(max(vh - sl * RPS, 0), RPS);
+            const float cnt = (float)(rows * vw);
+            float qj[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float s = 0.f;
+#pragma unroll
+                for (int k = 0; k < WPS; ++k) s += wred[0][w0 + k][4 * cq + i];
+                const float mu = cnt > 0.f ? s / cnt : 0.f;
+                float q = 0.f;
+#pragma unroll
+                for (int p = 0; p < PX; ++p) {
+                    const float d = v[p][i] - mu;
+                    if (rok && c0 + p < vw) q = fmaf(d, d, q);
+                }
+                q += __shfl_xor(q, 16, 64);
+                q += __shfl_xor(q, 32, 64);
+                qj[i] = q;
+            }
+            if (lane < 16)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) wred[1][wave][4 * cq + i] = qj[i];
+            __syncthreads();
+            if (tid < 64 * NWM) {
+                const int c = tid & 63, s2 = tid >> 6;
+                float sum = 0.f, m2 = 0.f;
+                for (int k = 0; k < WPS; ++k) {
+                    sum += wred[0][s2 * WPS + k][c];
+                    m2 += wred[1][s2 * WPS + k][c];
+                }
+                const int rows2 = min(max(vh - s2 * RPS, 0), RPS);
+                const size_t S = (size_t)NWM * a.ntiles, slot = (size_t)NWM * tile + s2;
+                a.stats[(0 * (size_t)a.Cout + c) * S + slot] = (float)(rows2 * vw);
+                a.stats[(1 * (size_t)a.Cout + c) * S + slot] = sum;
+                a.stats[(2 * (size_t)a.Cout + c) * S + slot] = m2;
+            }
+        }
+        __syncthreads();  // halo buffer swap; wred reuse
+    }
+}
+
 #ifndef X6R_ORDER_DEFAULT
 #define X6R_ORDER_DEFAULT 0
 #endif
 int g_x6_order = X6R_ORDER_DEFAULT;  // tuning knob "x6_order" (ConvFwdArgs::order)
+#ifndef X6_IMG_DEFAULT
+#define X6_IMG_DEFAULT 1
+#endif
+int g_x6_img = X6_IMG_DEFAULT;
+#ifndef IMG_PX
+#define IMG_PX 8
+#endif
+#ifndef IMG_BPC
+#define IMG_BPC 2
+#endif  // tuning knob "x6_img": direct fp32 kernel for the image layer
 
 void launch_fwd_x6(const ConvFwdArgs& a_in, int np, hipStream_t st) {
     ConvFwdArgs a = a_in;
     a.probe = g_x6_probe;
     a.order = g_x6_order;
     const int64_t items = (int64_t)a.ntiles * (a.Cout / 64);
+    if (np == 3 && use_x6r(a.W, np) && a.W >= 32 && a.C0 == 8 && a.C1 == 0 && a.Cin == 16 &&
+        a.Cout == 64 && a.sc0 == nullptr && a.split == a.Cout && !a.acc0 && g_x6_img) {
+        // persistent: IMG_BPC workgroups per CU
+        int64_t g = std::min<int64_t>(IMG_BPC * (int64_t)cu_count(st), (int64_t)a.ntiles);
+        g = std::max<int64_t>(1, g);
+        constexpr int PX = IMG_PX;
+        if (x6r_cw(np) == 8)
+            hipLaunchKernelGGL((conv3x3_img_fwd_kernel<4, PX>), dim3((unsigned)g), dim3(4096 / PX), 0, st, a);
+        else
+            hipLaunchKernelGGL((conv3x3_img_fwd_kernel<2, PX>), dim3((unsigned)g), dim3(4096 / PX), 0, st, a);
+        return;
+    }
     if (use_x6r(a.W, np)) {
         // persistent: one workgroup per CU (a multiple of 8: blockIdx % 8 = XCD), each
         // walking a strided share of its XCD's contiguous item range
