@@ -436,6 +436,146 @@ __global__ void __launch_bounds__(192) conv3x3_wgrad_c8_kernel(WgradArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Image-layer weight gradient (inc.conv_op.0: the 3 real channels of the 8-channel
+// padded image, no input activation, 64 outputs) on the fp32 VALU.  The GEMM is
+// 64 x 27 x (B*H*W): through v_mfma_f32_32x32x2_f32 (conv3x3_wgrad_c8_kernel) it pads N
+// 27 -> 96 and runs at the f32 MFMA rate, 219 us at bs16 x 256^2 for 301 MB of reads.
+// Here a thread owns 2 output channels x all 27 (tap, ci) columns (54 accumulators)
+// over an 8-pixel row segment: its dy (8 x float2; 32 lanes = one pixel's 64 channels,
+// so loads are whole 256-B rows) times a sliding 10-value input row from a
+// channel-planar LDS halo.  A persistent grid of WGI_GRID workgroups (8 waves) walks
+// 4 x 32 tiles, prefetching the next tile's dy and halo into registers while the
+// current one computes (about 100 VGPRs: 4 waves per SIMD); each workgroup then reduces
+// its 16 segments (a lane shuffle, then a fixed 8 -> 4 -> 2 -> 1 wave tree in LDS) and
+// writes one split-K partial slab (ci 3..7 as zeros) for wgrad_reduce_kernel.  The grid
+// is a fixed count, so the summation order is device-independent.
+// ---------------------------------------------------------------------------
+constexpr int WGI_TH = 2, WGI_TW = 32, WGI_PX = 8, WGI_GRID = 1024, WGI_NCI = 3;
+
+__global__ void __launch_bounds__(256)
+conv3x3_wgrad_img_kernel(WgradArgs a) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    constexpr int TH = WGI_TH, TW = WGI_TW, PX = WGI_PX, NCI = WGI_NCI, CIN = 8, NT = 256;
+    constexpr int HWP = TW + 4, HROWS = TH + 2, NH = HROWS * (TW + 2);
+    constexpr int NACC = 2 * 9 * NCI;  // [c][ky][kx][ci]
+    static_assert(NH <= NT, "one halo pixel per thread");
+    __shared__ __attribute__((aligned(16))) float xs[2][NCI][HROWS * HWP];
+    __shared__ float red[2][NACC][32];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tpi = a.tiles_x * a.tiles_y;
+    // halo: one 4-channel piece (channels 0..3) per pixel, held channel-planar
+    auto halo_fetch = [&](int tile) -> f32x4 {
+        const int b = tile / tpi, trem = tile % tpi;
+        const int ty0 = (trem / a.tiles_x) * TH, tx0 = (trem % a.tiles_x) * TW;
+        const int gy = ty0 - 1 + tid / (TW + 2), gx = tx0 - 1 + tid % (TW + 2);
+        f32x4 r = {0.f, 0.f, 0.f, 0.f};
+        if (tile < a.ntiles && tid < NH && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W)
+            r = *reinterpret_cast<const f32x4*>(a.src0 + ((size_t)(b * a.H + gy) * a.W + gx) * CIN);
+        return r;
+    };
+    auto halo_put = [&](int buf, f32x4 r) {
+        if (tid < NH) {
+            const int o = (tid / (TW + 2)) * HWP + tid % (TW + 2);
+#pragma unroll
+            for (int c = 0; c < NCI; ++c) xs[buf][c][o] = r[c];
+        }
+    };
+    // thread: channels 2*cp, 2*cp+1 of the 8-pixel segment (row, c0..c0+7)
+    const int cp = lane & 31, seg = tid >> 5, row = seg / (TW / PX), c0 = (seg % (TW / PX)) * PX;
+    auto dy_fetch = [&](int tile, f2* d) {
+        const int b = tile / tpi, trem = tile % tpi;
+        const int gy = (trem / a.tiles_x) * TH + row, gx0 = (trem % a.tiles_x) * TW + c0;
+        const float* dyp = a.dy + ((size_t)(b * a.H + gy) * a.W + gx0) * 64 + 2 * cp;
+#pragma unroll
+        for (int p = 0; p < PX; ++p) {
+            d[p] = f2{0.f, 0.f};
+            if (tile < a.ntiles && gy < a.H && gx0 + p < a.W)
+                d[p] = *reinterpret_cast<const f2*>(dyp + (size_t)p * 64);
+        }
+    };
+    float acc[NACC];
+#pragma unroll
+    for (int i = 0; i < NACC; ++i) acc[i] = 0.f;
+    f2 d[PX];
+    int buf = 0;
+    if ((int)blockIdx.x < a.ntiles) {
+        halo_put(0, halo_fetch(blockIdx.x));
+        dy_fetch(blockIdx.x, d);
+    }
+    __syncthreads();
+    for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x, buf ^= 1) {
+        // next tile (zeros past the end: no branch for the compiler to sink the FMAs past)
+        const int nxt = tile + gridDim.x;
+        const f32x4 hn = halo_fetch(nxt);
+        f2 dn[PX];
+        dy_fetch(nxt, dn);
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+            for (int ci = 0; ci < NCI; ++ci) {
+                const float* xr = &xs[buf][ci][(row + ky) * HWP + c0];
+                float x[PX + 2];
+#pragma unroll
+                for (int k = 0; k < PX / 4; ++k) {
+                    const f32x4 v = *reinterpret_cast<const f32x4*>(xr + 4 * k);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) x[4 * k + i] = v[i];
+                }
+                const f2 xt = *reinterpret_cast<const f2*>(xr + PX);
+                x[PX] = xt.x;
+                x[PX + 1] = xt.y;
+#pragma unroll
+                for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+                    for (int p = 0; p < PX; ++p)
+#pragma unroll
+                        for (int c = 0; c < 2; ++c) {
+                            float& r = acc[((c * 3 + ky) * 3 + kx) * NCI + ci];
+                            r = fmaf(d[p][c], x[p + kx], r);
+                        }
+                // pin this row's products here: otherwise they are sunk below the halo store
+                // and all 9 input rows are live at once (registers, hence occupancy)
+#pragma unroll
+                for (int c = 0; c < 2; ++c)
+#pragma unroll
+                    for (int kx = 0; kx < 3; ++kx) asm volatile("" : "+v"(acc[((c * 3 + ky) * 3 + kx) * NCI + ci]));
+            }
+        halo_put(buf ^ 1, hn);
+#pragma unroll
+        for (int p = 0; p < PX; ++p) d[p] = dn[p];
+        __syncthreads();
+    }
+    // the 2 segments of a wave that share cp (lane bit 5), then waves 4 -> 2 -> 1
+#pragma unroll
+    for (int i = 0; i < NACC; ++i) acc[i] += __shfl_xor(acc[i], 32, 64);
+#pragma unroll
+    for (int half = 2; half >= 1; half >>= 1) {
+        if (wave >= half && wave < 2 * half && lane < 32)
+#pragma unroll
+            for (int i = 0; i < NACC; ++i) red[wave - half][i][cp] = acc[i];
+        __syncthreads();
+        if (wave < half && lane < 32)
+#pragma unroll
+            for (int i = 0; i < NACC; ++i) acc[i] += red[wave][i][cp];
+        __syncthreads();
+    }
+    if (wave != 0 || lane >= 32) return;
+    float* part = a.part + (size_t)blockIdx.x * 9 * 64 * CIN;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            float v[CIN];
+#pragma unroll
+            for (int ci = 0; ci < CIN; ++ci)
+                v[ci] = ci < NCI ? acc[((c * 3 + t / 3) * 3 + t % 3) * NCI + ci] : 0.f;
+            f32x4* o = reinterpret_cast<f32x4*>(part + ((size_t)t * 64 + 2 * cp + c) * CIN);
+            o[0] = f32x4{v[0], v[1], v[2], v[3]};
+            o[1] = f32x4{v[4], v[5], v[6], v[7]};
+        }
+}
+
 // Fixed-order split-K reduction over the flat [9][Cout][Cin] partial slabs.
 // Block = 64 consecutive slab elements (16 lanes x float4) x 16 split-groups;
 // thread (g, l) sums splits g, g+16, ... in order, then a fixed 16-way LDS tree
@@ -615,6 +755,11 @@ namespace ugpg {
 extern int g_bn_bwd_blocks, g_bn_bwd_ppt, g_x6_cw, g_x6_order, g_x6_img;
 }
 
+#ifndef WG_IMG_DEFAULT
+#define WG_IMG_DEFAULT 1
+#endif
+static int g_wg_img = WG_IMG_DEFAULT;  // tuning knob "wg_img": conv3x3_wgrad_img_kernel
+
 extern "C" int ugpg_set_tuning(const char* key, int value) {
     if (key && std::string(key) == "fwd_cfg") {
         g_force_fwd_cfg = value;
@@ -626,6 +771,10 @@ extern "C" int ugpg_set_tuning(const char* key, int value) {
     }
     if (key && std::string(key) == "x6_wgrad") {
         g_x6_wgrad = value;
+        return UGPG_OK;
+    }
+    if (key && std::string(key) == "wg_img" && (value == 0 || value == 1)) {
+        g_wg_img = value;
         return UGPG_OK;
     }
     if (key && std::string(key) == "x6_img" && (value == 0 || value == 1)) {
@@ -821,9 +970,12 @@ static int wgrad_check(const ugpg_wgrad_t* p) {
     return UGPG_OK;
 }
 
-enum WgradKind { WG_GENERIC, WG_C8, WG_X6 };
+enum WgradKind { WG_GENERIC, WG_C8, WG_X6, WG_IMG };
 
 static WgradKind wgrad_kind(const ugpg_wgrad_t* p, int C0, int C1) {
+    if (g_wg_img && C1 == 0 && C0 == 8 && !p->db && !p->src[0].scale && p->Cout == 64 &&
+        p->Cin_real > 0 && p->Cin_real <= WGI_NCI)
+        return WG_IMG;
     if (wgrad_use_c8(C0, C1, p->db)) return WG_C8;
     if ((p->math == UGPG_WFMT_X6 || p->math == UGPG_WFMT_BF16) && !p->db && C0 % 64 == 0 &&
         C1 % 64 == 0)
@@ -833,6 +985,15 @@ static WgradKind wgrad_kind(const ugpg_wgrad_t* p, int C0, int C1) {
 
 static WgradPlan wgrad_plan_for(const ugpg_wgrad_t* p, WgradKind k, int Cin) {
     if (k == WG_C8) return wgrad_plan_c8(p->B, p->H, p->W, p->Cout);
+    if (k == WG_IMG) {
+        WgradPlan w;
+        w.tiles_x = (int)cdiv(p->W, WGI_TW);
+        w.tiles_y = (int)cdiv(p->H, WGI_TH);
+        w.ntiles = p->B * w.tiles_x * w.tiles_y;
+        w.nsplit = std::min(w.ntiles, WGI_GRID);  // one partial slab per workgroup
+        w.tps = (int)cdiv(w.ntiles, w.nsplit);
+        return w;
+    }
     if (k == WG_X6) {
         // bf16 (1 piece) always runs the persistent kernel
         const bool persist = g_x6_wgrad || p->math == UGPG_WFMT_BF16;
@@ -892,6 +1053,8 @@ extern "C" int ugpg_conv3x3_wgrad(const ugpg_wgrad_t* p, void* ws, size_t ws_byt
     if (kind == WG_X6) {
         launch_wgrad_x6(a, (unsigned)((p->Cout / 64) * (Cin / 64) * w.nsplit),
                         p->math == UGPG_WFMT_BF16 ? 1 : 3, st);
+    } else if (kind == WG_IMG) {
+        hipLaunchKernelGGL(conv3x3_wgrad_img_kernel, dim3((unsigned)w.nsplit), dim3(256), 0, st, a);
     } else if (kind == WG_C8) {
         const unsigned grid = (unsigned)((p->Cout / 64) * w.nsplit);
         hipLaunchKernelGGL((conv3x3_wgrad_c8_kernel<WG8_TH, WG8_TW>), dim3(grid), dim3(192), 0, st,
