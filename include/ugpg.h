@@ -89,6 +89,20 @@ typedef struct {
     int accumulate[2];
     float* stats;
     int wfmt;              /* UGPG_WFMT_F32, UGPG_WFMT_X6 or UGPG_WFMT_BF16 */
+    /* Optional BatchNorm-backward partials of the output, for a data gradient whose
+     * output da = dL/d(relu(bn(y))) feeds ugpg_bn_relu_bwd_partials (the reduction half
+     * of ugpg_bn_relu_bwd, done while the output tile is in registers): when bnb_part
+     * != NULL (one output, no accumulate, Cout % 4 == 0) the call also writes
+     * bnb_part[3][Cout][slots] = per-slot (sum g, sum g*xhat, sum xhat) with
+     * g = da*[scale*y+shift > 0], xhat = (y-mean)*invstd, y = bnb_y (NHWC, Cout
+     * channels), slots = ugpg_conv3x3_fwd_ntiles(...).  Forms whose epilogue does not
+     * fuse it run the reduction as a separate pass with the same layout. */
+    const float* bnb_y;
+    const float* bnb_mean;
+    const float* bnb_invstd;
+    const float* bnb_scale;
+    const float* bnb_shift;
+    float* bnb_part;
 } ugpg_conv_t;
 
 #define UGPG_WFMT_F32 0
@@ -163,6 +177,14 @@ int ugpg_bn_eval_params(const float* gamma, const float* beta, const float* runn
  * gradient of the conv that produced y (the reference's aten value is the same
  * sum in fp32; both are ~0 because train-mode BN cancels a preceding bias). */
 size_t ugpg_bn_relu_bwd_workspace(int64_t npix, int C);
+/* The same from partials a data gradient wrote (ugpg_conv_t.bnb_part, nslots slots):
+ * finalize + apply only; workspace ugpg_bn_relu_bwd_partials_workspace(C). */
+size_t ugpg_bn_relu_bwd_partials_workspace(int C);
+int ugpg_bn_relu_bwd_partials(const float* part, int nslots, const float* da, const float* y,
+                              int64_t npix, int C, const float* mean, const float* invstd,
+                              const float* scale, const float* shift, float* dy, float* dgamma,
+                              float* dbeta, float* dconv_bias, int accumulate_params, void* ws,
+                              size_t ws_bytes, void* stream);
 int ugpg_bn_relu_bwd(const float* da, const float* y, int64_t npix, int C, const float* mean,
                      const float* invstd, const float* scale, const float* shift,
                      float* dy, float* dgamma, float* dbeta, float* dconv_bias,

@@ -259,6 +259,53 @@ def test_bn_relu_bwd(dev, C, npix):
     close(dbt.cpu(), bd.grad, 1e-4, "dbeta")
 
 
+# (B, H, W, K = channels of dy, C = channels of da): the fused epilogue on the 8 x 32
+# and 8 x 16 persistent forms (ragged tiles included), the separate pass elsewhere
+BNB_CASES = [(2, 32, 32, 64, 64), (1, 20, 37, 64, 64), (2, 16, 16, 128, 128),
+             (1, 24, 18, 128, 64), (2, 8, 8, 128, 64)]
+
+
+@pytest.mark.parametrize("case", BNB_CASES)
+def test_dgrad_fused_bn_bwd_partials(dev, case, math):
+    """conv3x3_fwd(bnb=...) + bn_relu_bwd(part=...) == conv3x3_fwd + bn_relu_bwd: the
+    data gradient is unchanged and the BatchNorm backward (dy, dgamma, dbeta, the conv
+    bias grad) equals the standalone reduction's up to summation order."""
+    from ugpg import ops
+    B, H, W, K, Cc = case
+    dy2 = rnd((B, K, H, W), 30, "dy2")
+    w = rnd((K, Cc, 3, 3), 31, "w", 0.05)
+    y = rnd((B, Cc, H, W), 32, "y") * 2 + 0.3
+    gam, bet = rnd((Cc,), 33, "g", 0.3) + 1, rnd((Cc,), 34, "b", 0.3)
+    yd = y.double()
+    mean = yd.mean((0, 2, 3))
+    invstd = 1 / torch.sqrt(yd.var((0, 2, 3), unbiased=False) + 1e-5)
+    scale = gam.double() * invstd
+    shift = bet.double() - mean * scale
+    f = lambda t: t.float().to(dev)
+    st = [f(mean), f(invstd), f(scale), f(shift)]
+    ys, d2 = nhwc(y).to(dev), nhwc(dy2).to(dev)
+    wpk = ops.pack_conv3x3(w.to(dev), Cc, 1)
+    nt = ops.conv_ntiles(B, H, W, K, Cc, wpk)
+    part = torch.full((3 * Cc * nt,), float("nan"), device=dev)  # every slot must be written
+    da_f = torch.empty(B, H, W, Cc, device=dev)
+    ops.conv3x3_fwd([ops.Act(d2)], wpk, None, Cc, [da_f], bnb=(ys, *st, part))
+    da_r = torch.empty_like(da_f)
+    ops.conv3x3_fwd([ops.Act(d2)], wpk, None, Cc, [da_r])
+    assert torch.equal(da_f, da_r), "the partials must not change the data gradient"
+    assert torch.isfinite(part).all()
+    outs = []
+    for p in (part, None):
+        dy = torch.empty_like(da_f)
+        dg, dbt, dcb = (torch.empty(Cc, device=dev) for _ in range(3))
+        ops.bn_relu_bwd(da_f, ys, *st, dy, dg, dbt, dcb, part=p)
+        outs.append((dy.cpu(), dg.cpu(), dbt.cpu(), dcb.cpu()))
+    for name, a_, b_ in zip(("dy", "dgamma", "dbeta"), outs[0], outs[1]):
+        close(a_.double(), b_.double(), 1e-5, f"fused partials: {name}")
+    # the conv-bias gradient is a cancellation (~0): compare on the scale of |dy| sums
+    tol = 1e-6 * outs[1][0].abs().sum((0, 1, 2)).max().item()
+    assert (outs[0][3] - outs[1][3]).abs().max().item() <= tol
+
+
 def test_maxpool(dev):
     from ugpg import ops
     B, H, W, C = 2, 18, 22, 64

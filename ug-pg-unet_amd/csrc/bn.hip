@@ -329,6 +329,50 @@ extern "C" int ugpg_bn_relu_bwd(const float* da, const float* y, int64_t npix, i
     return check_launch("bn_bwd_apply");
 }
 
+namespace ugpg {
+void launch_bn_bwd_reduce(const float* da, const float* y, int64_t npix, int C, const float* mean,
+                          const float* invstd, const float* scale, const float* shift, float* part,
+                          int nslots, hipStream_t st) {
+    const int64_t ppb = cdiv(npix, (int64_t)nslots);
+    // blocks past the pixels (nslots > npix) write zero partials
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nslots), dim3(256), 0, st, da, y, npix, C, mean,
+                       invstd, scale, shift, ppb, part, nslots);
+}
+}  // namespace ugpg
+
+extern "C" size_t ugpg_bn_relu_bwd_partials_workspace(int C) {
+    return C > 0 ? (size_t)2 * C * sizeof(float) : 0;
+}
+
+// finalize + apply of ugpg_bn_relu_bwd from partials a data gradient wrote (bnb_part)
+extern "C" int ugpg_bn_relu_bwd_partials(const float* part, int nslots, const float* da,
+                                         const float* y, int64_t npix, int C, const float* mean,
+                                         const float* invstd, const float* scale,
+                                         const float* shift, float* dy, float* dgamma,
+                                         float* dbeta, float* dbias, int acc, void* ws,
+                                         size_t ws_bytes, void* stream) {
+    if (!part || nslots <= 0 || !da || !y || !dy || !mean || !invstd || !scale || !shift ||
+        C % 4 || C <= 0 || C > 1024 || npix <= 0) {
+        set_error("bn_relu_bwd_partials: bad arguments (C=%d nslots=%d)", C, nslots);
+        return UGPG_ERR_INVALID;
+    }
+    const size_t need = ugpg_bn_relu_bwd_partials_workspace(C);
+    if (!ws || ws_bytes < need) {
+        set_error("bn_relu_bwd_partials: workspace %zu < %zu", ws_bytes, need);
+        return UGPG_ERR_WORKSPACE;
+    }
+    float* coef = static_cast<float*>(ws);
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, part, nslots, C, npix,
+                       scale, dgamma, dbeta, dbias, acc, coef);
+    if (int e = check_launch("bn_bwd_finalize")) return e;
+    const unsigned q = (unsigned)(C / std::gcd(1024, C));
+    const unsigned ga = (stream_grid(npix * C / 4) + q - 1) / q * q;
+    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ga), dim3(256), 0, st, da, y, npix, C, mean,
+                       invstd, scale, shift, coef, dy);
+    return check_launch("bn_bwd_apply");
+}
+
 extern "C" int ugpg_bn_relu_apply(ugpg_src_t src, int64_t npix, float* out, void* stream) {
     if (!src.data || !out || src.C % 4) {
         set_error("bn_relu_apply: bad arguments");

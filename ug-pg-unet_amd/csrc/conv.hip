@@ -844,9 +844,29 @@ extern "C" int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream) {
         set_error("conv3x3_fwd: split-bf16 path needs 16-channel sources (C0=%d C1=%d)", C0, C1);
         return UGPG_ERR_INVALID;
     }
+    const bool bnb = p->bnb_part != nullptr;
+    if (bnb && (!p->bnb_y || !p->bnb_mean || !p->bnb_invstd || !p->bnb_scale || !p->bnb_shift ||
+                p->out_split != p->Cout || p->accumulate[0] || p->Cout > 1024)) {
+        set_error("conv3x3_fwd: BatchNorm-backward partials need bnb_y/mean/invstd/scale/shift, "
+                  "one output and no accumulate");
+        return UGPG_ERR_INVALID;
+    }
     ConvFwdArgs a;
     a.probe = 0;
     a.order = 0;
+    a.bnb_y = p->bnb_y;
+    a.bnb_mean = p->bnb_mean;
+    a.bnb_invstd = p->bnb_invstd;
+    a.bnb_scale = p->bnb_scale;
+    a.bnb_shift = p->bnb_shift;
+    a.bnb_part = p->bnb_part;
+    // forms that do not fuse the partials: the same reduction as a pass after the conv
+    auto bnb_pass = [&]() {
+        const int nslots = ugpg_conv3x3_fwd_ntiles(p->B, p->H, p->W, Cin, p->Cout, p->wfmt);
+        launch_bn_bwd_reduce(p->out[0], p->bnb_y, (int64_t)p->B * p->H * p->W, p->Cout,
+                             p->bnb_mean, p->bnb_invstd, p->bnb_scale, p->bnb_shift, p->bnb_part,
+                             nslots, as_stream(stream));
+    };
     a.src0 = p->src[0].data;
     a.sc0 = p->src[0].scale;
     a.sh0 = p->src[0].shift;
@@ -874,7 +894,8 @@ extern "C" int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream) {
         a.tiles_x = (int)cdiv(p->W, fwd_x6_tile_w(p->W, np));
         a.tiles_y = (int)cdiv(p->H, fwd_x6_tile_h(p->W, np));
         a.ntiles = p->B * a.tiles_x * a.tiles_y;
-        launch_fwd_x6(a, np, st);
+        const bool fused = launch_fwd_x6(a, np, st);
+        if (bnb && !fused) bnb_pass();
         return check_launch("conv3x3_fwd_x6");
     }
     const int cfg = pick_fwd_cfg(p->B, p->H, p->W, p->Cout, p->out_split);
@@ -901,6 +922,7 @@ extern "C" int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream) {
             else launch_fwd<8, 8, 64, 8, 2, 2>(a, st);
             break;
     }
+    if (bnb) bnb_pass();
     return check_launch("conv3x3_fwd");
 }
 

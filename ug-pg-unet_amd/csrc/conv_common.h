@@ -27,6 +27,13 @@ struct ConvFwdArgs {
     int probe;  // diagnostics only (tuning knob "x6_probe"): bit0 skip prefetch, bit1 skip staging
     int order;  // persistent x6r item order: 0 = tile-major (it = tile*NB + nb), 1 = column-
                 // block-major (it = nb*ntiles + tile: an XCD's range shares one weight slab)
+    // BatchNorm-backward partials of out0 (ugpg_conv_t.bnb_*; bnb_part == nullptr: off)
+    const float* bnb_y;
+    const float* bnb_mean;
+    const float* bnb_invstd;
+    const float* bnb_scale;
+    const float* bnb_shift;
+    float* bnb_part;
 };
 
 // Output pixel (row*TW + col inside the tile) of GEMM row m.  PERM16 is the
@@ -162,7 +169,13 @@ struct WgradArgs {
 };
 
 // split-bf16 path (conv_x6.hip)
-void launch_fwd_x6(const ConvFwdArgs& a, int np, hipStream_t st);  // np: bf16 pieces (3 or 1)
+// np: bf16 pieces (3 or 1); returns whether the launched form wrote the BatchNorm-backward
+// partials (a.bnb_part) itself
+bool launch_fwd_x6(const ConvFwdArgs& a, int np, hipStream_t st);
+// bn.hip: the per-slot BatchNorm-backward reduction (partials layout of ugpg_conv_t.bnb_part)
+void launch_bn_bwd_reduce(const float* da, const float* y, int64_t npix, int C, const float* mean,
+                          const float* invstd, const float* scale, const float* shift, float* part,
+                          int nslots, hipStream_t st);
 // batched weight packing (ugpg_pack_conv3x3_batch), kernel-argument descriptors
 struct PackItem {
     const float* w;

@@ -528,6 +528,80 @@ __device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a,
     };
     if (oacc) store_tiles(std::integral_constant<bool, true>{});
     else store_tiles(std::integral_constant<bool, false>{});
+    if (a.bnb_part != nullptr) {
+        // BatchNorm-backward partials of the stored output da (the reduction of
+        // ugpg_bn_relu_bwd, bn.hip bn_bwd_reduce_kernel, on the tile still in registers):
+        // g = da*[scale*y+shift > 0], xhat = (y-mean)*invstd; per slot sum g, g*xhat, xhat
+        f32x4 mu[2], is[2], sc[2], sh[2], sg[2], sgx[2], sx[2];
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+            const int c = n0 + c0 + 16 * nt;
+            mu[nt] = *reinterpret_cast<const f32x4*>(a.bnb_mean + c);
+            is[nt] = *reinterpret_cast<const f32x4*>(a.bnb_invstd + c);
+            sc[nt] = *reinterpret_cast<const f32x4*>(a.bnb_scale + c);
+            sh[nt] = *reinterpret_cast<const f32x4*>(a.bnb_shift + c);
+            sg[nt] = sgx[nt] = sx[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        // y loads of 4 m-tiles issued before the first is used (registers: the cw8 forms)
+        constexpr int YB = NWM == 4 ? 1 : (MTW < 4 ? MTW : 4);
+#pragma unroll
+        for (int m0 = 0; m0 < MTW; m0 += YB) {
+            f32x4 yv[YB][2];
+#pragma unroll
+            for (int u = 0; u < YB; ++u) {
+                const int mt = m0 + u;
+                const int py = min(wm * WR + prow(mt), vh - 1), px = min(pcol(mt) + l16, vw - 1);
+                const float* yp =
+                    a.bnb_y + (size_t)((b * a.H + ty0 + py) * a.W + tx0 + px) * a.Cout + n0 + c0;
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt) yv[u][nt] = *reinterpret_cast<const f32x4*>(yp + 16 * nt);
+            }
+#pragma unroll
+            for (int u = 0; u < YB; ++u) {
+                const int mt = m0 + u;
+                if (wm * WR + prow(mt) < vh && pcol(mt) + l16 < vw) {
+#pragma unroll
+                    for (int nt = 0; nt < 2; ++nt) {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const float y = yv[u][nt][i];
+                            const float gv =
+                                fmaf(y, sc[nt][i], sh[nt][i]) > 0.f ? acc[mt][nt][i] : 0.f;
+                            const float xh = (y - mu[nt][i]) * is[nt][i];
+                            sg[nt][i] += gv;
+                            sgx[nt][i] = fmaf(gv, xh, sgx[nt][i]);
+                            sx[nt][i] += xh;
+                        }
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                sg[nt][i] = row16_sum(sg[nt][i]);
+                sgx[nt][i] = row16_sum(sgx[nt][i]);
+                sx[nt][i] = row16_sum(sx[nt][i]);
+            }
+        if (l16 < 8) {
+            const int nt = l16 >> 2, i = l16 & 3;
+            float v0 = 0.f, v1 = 0.f, v2 = 0.f;
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+                if (t == l16) {
+                    v0 = sg[t >> 2][t & 3];
+                    v1 = sgx[t >> 2][t & 3];
+                    v2 = sx[t >> 2][t & 3];
+                }
+            const size_t n = n0 + c0 + 16 * nt + i, S = NWM * (size_t)a.ntiles,
+                         slot = NWM * (size_t)tile + wm;
+            a.bnb_part[(0 * (size_t)a.Cout + n) * S + slot] = v0;
+            a.bnb_part[(1 * (size_t)a.Cout + n) * S + slot] = v1;
+            a.bnb_part[(2 * (size_t)a.Cout + n) * S + slot] = v2;
+        }
+        return;
+    }
     if (a.stats == nullptr) return;
 #ifdef X6Q_NOSTATS
     return;
@@ -2074,7 +2148,7 @@ int g_x6_img = X6_IMG_DEFAULT;
 #define IMG_BPC 2
 #endif  // tuning knob "x6_img": direct fp32 kernel for the image layer
 
-void launch_fwd_x6(const ConvFwdArgs& a_in, int np, hipStream_t st) {
+bool launch_fwd_x6(const ConvFwdArgs& a_in, int np, hipStream_t st) {
     ConvFwdArgs a = a_in;
     a.probe = g_x6_probe;
     a.order = g_x6_order;
@@ -2089,7 +2163,7 @@ void launch_fwd_x6(const ConvFwdArgs& a_in, int np, hipStream_t st) {
             hipLaunchKernelGGL((conv3x3_img_fwd_kernel<4, PX>), dim3((unsigned)g), dim3(4096 / PX), 0, st, a);
         else
             hipLaunchKernelGGL((conv3x3_img_fwd_kernel<2, PX>), dim3((unsigned)g), dim3(4096 / PX), 0, st, a);
-        return;
+        return false;
     }
     if (use_x6r(a.W, np)) {
         // persistent: one workgroup per CU (a multiple of 8: blockIdx % 8 = XCD), each
@@ -2121,7 +2195,8 @@ void launch_fwd_x6(const ConvFwdArgs& a_in, int np, hipStream_t st) {
         else
             hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false>), dim3((unsigned)g), dim3(512), 0,
                                st, a);
-        return;
+        // the 16x16x32 (M16) forms fuse the BatchNorm-backward partials into the epilogue
+        return np == 3 && g_x6_pipe >= 2;
     }
     const unsigned grid = (unsigned)items;
     const bool wide = fwd_x6_tile_w(a.W, np) == 32;
@@ -2136,6 +2211,7 @@ void launch_fwd_x6(const ConvFwdArgs& a_in, int np, hipStream_t st) {
         else
             hipLaunchKernelGGL((conv3x3_fwd_x6_kernel<8, 16, true, 1>), dim3(grid), dim3(256), 0, st, a);
     }
+    return false;
 }
 
 void launch_pack_x6(const float* w, void* wpk, int Cout, int Cin, int Cin_pad, int mode, int np,

@@ -25,7 +25,8 @@ class ConvDesc(C.Structure):
     """ugpg_conv_t."""
     _fields_ = [("B", _i), ("H", _i), ("W", _i), ("src", Src * 2), ("wpk", _p), ("bias", _p),
                 ("Cout", _i), ("out", _p * 2), ("out_split", _i), ("accumulate", _i * 2),
-                ("stats", _p), ("wfmt", _i)]
+                ("stats", _p), ("wfmt", _i), ("bnb_y", _p), ("bnb_mean", _p),
+                ("bnb_invstd", _p), ("bnb_scale", _p), ("bnb_shift", _p), ("bnb_part", _p)]
 
 
 class PackItem(C.Structure):
@@ -55,6 +56,9 @@ SIGNATURES = {
     "ugpg_bn_eval_params": (_i, [_p, _p, _p, _p, _f, _i, _p, _p, _p]),
     "ugpg_bn_relu_bwd_workspace": (_sz, [_i64, _i]),
     "ugpg_bn_relu_bwd": (_i, [_p, _p, _i64, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i, _p, _sz, _p]),
+    "ugpg_bn_relu_bwd_partials_workspace": (_sz, [_i]),
+    "ugpg_bn_relu_bwd_partials": (_i, [_p, _i, _p, _p, _i64, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i,
+                                       _p, _sz, _p]),
     "ugpg_bn_relu_apply": (_i, [Src, _i64, _p, _p]),
     "ugpg_maxpool2_fwd": (_i, [Src, _i, _i, _i, _p, _p, _p]),
     "ugpg_maxpool2_bwd": (_i, [_p, _p, _i, _i, _i, _i, _p, _i, _p]),

@@ -13,12 +13,17 @@ PyTorch arithmetic runs anywhere on the path.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 
 import torch
 
 from . import ops
 from .ops import Act
+
+# A/B switch: BN1's backward reduction fused into the data gradient of conv2
+_FUSE_BN_BWD = os.environ.get("UGPG_FUSE_BN_BWD", "1") != "0"
+_FUSE_BN_BWD_MIN_K = int(os.environ.get("UGPG_FUSE_BN_BWD_MIN_K", "64"))
 
 
 def ceil_to(v: int, m: int) -> int:
@@ -102,15 +107,16 @@ def double_conv_forward(mod, srcs, ctx: BlockCtx, save: bool):
     return cur[0]
 
 
-def _bn_relu_wgrad(conv, bn, y, st, in_srcs, dy, grads):
-    """In place: dy <- dL/d(conv output) from dL/d(relu(bn(y))); then dW, db."""
+def _bn_relu_wgrad(conv, bn, y, st, in_srcs, dy, grads, part=None):
+    """In place: dy <- dL/d(conv output) from dL/d(relu(bn(y))); then dW, db.
+    part: BatchNorm-backward partials written by the data gradient that produced dy."""
     mean, invstd, scale, shift = st
     if mean is None:
         raise RuntimeError("backward through an eval-mode BatchNorm is not supported")
     # the conv bias gradient (sum of dy) comes out of the BN-backward reduction
     db = grads.get(conv.bias) if conv.bias is not None else None
     ops.bn_relu_bwd(dy, y, mean, invstd, scale, shift, dy, grads.get(bn.weight),
-                    grads.get(bn.bias), db)
+                    grads.get(bn.bias), db, part=part)
     dw = grads.get(conv.weight)
     if dw is not None:
         co, ci = conv.weight.shape[0], conv.weight.shape[1]
@@ -131,10 +137,20 @@ def double_conv_backward(mod, ctx: BlockCtx, da2, targets, acc_flags, grads, pad
     cmid = c2.weight.shape[1]
     da1 = ops.empty(B, H, W, cmid, like=da2)
     npix = B * H * W
-    ops.conv3x3_fwd([Act(da2)], ops.pack_conv3x3(c2.weight.detach(), cmid, 1), None, cmid, [da1],
-                    flops=2.0 * npix * cmid * 9 * cout)
+    wpk2 = ops.pack_conv3x3(c2.weight.detach(), cmid, 1)
+    # the data gradient also reduces BN1's backward sums over da1 while each tile is in
+    # registers (ugpg_conv_t.bnb_*), so BN1's backward is finalize + apply only
+    part = bnb = None
+    # (tools/ab_step.py, interleaved: -0.9 % step time fusing every layer, -0.2 % with
+    # K >= 128 only; the K = 64 items are 4 steps long, so the extra epilogue pass costs
+    # those dgrads most of what the separate reduction did -- UGPG_FUSE_BN_BWD_MIN_K)
+    if ctx.st1[0] is not None and _FUSE_BN_BWD and cout >= _FUSE_BN_BWD_MIN_K:
+        part = ops.empty(3 * cmid * ops.conv_ntiles(B, H, W, cout, cmid, wpk2), like=da2)
+        bnb = (ctx.y1, *ctx.st1, part)
+    ops.conv3x3_fwd([Act(da2)], wpk2, None, cmid, [da1], flops=2.0 * npix * cmid * 9 * cout,
+                    bnb=bnb)
     # stage 1: BN1/ReLU backward, wgrad(conv1), dgrad(conv1) -> source targets
-    _bn_relu_wgrad(c1, b1, ctx.y1, ctx.st1, ctx.srcs, da1, grads)
+    _bn_relu_wgrad(c1, b1, ctx.y1, ctx.st1, ctx.srcs, da1, grads, part=part)
     if not any(t is not None for t in targets):
         return
     cin = c1.weight.shape[1]

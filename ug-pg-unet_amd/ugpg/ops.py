@@ -262,9 +262,12 @@ def _timed(name, flops, fn):
 
 
 def conv3x3_fwd(srcs, wpk, bias, cout, outs, split=None, accumulate=(0, 0), stats=None,
-                flops=None):
+                flops=None, bnb=None):
     """srcs: 1-2 Act; outs: 1-2 NHWC tensors (channel split at `split`).
-    flops: algorithmic FLOPs of this call (for the optional KernelTimer)."""
+    flops: algorithmic FLOPs of this call (for the optional KernelTimer).
+    bnb: (y, mean, invstd, scale, shift, part) -- also write the BatchNorm-backward
+    partials of outs[0] = dL/d(relu(bn(y))) into `part` (3*cout*conv_ntiles floats) for
+    bn_relu_bwd(..., part=part)."""
     B, H, W, _ = srcs[0].shape
     d = ConvDesc()
     d.B, d.H, d.W = B, H, W
@@ -277,6 +280,9 @@ def conv3x3_fwd(srcs, wpk, bias, cout, outs, split=None, accumulate=(0, 0), stat
     d.accumulate[0], d.accumulate[1] = int(accumulate[0]), int(accumulate[1])
     d.stats = ptr(stats)
     d.wfmt = wpk.ugpg_fmt
+    if bnb is not None:
+        (d.bnb_y, d.bnb_mean, d.bnb_invstd, d.bnb_scale, d.bnb_shift,
+         d.bnb_part) = (ptr(t) for t in bnb)
     _timed("conv3x3_fwd", flops,
            lambda: check(lib.ugpg_conv3x3_fwd(C.byref(d), stream()), "conv3x3_fwd"))
 
@@ -318,9 +324,18 @@ def bn_eval_params(gamma, beta, rm, rv, eps):
 
 
 def bn_relu_bwd(da, y, mean, invstd, scale, shift, dy, dgamma, dbeta, dconv_bias=None,
-                accumulate=0):
+                accumulate=0, part=None):
+    """part: partials the data gradient producing `da` wrote (conv3x3_fwd(bnb=...)):
+    only the finalize and apply passes run."""
     c = y.shape[-1]
     npix = y.numel() // c
+    if part is not None:
+        ws = workspace(lib.ugpg_bn_relu_bwd_partials_workspace(c), y.device)
+        check(lib.ugpg_bn_relu_bwd_partials(
+            ptr(part), part.numel() // (3 * c), ptr(da), ptr(y), npix, c, ptr(mean), ptr(invstd),
+            ptr(scale), ptr(shift), ptr(dy), ptr(dgamma), ptr(dbeta), ptr(dconv_bias),
+            int(accumulate), ptr(ws), ws.numel(), stream()), "bn_relu_bwd_partials")
+        return
     ws = workspace(lib.ugpg_bn_relu_bwd_workspace(npix, c), y.device)
     check(lib.ugpg_bn_relu_bwd(ptr(da), ptr(y), npix, c, ptr(mean), ptr(invstd), ptr(scale),
                                ptr(shift), ptr(dy), ptr(dgamma), ptr(dbeta), ptr(dconv_bias),
