@@ -306,6 +306,47 @@ def test_dgrad_fused_bn_bwd_partials(dev, case, math):
     assert (outs[0][3] - outs[1][3]).abs().max().item() <= tol
 
 
+def test_bn_eval_params_cache(dev):
+    """Eval-mode BN (scale, shift) cached on the module: reused while gamma, beta and the
+    running stats are unchanged, recomputed after any in-place write (torch ops, the
+    optimizers' and bn_finalize's raw-pointer writes bump the version counter)."""
+    from ugpg import ops
+    bn = torch.nn.BatchNorm2d(64).to(dev)
+    with torch.no_grad():
+        bn.running_mean.copy_(rnd((64,), 40, "rm").to(dev))
+        bn.running_var.copy_(rnd((64,), 41, "rv").abs().to(dev) + 0.5)
+        bn.weight.copy_(rnd((64,), 42, "g").to(dev))
+
+    def ref():
+        sc = bn.weight.double() / torch.sqrt(bn.running_var.double() + bn.eps)
+        return sc, bn.bias.double() - bn.running_mean.double() * sc
+
+    def get():
+        return ops.bn_eval_params(bn.weight.detach(), bn.bias.detach(), bn.running_mean,
+                                  bn.running_var, bn.eps, owner=bn)
+    s1, h1 = get()
+    s2, h2 = get()
+    assert s2 is s1 and h2 is h1, "unchanged parameters: cached"
+    close(s1, ref()[0], 1e-6, "scale")
+    with torch.no_grad():
+        bn.running_var.mul_(2.0)
+    s3, h3 = get()
+    assert s3 is not s1
+    close(s3, ref()[0], 1e-6, "scale after running_var write")
+    # bn_finalize updates the running stats through a raw pointer: must invalidate too
+    stats = torch.zeros(3 * 64 * 4, device=dev)
+    stats[:64 * 4] = 10.0
+    stats[64 * 4:2 * 64 * 4] = 5.0
+    stats[2 * 64 * 4:] = 7.0
+    nbt = torch.zeros((), dtype=torch.int64, device=dev)
+    ops.bn_finalize(stats, 4, bn.weight.detach(), bn.bias.detach(), bn.running_mean,
+                    bn.running_var, nbt, 0.1, bn.eps)
+    s4, h4 = get()
+    assert s4 is not s3
+    close(s4, ref()[0], 1e-6, "scale after bn_finalize")
+    close(h4, ref()[1], 1e-6, "shift after bn_finalize")
+
+
 def test_maxpool(dev):
     from ugpg import ops
     B, H, W, C = 2, 18, 22, 64

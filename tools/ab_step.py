@@ -39,9 +39,12 @@ def main():
     ap.add_argument("--b", required=True)
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--conv-math", default="x6", choices=("x6", "bf16", "f32"))
     a = ap.parse_args()
     import torch
     import ugpg
+    from ugpg import ops
+    ops.set_conv_math(a.conv_math)
     from ugpg.trainer import MetricsReadback
     dev = torch.device("cuda:0")
     torch.manual_seed(1234)

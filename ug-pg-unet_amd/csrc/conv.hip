@@ -806,12 +806,12 @@ extern "C" int ugpg_set_tuning(const char* key, int value) {
 }
 
 extern "C" int ugpg_conv3x3_fwd_ntiles(int B, int H, int W, int Cin, int Cout, int wfmt) {
-    (void)Cin;
     if (wfmt == UGPG_WFMT_X6 || wfmt == UGPG_WFMT_BF16) {
         const int np = wfmt == UGPG_WFMT_X6 ? 3 : 1;
         return fwd_x6_stat_slots(
             (int)(B * cdiv(H, fwd_x6_tile_h(W, np)) * cdiv(W, fwd_x6_tile_w(W, np))), W, np);
     }
+    if (img_fwd_eligible(W, Cin, 0, Cout)) return img_fwd_slots(B, H, W, 2);
     const int cfg = pick_fwd_cfg(B, H, W, Cout, Cout);
     return (int)(B * cdiv(H, kFwd[cfg].th) * cdiv(W, kFwd[cfg].tw));
 }
@@ -897,6 +897,18 @@ extern "C" int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream) {
         const bool fused = launch_fwd_x6(a, np, st);
         if (bnb && !fused) bnb_pass();
         return check_launch("conv3x3_fwd_x6");
+    }
+    if (img_fwd_eligible(p->W, C0, C1, p->Cout)) {
+        // the image layer in fp32 / bf16 mode: the direct fp32 kernel on the fp32 pack
+        a.tiles_x = (int)cdiv(p->W, 32);
+        a.tiles_y = (int)cdiv(p->H, 8);
+        a.ntiles = p->B * a.tiles_x * a.tiles_y;
+        if (launch_img_fwd(a, true, st)) return check_launch("conv3x3_img_fwd");
+        if (p->stats) {  // ugpg_conv3x3_fwd_ntiles counted the image kernel's slots
+            set_error("conv3x3_fwd: BatchNorm partials of an 8-channel source need one "
+                      "output without accumulate");
+            return UGPG_ERR_INVALID;
+        }
     }
     const int cfg = pick_fwd_cfg(p->B, p->H, p->W, p->Cout, p->out_split);
     if (p->out_split % kFwd[cfg].bn) {

@@ -172,6 +172,11 @@ struct WgradArgs {
 // np: bf16 pieces (3 or 1); returns whether the launched form wrote the BatchNorm-backward
 // partials (a.bnb_part) itself
 bool launch_fwd_x6(const ConvFwdArgs& a, int np, hipStream_t st);
+// the image layer's direct fp32 forward (conv_x6.hip, knob "x6_img"): shape predicate,
+// BatchNorm slot count (nwm row groups per 8 x 32 tile), launch (false: not applicable)
+bool img_fwd_eligible(int W, int C0, int C1, int Cout);
+int img_fwd_slots(int B, int H, int W, int nwm);
+bool launch_img_fwd(const ConvFwdArgs& a, bool wf32, hipStream_t st);
 // bn.hip: the per-slot BatchNorm-backward reduction (partials layout of ugpg_conv_t.bnb_part)
 void launch_bn_bwd_reduce(const float* da, const float* y, int64_t npix, int C, const float* mean,
                           const float* invstd, const float* scale, const float* shift, float* part,

@@ -421,6 +421,48 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
     };
     if (oacc) store_rows(std::integral_constant<bool, true>{});
     else store_rows(std::integral_constant<bool, false>{});
+    if (a.bnb_part != nullptr) {
+        // BatchNorm-backward partials of the stored output (as x6q_epilogue_wave): this
+        // lane's channel over its pixels, the two pixel halves (h) combined by a shuffle
+        const int n = n0 + nl;
+        const float mu = a.bnb_mean[n], is = a.bnb_invstd[n], sc = a.bnb_scale[n],
+                    sh = a.bnb_shift[n];
+        float sg = 0.f, sgx = 0.f, sx = 0.f;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+            const int py = wm * MT + mt;
+            if (py >= vh) break;  // uniform
+            const float* yrow =
+                a.bnb_y + (size_t)((b * a.H + ty0 + py) * a.W + tx0 + 4 * h) * a.Cout + n;
+            float yv[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int pxc = min((r & 3) + 8 * (r >> 2), vw - 1 - 4 * h);
+                yv[r] = yrow[(size_t)max(pxc, -4 * h) * a.Cout];
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int pxc = (r & 3) + 8 * (r >> 2);
+                if (fullw || pxc + 4 * h < vw) {
+                    const float gv = fmaf(yv[r], sc, sh) > 0.f ? acc[mt][r] : 0.f;
+                    const float xh = (yv[r] - mu) * is;
+                    sg += gv;
+                    sgx = fmaf(gv, xh, sgx);
+                    sx += xh;
+                }
+            }
+        }
+        sg += __shfl_xor(sg, 32, 64);
+        sgx += __shfl_xor(sgx, 32, 64);
+        sx += __shfl_xor(sx, 32, 64);
+        if (lane < 32) {
+            const size_t S = 2 * (size_t)a.ntiles, slot = 2 * (size_t)tile + wm;
+            a.bnb_part[(0 * (size_t)a.Cout + n) * S + slot] = sg;
+            a.bnb_part[(1 * (size_t)a.Cout + n) * S + slot] = sgx;
+            a.bnb_part[(2 * (size_t)a.Cout + n) * S + slot] = sx;
+        }
+        return;
+    }
     if (a.stats == nullptr) return;
     constexpr int WROWS = MT * 32 / TW;  // image rows of one wave's pixels
     const int rows = min(max(vh - wm * WROWS, 0), WROWS);
@@ -1942,7 +1984,7 @@ int g_x6_probe = 0;  // "x6_probe": timing diagnostics (see ugpg_set_tuning)
 // Products and sums in fp32 (the fp32-MFMA path's arithmetic class), as packed pairs.
 // Epilogue: bias, store, BatchNorm partials (count, sum, M2 about the slot mean) in
 // x6r's slot layout (NWM row groups per tile).
-template <int NWM, int PX>
+template <int NWM, int PX, bool WF32>
 __global__ void __launch_bounds__(4096 / PX) conv3x3_img_fwd_kernel(ConvFwdArgs a) {
     typedef float f2 __attribute__((ext_vector_type(2)));
     // PX pixels per thread: 16 lanes x (TW / PX) segments per tile row
@@ -1956,39 +1998,68 @@ __global__ void __launch_bounds__(4096 / PX) conv3x3_img_fwd_kernel(ConvFwdArgs 
     __shared__ int nci_s;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int tpi = a.tiles_x * a.tiles_y;
-    auto halo_fetch = [&](int tile, f32x4* r) {
+    // lazy BN+ReLU of the source (the image itself has none): this thread's 4 channels
+    // are fixed (piece q = tid & 1, NT even); zero padding stays zero
+    const bool aon = a.sc0 != nullptr;
+    f32x4 asc = {1.f, 1.f, 1.f, 1.f}, ash = {0.f, 0.f, 0.f, 0.f};
+    if (aon)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            asc[i] = a.sc0[4 * (tid & 1) + i];
+            ash[i] = a.sh0[4 * (tid & 1) + i];
+        }
+    auto halo_fetch = [&](int tile, f32x4* r, unsigned& hv) {
         const int b = tile / tpi, trem = tile % tpi;
         const int ty0 = (trem / a.tiles_x) * TH, tx0 = (trem % a.tiles_x) * TW;
+        hv = 0u;
 #pragma unroll
         for (int k = 0; k < HPT; ++k) {
             const int e = tid + NT * k, hp = e >> 1, q = e & 1;
             const int gy = ty0 - 1 + hp / (TW + 2), gx = tx0 - 1 + hp % (TW + 2);
             r[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (e < NH && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W)
+            if (e < NH && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
                 r[k] = *reinterpret_cast<const f32x4*>(
                     a.src0 + ((size_t)(b * a.H + gy) * a.W + gx) * CIN + 4 * q);
+                hv |= 1u << k;
+            }
         }
     };
-    auto halo_put = [&](int buf, const f32x4* r) {
+    auto halo_put = [&](int buf, const f32x4* r, unsigned hv) {
 #pragma unroll
         for (int k = 0; k < HPT; ++k) {
             const int e = tid + NT * k, hp = e >> 1, q = e & 1;
             const int o = (hp / (TW + 2)) * HWP + hp % (TW + 2);
+            const bool act = aon && ((hv >> k) & 1u);
             if (e < NH)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) xs[buf][4 * q + i][o] = r[k][i];
+                for (int i = 0; i < 4; ++i)
+                    xs[buf][4 * q + i][o] = act ? fmaxf(fmaf(r[k][i], asc[i], ash[i]), 0.f) : r[k][i];
         }
     };
     if (blockIdx.x >= a.ntiles) return;
     f32x4 hr[HPT];
-    halo_fetch(blockIdx.x, hr);
+    unsigned hv;
+    halo_fetch(blockIdx.x, hr, hv);
     // weights: pack layout of pack_x6_elem (mode 0, K = 16, nb = 0)
     const __bf16* wp = static_cast<const __bf16*>(a.wpk);
     constexpr int plane = 3 * 64 * 8;
     if (tid == 0) nci_s = 0;
     __syncthreads();
     int hi = 0;
-    {
+    if constexpr (WF32) {
+        // fp32 pack [K/8][9][N][8] (K = 8): element (t, co, ci) at (t*64 + co)*8 + ci
+        constexpr int NE = 9 * CIN * 64 / NT;
+        const float* wf = static_cast<const float*>(a.wpk);
+        float pv[NE];
+#pragma unroll
+        for (int k = 0; k < NE; ++k) pv[k] = wf[tid + NT * k];
+#pragma unroll
+        for (int k = 0; k < NE; ++k) {
+            const int e = tid + NT * k, ci = e & 7, co = (e >> 3) & 63, t = e >> 9;
+            wsm[t * CIN + ci][co] = pv[k];
+            if (pv[k] != 0.f) hi = max(hi, ci + 1);
+        }
+    } else {
         // all 3 x 9 * 512 / NT loads issued before the first is used (one round trip)
         constexpr int NE = 9 * CIN * 64 / NT;
         __bf16 pc[NE][3];
@@ -2009,7 +2080,7 @@ __global__ void __launch_bounds__(4096 / PX) conv3x3_img_fwd_kernel(ConvFwdArgs 
     }
     for (int o = 32; o > 0; o >>= 1) hi = max(hi, __shfl_xor(hi, o, 64));
     if (lane == 0) atomicMax(&nci_s, hi);
-    halo_put(0, hr);
+    halo_put(0, hr, hv);
     __syncthreads();
     const int nci = nci_s;
     // thread: channels 4*cq..+3 of the PX-pixel row segment (row, c0..c0+PX-1)
@@ -2020,7 +2091,7 @@ __global__ void __launch_bounds__(4096 / PX) conv3x3_img_fwd_kernel(ConvFwdArgs 
     int buf = 0;
     for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x, buf ^= 1) {
         const int nxt = tile + gridDim.x;
-        if (nxt < a.ntiles) halo_fetch(nxt, hr);
+        if (nxt < a.ntiles) halo_fetch(nxt, hr, hv);
         const int b = tile / tpi, trem = tile % tpi;
         const int ty0 = (trem / a.tiles_x) * TH, tx0 = (trem % a.tiles_x) * TW;
         f2 acc[PX][2];
@@ -2078,7 +2149,7 @@ __global__ void __launch_bounds__(4096 / PX) conv3x3_img_fwd_kernel(ConvFwdArgs 
                 for (int i = 0; i < 4; ++i) sj[i] += v[p][i];
             }
         }
-        if (nxt < a.ntiles) halo_put(buf ^ 1, hr);
+        if (nxt < a.ntiles) halo_put(buf ^ 1, hr, hv);
         if (a.stats != nullptr) {
             // BatchNorm partials per (channel, slot): slot = NWM * tile + row group.
             // wave sums: the 4 segments holding the same channels (lane bits 4, 5)
@@ -2148,23 +2219,39 @@ int g_x6_img = X6_IMG_DEFAULT;
 #define IMG_BPC 2
 #endif  // tuning knob "x6_img": direct fp32 kernel for the image layer
 
+bool img_fwd_eligible(int W, int C0, int C1, int Cout) {
+    return g_x6_img && W >= 32 && C0 == 8 && C1 == 0 && Cout == 64;
+}
+int img_fwd_slots(int B, int H, int W, int nwm) {
+    return nwm * B * (int)cdiv(H, 8) * (int)cdiv(W, 32);
+}
+
+// the image layer's direct fp32 kernel (8 x 32 tiles; a.tiles_* / ntiles set for them);
+// false when the call does not qualify
+bool launch_img_fwd(const ConvFwdArgs& a, bool wf32, hipStream_t st) {
+    if (!img_fwd_eligible(a.W, a.C0, a.C1, a.Cout) || a.split != a.Cout || a.acc0 ||
+        a.bnb_part)
+        return false;
+    // persistent: IMG_BPC workgroups per CU
+    int64_t g = std::min<int64_t>(IMG_BPC * (int64_t)cu_count(st), (int64_t)a.ntiles);
+    g = std::max<int64_t>(1, g);
+    constexpr int PX = IMG_PX;
+    const dim3 grid((unsigned)g), block(4096 / PX);
+    if (wf32)
+        hipLaunchKernelGGL((conv3x3_img_fwd_kernel<2, PX, true>), grid, block, 0, st, a);
+    else if (x6r_cw(3) == 8)
+        hipLaunchKernelGGL((conv3x3_img_fwd_kernel<4, PX, false>), grid, block, 0, st, a);
+    else
+        hipLaunchKernelGGL((conv3x3_img_fwd_kernel<2, PX, false>), grid, block, 0, st, a);
+    return true;
+}
+
 bool launch_fwd_x6(const ConvFwdArgs& a_in, int np, hipStream_t st) {
     ConvFwdArgs a = a_in;
     a.probe = g_x6_probe;
     a.order = g_x6_order;
     const int64_t items = (int64_t)a.ntiles * (a.Cout / 64);
-    if (np == 3 && use_x6r(a.W, np) && a.W >= 32 && a.C0 == 8 && a.C1 == 0 && a.Cin == 16 &&
-        a.Cout == 64 && a.sc0 == nullptr && a.split == a.Cout && !a.acc0 && g_x6_img) {
-        // persistent: IMG_BPC workgroups per CU
-        int64_t g = std::min<int64_t>(IMG_BPC * (int64_t)cu_count(st), (int64_t)a.ntiles);
-        g = std::max<int64_t>(1, g);
-        constexpr int PX = IMG_PX;
-        if (x6r_cw(np) == 8)
-            hipLaunchKernelGGL((conv3x3_img_fwd_kernel<4, PX>), dim3((unsigned)g), dim3(4096 / PX), 0, st, a);
-        else
-            hipLaunchKernelGGL((conv3x3_img_fwd_kernel<2, PX>), dim3((unsigned)g), dim3(4096 / PX), 0, st, a);
-        return false;
-    }
+    if (np == 3 && use_x6r(a.W, np) && a.Cin == 16 && launch_img_fwd(a, false, st)) return false;
     if (use_x6r(a.W, np)) {
         // persistent: one workgroup per CU (a multiple of 8: blockIdx % 8 = XCD), each
         // walking a strided share of its XCD's contiguous item range
@@ -2195,8 +2282,8 @@ bool launch_fwd_x6(const ConvFwdArgs& a_in, int np, hipStream_t st) {
         else
             hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false>), dim3((unsigned)g), dim3(512), 0,
                                st, a);
-        // the 16x16x32 (M16) forms fuse the BatchNorm-backward partials into the epilogue
-        return np == 3 && g_x6_pipe >= 2;
+        // every persistent form fuses the BatchNorm-backward partials into its epilogue
+        return true;
     }
     const unsigned grid = (unsigned)items;
     const bool wide = fwd_x6_tile_w(a.W, np) == 32;

@@ -327,10 +327,12 @@ def broadcast_parameters(module: torch.nn.Module, src: int = 0):
     if ws <= 1:
         return
     params = list(module.parameters())
-    for t in params + list(module.buffers()):
+    bufs = list(module.buffers())
+    for t in params + bufs:
         dist.broadcast(t.data, src)
     from . import ops
-    ops.weights_written(params)  # written behind autograd's back: cached packs are stale
+    # written behind autograd's back: cached packs / eval BN params are stale
+    ops.weights_written(params + bufs)
 
 
 def broadcast_buffers(module: torch.nn.Module, src: int = 0):
@@ -339,8 +341,11 @@ def broadcast_buffers(module: torch.nn.Module, src: int = 0):
     _, ws = world()
     if ws <= 1:
         return
-    for t in module.buffers():
+    bufs = list(module.buffers())
+    for t in bufs:
         dist.broadcast(t.data, src)
+    from . import ops
+    ops.weights_written(bufs)  # cached eval-mode BN parameters are stale
 
 
 def allreduce_metrics(mbuf, ip: int, n_stat: float, avg_mask: int):

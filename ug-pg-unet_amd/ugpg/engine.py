@@ -95,7 +95,8 @@ def double_conv_forward(mod, srcs, ctx: BlockCtx, save: bool):
             st = (mean, invstd, scale, shift)
         else:
             scale, shift = ops.bn_eval_params(bn.weight.detach(), bn.bias.detach(),
-                                              bn.running_mean, bn.running_var, float(bn.eps))
+                                              bn.running_mean, bn.running_var, float(bn.eps),
+                                              owner=bn)
             st = (None, None, scale, shift)
         if save:
             if i == 0:

@@ -312,14 +312,32 @@ def bn_finalize(stats, ntiles, gamma, beta, rm, rv, nbt, momentum, eps):
     check(lib.ugpg_bn_finalize(ptr(stats), ntiles, c, _f32(gamma), _f32(beta), ptr(rm), ptr(rv),
                                ptr(nbt), momentum, eps, ptr(mean), ptr(invstd), ptr(scale),
                                ptr(shift), stream()), "bn_finalize")
+    if rm is not None:
+        weights_written([rm, rv])  # running stats updated in place (eval-param cache keys)
     return mean, invstd, scale, shift
 
 
-def bn_eval_params(gamma, beta, rm, rv, eps):
+_EVAL_CACHE_ON = os.environ.get("UGPG_BN_EVAL_CACHE", "1") != "0"  # A/B switch
+
+
+def bn_eval_params(gamma, beta, rm, rv, eps, owner=None):
+    """(scale, shift) of an eval-mode BatchNorm.  With `owner` (the module) the result is
+    cached on it, keyed on the storage and version counter of gamma, beta and the running
+    stats -- every writer of those bumps the version (optimizers, bn_finalize, the DP
+    broadcasts, load_state_dict's copy_) -- so a frozen previous stage (the U-map
+    producer) costs no launch per step."""
+    key = None
+    if owner is not None and _EVAL_CACHE_ON:
+        key = tuple((t.data_ptr(), t._version) for t in (gamma, beta, rm, rv)) + (float(eps),)
+        hit = getattr(owner, "_ugpg_eval_params", None)
+        if hit is not None and hit[0] == key:
+            return hit[1]
     c = gamma.numel()
     scale, shift = empty(c, like=gamma), empty(c, like=gamma)
     check(lib.ugpg_bn_eval_params(_f32(gamma), _f32(beta), _f32(rm), _f32(rv), eps, c,
                                   ptr(scale), ptr(shift), stream()), "bn_eval_params")
+    if key is not None:
+        owner._ugpg_eval_params = (key, (scale, shift))
     return scale, shift
 
 
