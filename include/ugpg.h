@@ -180,6 +180,19 @@ size_t ugpg_bn_relu_bwd_workspace(int64_t npix, int C);
 /* The same from partials a data gradient wrote (ugpg_conv_t.bnb_part, nslots slots):
  * finalize + apply only; workspace ugpg_bn_relu_bwd_partials_workspace(C). */
 size_t ugpg_bn_relu_bwd_partials_workspace(int C);
+/* BatchNorm-backward partials folded into the kernel that last writes da (the pooling,
+ * upsampling and head backward entries *_bnb): same partial layout, nslots from
+ * ugpg_bnb_slots(npix, C) (0 for unsupported shapes). */
+typedef struct {
+    const float* y;        /* NHWC [npix][C]: the BN input */
+    const float* mean;
+    const float* invstd;
+    const float* scale;
+    const float* shift;
+    float* part;           /* [3][C][nslots] */
+    int nslots;
+} ugpg_bnb_t;
+int ugpg_bnb_slots(int64_t npix, int C);
 int ugpg_bn_relu_bwd_partials(const float* part, int nslots, const float* da, const float* y,
                               int64_t npix, int C, const float* mean, const float* invstd,
                               const float* scale, const float* shift, float* dy, float* dgamma,
@@ -197,6 +210,9 @@ int ugpg_maxpool2_fwd(ugpg_src_t src, int B, int H, int W, float* out, uint8_t* 
                       void* stream);
 int ugpg_maxpool2_bwd(const float* dout, const uint8_t* argmax, int B, int H, int W, int C,
                       float* din, int accumulate, void* stream);
+/* The same, also writing the BatchNorm-backward partials of din (see ugpg_bnb_t). */
+int ugpg_maxpool2_bwd_bnb(const float* dout, const uint8_t* argmax, int B, int H, int W, int C,
+                          float* din, int accumulate, const ugpg_bnb_t* bnb, void* stream);
 
 /* ---- align_corners=True bilinear resize, NHWC (UG_unet_parts.py:78, K9) ---- */
 int ugpg_bilinear_nhwc_fwd(ugpg_src_t src, int B, int Hi, int Wi, float* out, int Ho, int Wo,
@@ -236,6 +252,12 @@ size_t ugpg_head_bwd_workspace(int64_t npix, int C, int nc);
 int ugpg_head_bwd(ugpg_src_t src, int64_t npix, const float* w, int nc, const float* dh,
                   float* dw, float* db, float* da, int accumulate_da, void* ws, size_t ws_bytes,
                   void* stream);
+/* The same, also writing the BatchNorm-backward partials of da (ugpg_bnb_t; bnb->y must
+ * be src.data, the BN input the head reads lazily): nslots = ugpg_head_bwd_bnb_slots. */
+int ugpg_head_bwd_bnb_slots(int64_t npix);
+int ugpg_head_bwd_bnb(ugpg_src_t src, int64_t npix, const float* w, int nc, const float* dh,
+                      float* dw, float* db, float* da, int accumulate_da, void* ws,
+                      size_t ws_bytes, const ugpg_bnb_t* bnb, void* stream);
 
 /* ---- uncertainty-weighted BCE-with-logits (UG_unet.py:61-94, K13) ---------
  * pixel = (1-t)x + (1+(pw-1)t)*softplus(-x);  final = mean(pixel*(1+alpha*U))

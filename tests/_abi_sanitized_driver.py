@@ -33,7 +33,8 @@ def main():
         if name in ("ugpg_version", "ugpg_last_error", "ugpg_comm_id_bytes"):
             getattr(lib, name)()
             continue
-        if res is not C.c_int or name in ("ugpg_conv3x3_fwd_ntiles",):  # size/count queries
+        if res is not C.c_int or name in ("ugpg_conv3x3_fwd_ntiles", "ugpg_bnb_slots",
+                                                 "ugpg_head_bwd_bnb_slots"):  # queries
             getattr(lib, name)(*[bad_value(a) for a in args])
             continue
         rc = getattr(lib, name)(*[bad_value(a) for a in args])

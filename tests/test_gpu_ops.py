@@ -306,6 +306,59 @@ def test_dgrad_fused_bn_bwd_partials(dev, case, math):
     assert (outs[0][3] - outs[1][3]).abs().max().item() <= tol
 
 
+@pytest.mark.parametrize("C,acc", [(64, 0), (64, 1), (128, 1), (512, 0)])
+def test_maxpool2_bwd_fused_bn_partials(dev, C, acc):
+    """maxpool2_bwd(bnb=...) writes the same din and the BatchNorm-backward partials that
+    make bn_relu_bwd(part=...) equal the standalone reduction."""
+    from ugpg import ops
+    B, H, W = 2, 18, 22
+    x = nhwc(rnd((B, C, H, W), 50, "x")).to(dev)
+    out, am = ops.maxpool2_fwd(ops.Act(x))
+    dout = nhwc(rnd((B, C, H // 2, W // 2), 51, "dp")).to(dev)
+    base = nhwc(rnd((B, C, H, W), 52, "base")).to(dev)
+    y = nhwc(rnd((B, C, H, W), 53, "y") * 2 + 0.3).to(dev)
+    st = [rnd((C,), 54 + i, f"s{i}").abs().to(dev) + 0.1 for i in range(4)]
+    st[3] = st[3] - 0.5
+    d1, d2 = base.clone(), base.clone()
+    part = ops.maxpool2_bwd(dout, am, H, W, d1, acc, bnb=(y, *st))
+    ops.maxpool2_bwd(dout, am, H, W, d2, acc)
+    assert torch.equal(d1, d2)
+    outs = []
+    for p in (part, None):
+        dy = torch.empty_like(d1)
+        dg, dbt, dcb = (torch.empty(C, device=dev) for _ in range(3))
+        ops.bn_relu_bwd(d1, y, *st, dy, dg, dbt, dcb, part=p)
+        outs.append((dy.cpu(), dg.cpu(), dbt.cpu()))
+    for name, a_, b_ in zip(("dy", "dgamma", "dbeta"), outs[0], outs[1]):
+        close(a_, b_, 1e-5, f"maxpool-fused partials: {name}")
+
+
+@pytest.mark.parametrize("C,nc,acc", [(64, 1, 0), (64, 2, 1), (128, 1, 1)])
+def test_head_bwd_fused_bn_partials(dev, C, nc, acc):
+    """head_bwd(bnb=...) = head_bwd + the standalone BatchNorm-backward reduction."""
+    from ugpg import ops
+    B, H, W = 2, 20, 24
+    y = nhwc(rnd((B, C, H, W), 60, "y") * 2 + 0.3).to(dev)
+    mean, invstd = rnd((C,), 61, "m").to(dev), rnd((C,), 62, "i").abs().to(dev) + 0.2
+    sc, sh = rnd((C,), 63, "s").abs().to(dev) + 0.1, rnd((C,), 64, "h").to(dev)
+    a = ops.Act(y, sc, sh)
+    w = rnd((nc, C), 65, "w", 0.1).to(dev)
+    dh = rnd((B * H * W, nc), 66, "dh").to(dev)
+    base = nhwc(rnd((B, C, H, W), 67, "base")).to(dev)
+    res = []
+    for fused in (True, False):
+        da = base.clone()
+        dw, db = torch.empty(nc, C, device=dev), torch.empty(nc, device=dev)
+        part = ops.head_bwd(a, w, dh, dw, db, da, acc, bnb=(mean, invstd) if fused else None)
+        dy = torch.empty_like(da)
+        dg, dbt, dcb = (torch.empty(C, device=dev) for _ in range(3))
+        ops.bn_relu_bwd(da, y, mean, invstd, sc, sh, dy, dg, dbt, dcb, part=part)
+        res.append((da.cpu(), dw.cpu(), db.cpu(), dy.cpu(), dg.cpu(), dbt.cpu()))
+    assert all(torch.equal(x_, y_) for x_, y_ in zip(res[0][:3], res[1][:3]))
+    for name, a_, b_ in zip(("dy", "dgamma", "dbeta"), res[0][3:], res[1][3:]):
+        close(a_, b_, 1e-5, f"head-fused partials: {name}")
+
+
 def test_bn_eval_params_cache(dev):
     """Eval-mode BN (scale, shift) cached on the module: reused while gamma, beta and the
     running stats are unchanged, recomputed after any in-place write (torch ops, the

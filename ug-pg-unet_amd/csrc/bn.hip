@@ -340,6 +340,11 @@ void launch_bn_bwd_reduce(const float* da, const float* y, int64_t npix, int C, 
 }
 }  // namespace ugpg
 
+extern "C" int ugpg_bnb_slots(int64_t npix, int C) {
+    if (npix <= 0 || C <= 0 || C % 4 || C > 1024) return 0;
+    return bwd_plan(npix, C).nblk;
+}
+
 extern "C" size_t ugpg_bn_relu_bwd_partials_workspace(int C) {
     return C > 0 ? (size_t)2 * C * sizeof(float) : 0;
 }

@@ -113,4 +113,66 @@ __device__ __forceinline__ void ac_index(int o, int in, int out, int& i0, int& i
     l0 = 1.0f - l1;
 }
 
+// BatchNorm-backward partials folded into the kernel that produces da = dL/d(relu(bn(y)))
+// (ugpg_bnb_t): g = da*[scale*y+shift > 0], xhat = (y-mean)*invstd, per block and
+// channel sum g, sum g*xhat, sum xhat -> part[3][C][nblk] (the layout of bn.hip's
+// bn_bwd_reduce_kernel, finalized by ugpg_bn_relu_bwd_partials).  Thread layout of that
+// kernel: C/4 threads per pixel (4 channels each), 256/(C/4) pixel slots per block.
+struct BnbArgs {
+    const float* y;
+    const float* mean;
+    const float* invstd;
+    const float* scale;
+    const float* shift;
+    float* part;
+    int nblk;
+    int64_t ppb;  // pixels per block
+};
+struct BnbAcc {
+    f32x4 mu, is, sc, sh, sg, sgx, sx;
+    __device__ void init(const BnbArgs& b, int c) {
+        mu = *reinterpret_cast<const f32x4*>(b.mean + c);
+        is = *reinterpret_cast<const f32x4*>(b.invstd + c);
+        sc = *reinterpret_cast<const f32x4*>(b.scale + c);
+        sh = *reinterpret_cast<const f32x4*>(b.shift + c);
+        sg = sgx = sx = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    __device__ void add(f32x4 d, f32x4 v) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float g = fmaf(v[k], sc[k], sh[k]) > 0.f ? d[k] : 0.f;
+            const float xh = (v[k] - mu[k]) * is[k];
+            sg[k] += g;
+            sgx[k] = fmaf(g, xh, sgx[k]);
+            sx[k] += xh;
+        }
+    }
+    // block reduction over the pixel slots (fixed order) and the partial write; every
+    // thread of the block calls it (LDS: 3 x 256 f32x4)
+    __device__ void write(const BnbArgs& b, int C) {
+        __shared__ f32x4 rs[256], rq[256], rx[256];
+        const int tid = threadIdx.x, c4n = C / 4, slots = 256 / c4n;
+        const int q = tid % c4n, slot = tid / c4n;
+        rs[tid] = sg;
+        rq[tid] = sgx;
+        rx[tid] = sx;
+        __syncthreads();
+        if (slot == 0) {
+            f32x4 a = sg, g2 = sgx, x = sx;
+            for (int s2 = 1; s2 < slots; ++s2) {
+                a += rs[s2 * c4n + q];
+                g2 += rq[s2 * c4n + q];
+                x += rx[s2 * c4n + q];
+            }
+            const int c = 4 * q;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                b.part[(size_t)(c + k) * b.nblk + blockIdx.x] = a[k];
+                b.part[((size_t)C + c + k) * b.nblk + blockIdx.x] = g2[k];
+                b.part[((size_t)2 * C + c + k) * b.nblk + blockIdx.x] = x[k];
+            }
+        }
+    }
+};
+
 }  // namespace ugpg

@@ -76,6 +76,44 @@ __global__ void maxpool2_bwd_kernel(const float* dout, const uint8_t* am, int B,
     }
 }
 
+// maxpool backward fused with the BatchNorm-backward partials of its output (the BN of
+// the block whose activation was pooled: this gather is the last writer of its da).
+// Block = a contiguous pixel range, thread = 4 channels of every slots-th pixel.
+__global__ void __launch_bounds__(256)
+    maxpool2_bwd_bnb_kernel(const float* dout, const uint8_t* am, int B, int H, int W, int C,
+                            float* din, int acc, BnbArgs bnb) {
+    const int Ho = H / 2, Wo = W / 2, c4n = C / 4, slots = 256 / c4n;
+    const int tid = threadIdx.x, q = tid % c4n, slot = tid / c4n, c = 4 * q;
+    const int64_t npix = (int64_t)B * H * W;
+    BnbAcc st;
+    st.init(bnb, c);
+    if (slot < slots) {
+        const int64_t p0 = blockIdx.x * bnb.ppb, p1 = min(npix, p0 + bnb.ppb);
+        for (int64_t p = p0 + slot; p < p1; p += slots) {
+            const int x = (int)(p % W);
+            const int64_t r = p / W;
+            const int yy = (int)(r % H), b = (int)(r / H);
+            const int oy = yy >> 1, ox = x >> 1;
+            f32x4 g = {0.f, 0.f, 0.f, 0.f};
+            if (oy < Ho && ox < Wo) {
+                const int k = (yy & 1) * 2 + (x & 1);
+                const size_t o = ((size_t)(b * Ho + oy) * Wo + ox) * C + c;
+                const f32x4 d = *reinterpret_cast<const f32x4*>(dout + o);
+                const uchar4 m = *reinterpret_cast<const uchar4*>(am + o);
+                g[0] = m.x == k ? d[0] : 0.f;
+                g[1] = m.y == k ? d[1] : 0.f;
+                g[2] = m.z == k ? d[2] : 0.f;
+                g[3] = m.w == k ? d[3] : 0.f;
+            }
+            f32x4* dst = reinterpret_cast<f32x4*>(din + p * C + c);
+            if (acc) g += *dst;
+            *dst = g;
+            st.add(g, *reinterpret_cast<const f32x4*>(bnb.y + p * C + c));
+        }
+    }
+    st.write(bnb, C);
+}
+
 // ------------------------------------------------- bilinear (align_corners)
 // gather-form backward: input index i collects from outputs o with i0(o)==i or i1(o)==i
 __device__ __forceinline__ void ac_range(int i, int in, int out, int& lo, int& hi) {
@@ -476,13 +514,20 @@ __global__ void __launch_bounds__(256) head_split_bwd_kernel(const float* dl, in
 // da (+)= dh @ w ; per-block partials of dW = dh^T act and db = sum dh.  Compile-time
 // class count NC and 64-channel slices CJ keep the accumulators in registers (runtime
 // bounds put them in scratch); two pixels per iteration keep 2x the loads in flight.
-template <int NC, int CJ>
+// BNB: also the BatchNorm-backward partials of da (x is that BatchNorm's input y and
+// (sc, sh) its affine, already loaded here: the fusion costs no memory traffic); same
+// block plan, so nslots = the block count (ugpg_head_bwd_bnb_slots).
+template <int NC, int CJ, bool BNB>
 __global__ void __launch_bounds__(256) head_bwd_kernel(const float* x, const float* sc,
                                                        const float* sh, int64_t npix, int C,
                                                        const float* w, int nc, const float* dh,
                                                        float* da, int acc_da, int64_t ppb,
-                                                       float* part, int nblk) {
+                                                       float* part, int nblk, BnbArgs bnb) {
     const int tid = threadIdx.x, l16 = tid & 15, slot = tid >> 4;
+    BnbAcc bacc[BNB ? CJ : 1];
+    if constexpr (BNB)
+#pragma unroll
+        for (int j = 0; j < CJ; ++j) bacc[j].init(bnb, l16 * 4 + 64 * j);
     f32x4 gw[NC][CJ];
     float gb[NC];
 #pragma unroll
@@ -512,6 +557,7 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(const float* x, const flo
             f32x4* dst = reinterpret_cast<f32x4*>(da + p * C + c);
             if (acc_da) g += *dst;
             *dst = g;
+            if constexpr (BNB) bacc[j].add(g, xv[j]);
         }
         if (l16 == 0)
 #pragma unroll
@@ -565,6 +611,33 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(const float* x, const flo
                     float sb = 0.f;
                     for (int q = 0; q < 16; ++q) sb += redb[q];
                     part[((size_t)blockIdx.x * NC + k) * (C + 1) + C] = sb;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    if constexpr (BNB) {
+        // BatchNorm-backward partials: per 64-channel slice, the 16 pixel slots in order
+        __shared__ f32x4 rb[3][256];
+#pragma unroll
+        for (int j = 0; j < CJ; ++j) {
+            rb[0][tid] = bacc[j].sg;
+            rb[1][tid] = bacc[j].sgx;
+            rb[2][tid] = bacc[j].sx;
+            __syncthreads();
+            if (slot == 0) {
+                f32x4 a0 = rb[0][l16], a1 = rb[1][l16], a2 = rb[2][l16];
+                for (int q = 1; q < 16; ++q) {
+                    a0 += rb[0][q * 16 + l16];
+                    a1 += rb[1][q * 16 + l16];
+                    a2 += rb[2][q * 16 + l16];
+                }
+                const int c = l16 * 4 + 64 * j;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    bnb.part[(size_t)(c + k) * nblk + blockIdx.x] = a0[k];
+                    bnb.part[((size_t)C + c + k) * nblk + blockIdx.x] = a1[k];
+                    bnb.part[((size_t)2 * C + c + k) * nblk + blockIdx.x] = a2[k];
                 }
             }
             __syncthreads();
@@ -1117,6 +1190,33 @@ extern "C" int ugpg_maxpool2_bwd(const float* dout, const uint8_t* am, int B, in
     return check_launch("maxpool2_bwd");
 }
 
+static bool bnb_args(const ugpg_bnb_t* d, int64_t npix, int C, BnbArgs& b) {
+    if (!d || !d->y || !d->mean || !d->invstd || !d->scale || !d->shift || !d->part ||
+        d->nslots != ugpg_bnb_slots(npix, C) || C % 4 || C > 1024)
+        return false;
+    b.y = d->y;
+    b.mean = d->mean;
+    b.invstd = d->invstd;
+    b.scale = d->scale;
+    b.shift = d->shift;
+    b.part = d->part;
+    b.nblk = d->nslots;
+    b.ppb = cdiv(npix, (int64_t)d->nslots);
+    return true;
+}
+
+extern "C" int ugpg_maxpool2_bwd_bnb(const float* dout, const uint8_t* am, int B, int H, int W,
+                                     int C, float* din, int acc, const ugpg_bnb_t* bnb,
+                                     void* stream) {
+    BnbArgs b;
+    UGPG_REQUIRE(dout && am && din && B > 0 && H > 0 && W > 0 &&
+                     bnb_args(bnb, (int64_t)B * H * W, C, b),
+                 "maxpool2_bwd_bnb");
+    hipLaunchKernelGGL(maxpool2_bwd_bnb_kernel, dim3(b.nblk), dim3(256), 0, as_stream(stream),
+                       dout, am, B, H, W, C, din, acc, b);
+    return check_launch("maxpool2_bwd_bnb");
+}
+
 extern "C" int ugpg_bilinear_nhwc_fwd(ugpg_src_t s, int B, int Hi, int Wi, float* out, int Ho,
                                       int Wo, void* stream) {
     UGPG_REQUIRE(s.data && out && s.C % 4 == 0 && Ho > 0 && Wo > 0, "bilinear_nhwc_fwd");
@@ -1221,12 +1321,47 @@ extern "C" size_t ugpg_head_bwd_workspace(int64_t npix, int C, int nc) {
     return (size_t)nblk * nc * (C + 1) * sizeof(float);
 }
 
+extern "C" int ugpg_head_bwd_bnb_slots(int64_t npix) {
+    int64_t ppb;
+    return npix > 0 ? head_nblk(npix, ppb) : 0;
+}
+
+static int head_bwd_common(ugpg_src_t s, int64_t npix, const float* w, int nc, const float* dh,
+                           float* dw, float* db, float* da, int acc_da, void* ws,
+                           size_t ws_bytes, const ugpg_bnb_t* bnbd, void* stream);
+
 extern "C" int ugpg_head_bwd(ugpg_src_t s, int64_t npix, const float* w, int nc, const float* dh,
                              float* dw, float* db, float* da, int acc_da, void* ws,
                              size_t ws_bytes, void* stream) {
+    return head_bwd_common(s, npix, w, nc, dh, dw, db, da, acc_da, ws, ws_bytes, nullptr, stream);
+}
+
+extern "C" int ugpg_head_bwd_bnb(ugpg_src_t s, int64_t npix, const float* w, int nc,
+                                 const float* dh, float* dw, float* db, float* da, int acc_da,
+                                 void* ws, size_t ws_bytes, const ugpg_bnb_t* bnb, void* stream) {
+    UGPG_REQUIRE(bnb && bnb->y == s.data && s.scale && bnb->nslots == ugpg_head_bwd_bnb_slots(npix),
+                 "head_bwd_bnb");
+    return head_bwd_common(s, npix, w, nc, dh, dw, db, da, acc_da, ws, ws_bytes, bnb, stream);
+}
+
+static int head_bwd_common(ugpg_src_t s, int64_t npix, const float* w, int nc, const float* dh,
+                           float* dw, float* db, float* da, int acc_da, void* ws,
+                           size_t ws_bytes, const ugpg_bnb_t* bnbd, void* stream) {
     UGPG_REQUIRE(s.data && w && dh && dw && da && s.C % 64 == 0 && s.C <= 64 * HEAD_CJ_MAX &&
                      nc >= 1 && nc <= HEAD_NC_MAX,
                  "head_bwd");
+    BnbArgs bnb{};
+    if (bnbd) {
+        UGPG_REQUIRE(bnbd->mean && bnbd->invstd && bnbd->scale && bnbd->shift && bnbd->part,
+                     "head_bwd_bnb");
+        bnb.y = bnbd->y;
+        bnb.mean = bnbd->mean;
+        bnb.invstd = bnbd->invstd;
+        bnb.scale = bnbd->scale;
+        bnb.shift = bnbd->shift;
+        bnb.part = bnbd->part;
+        bnb.nblk = bnbd->nslots;
+    }
     const size_t need = ugpg_head_bwd_workspace(npix, s.C, nc);
     if (!ws || ws_bytes < need) {
         set_error("head_bwd: workspace %zu < %zu", ws_bytes, need);
@@ -1236,15 +1371,21 @@ extern "C" int ugpg_head_bwd(ugpg_src_t s, int64_t npix, const float* w, int nc,
     const int nblk = head_nblk(npix, ppb);
     hipStream_t st = as_stream(stream);
     using K = void (*)(const float*, const float*, const float*, int64_t, int, const float*, int,
-                       const float*, float*, int, int64_t, float*, int);
-    static const K table[HEAD_NC_MAX][HEAD_CJ_MAX] = {
-        {head_bwd_kernel<1, 1>, head_bwd_kernel<1, 2>, head_bwd_kernel<1, 3>, head_bwd_kernel<1, 4>},
-        {head_bwd_kernel<2, 1>, head_bwd_kernel<2, 2>, head_bwd_kernel<2, 3>, head_bwd_kernel<2, 4>},
-        {head_bwd_kernel<3, 1>, head_bwd_kernel<3, 2>, head_bwd_kernel<3, 3>, head_bwd_kernel<3, 4>},
-        {head_bwd_kernel<4, 1>, head_bwd_kernel<4, 2>, head_bwd_kernel<4, 3>, head_bwd_kernel<4, 4>}};
-    hipLaunchKernelGGL(table[nc - 1][s.C / 64 - 1], dim3(nblk), dim3(256), 0, st, s.data, s.scale,
-                       s.shift, npix, s.C, w, nc, dh, da, acc_da, ppb, static_cast<float*>(ws),
-                       nblk);
+                       const float*, float*, int, int64_t, float*, int, BnbArgs);
+#define HB(B_)                                                                              \
+    {{head_bwd_kernel<1, 1, B_>, head_bwd_kernel<1, 2, B_>, head_bwd_kernel<1, 3, B_>,     \
+      head_bwd_kernel<1, 4, B_>},                                                          \
+     {head_bwd_kernel<2, 1, B_>, head_bwd_kernel<2, 2, B_>, head_bwd_kernel<2, 3, B_>,     \
+      head_bwd_kernel<2, 4, B_>},                                                          \
+     {head_bwd_kernel<3, 1, B_>, head_bwd_kernel<3, 2, B_>, head_bwd_kernel<3, 3, B_>,     \
+      head_bwd_kernel<3, 4, B_>},                                                          \
+     {head_bwd_kernel<4, 1, B_>, head_bwd_kernel<4, 2, B_>, head_bwd_kernel<4, 3, B_>,     \
+      head_bwd_kernel<4, 4, B_>}}
+    static const K table[2][HEAD_NC_MAX][HEAD_CJ_MAX] = {HB(false), HB(true)};
+#undef HB
+    hipLaunchKernelGGL(table[bnbd ? 1 : 0][nc - 1][s.C / 64 - 1], dim3(nblk), dim3(256), 0, st,
+                       s.data, s.scale, s.shift, npix, s.C, w, nc, dh, da, acc_da, ppb,
+                       static_cast<float*>(ws), nblk, bnb);
     if (int e = check_launch("head_bwd")) return e;
     hipLaunchKernelGGL(head_bwd_finalize_kernel, dim3((unsigned)cdiv(nc * (s.C + 1), 64)), dim3(1024), 0,
                        st, static_cast<const float*>(ws), nblk, nc, s.C, dw, db);

@@ -29,6 +29,12 @@ class ConvDesc(C.Structure):
                 ("bnb_invstd", _p), ("bnb_scale", _p), ("bnb_shift", _p), ("bnb_part", _p)]
 
 
+class Bnb(C.Structure):
+    """ugpg_bnb_t."""
+    _fields_ = [("y", _p), ("mean", _p), ("invstd", _p), ("scale", _p), ("shift", _p),
+                ("part", _p), ("nslots", _i)]
+
+
 class PackItem(C.Structure):
     """ugpg_pack_item_t."""
     _fields_ = [("w", _p), ("wpk", _p), ("Cout", _i), ("Cin", _i), ("Cin_pad", _i), ("mode", _i)]
@@ -62,6 +68,8 @@ SIGNATURES = {
     "ugpg_bn_relu_apply": (_i, [Src, _i64, _p, _p]),
     "ugpg_maxpool2_fwd": (_i, [Src, _i, _i, _i, _p, _p, _p]),
     "ugpg_maxpool2_bwd": (_i, [_p, _p, _i, _i, _i, _i, _p, _i, _p]),
+    "ugpg_maxpool2_bwd_bnb": (_i, [_p, _p, _i, _i, _i, _i, _p, _i, C.POINTER(Bnb), _p]),
+    "ugpg_bnb_slots": (_i, [_i64, _i]),
     "ugpg_bilinear_nhwc_fwd": (_i, [Src, _i, _i, _i, _p, _i, _i, _p]),
     "ugpg_bilinear_nhwc_bwd": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _i, _p]),
     "ugpg_resize_nchw": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _i, _p]),
@@ -73,6 +81,8 @@ SIGNATURES = {
     "ugpg_heads_split_bwd": (_i, [_p, _i, _i, _i, _i, _p, _p, _i, _p]),
     "ugpg_head_bwd_workspace": (_sz, [_i64, _i, _i]),
     "ugpg_head_bwd": (_i, [Src, _i64, _p, _i, _p, _p, _p, _p, _i, _p, _sz, _p]),
+    "ugpg_head_bwd_bnb_slots": (_i, [_i64]),
+    "ugpg_head_bwd_bnb": (_i, [Src, _i64, _p, _i, _p, _p, _p, _p, _i, _p, _sz, C.POINTER(Bnb), _p]),
     "ugpg_ug_loss_workspace": (_sz, [_i64]),
     "ugpg_ug_loss_fwd": (_i, [_p, _p, _p, _i, _i, _i, _i, _p, _f, _p, _p, _sz, _p]),
     "ugpg_ug_loss_bwd": (_i, [_p, _p, _p, _i, _i, _i, _i, _p, _f, _p, _p, _p]),

@@ -53,6 +53,7 @@ class BlockCtx:
     y2: torch.Tensor = None
     st2: tuple = None
     extra: dict = field(default_factory=dict)
+    part2: torch.Tensor = None  # BN2-backward partials written by the last producer of da2
 
 
 def _conv_bn(seq):
@@ -134,7 +135,7 @@ def double_conv_backward(mod, ctx: BlockCtx, da2, targets, acc_flags, grads, pad
     B, H, W, cout = ctx.y2.shape
     a1 = Act(ctx.y1, ctx.st1[2], ctx.st1[3])
     # stage 2: BN2/ReLU backward, wgrad(conv2), dgrad(conv2) -> dL/d(a1)
-    _bn_relu_wgrad(c2, b2, ctx.y2, ctx.st2, [a1], da2, grads)
+    _bn_relu_wgrad(c2, b2, ctx.y2, ctx.st2, [a1], da2, grads, part=ctx.part2)
     cmid = c2.weight.shape[1]
     da1 = ops.empty(B, H, W, cmid, like=da2)
     npix = B * H * W
@@ -263,9 +264,23 @@ class UNetGraph:
         outs, ctxs = state["outs"], state["ctxs"]
         nb = len(self.blocks)
         da = [None] * nb
+        # the backward walks heads, then blocks in reverse: a block's output gradient is
+        # final after its lowest-indexed block consumer (or, with none, its last head),
+        # which may then also reduce the block's BN2 backward sums
+        first_use = {}
+        for bi, blk in enumerate(self.blocks):
+            for src in blk.inputs:
+                first_use.setdefault(src, bi)
+        last_head = {hd.block: i for i, hd in enumerate(self.heads)}
+
+        def bn2_state(src, bi):
+            c = ctxs[src]
+            if not _FUSE_BN_BWD or first_use.get(src) != bi or c.st2 is None or c.st2[0] is None:
+                return None
+            return (c.y2, *c.st2)
         if self.heads:
             dhs = ops.heads_split_bwd(dlogits.contiguous(), state["hres"])
-            for hd, dh in zip(self.heads, dhs):
+            for hi, (hd, dh) in enumerate(zip(self.heads, dhs)):
                 conv = hd.mod.conv
                 w = conv.weight.detach().reshape(conv.weight.shape[0], -1).contiguous()
                 a = outs[hd.block]
@@ -275,7 +290,13 @@ class UNetGraph:
                 dw = grads.get(conv.weight)
                 dw_flat = dw.view(w.shape) if dw is not None else torch.empty_like(w)
                 db = grads.get(conv.bias)
-                ops.head_bwd(a, w, dh.contiguous(), dw_flat, db, da[hd.block], acc)
+                c = ctxs[hd.block]
+                fuse = (_FUSE_BN_BWD and hd.block not in first_use and last_head[hd.block] == hi
+                        and c.st2 is not None and c.st2[0] is not None and a.y is c.y2)
+                part = ops.head_bwd(a, w, dh.contiguous(), dw_flat, db, da[hd.block], acc,
+                                    bnb=c.st2[:2] if fuse else None)
+                if part is not None:
+                    c.part2 = part
             if on_done is not None:
                 on_done([grads.get(p) for hd in self.heads for p in hd.mod.parameters()])
         else:
@@ -301,7 +322,10 @@ class UNetGraph:
                 acc = da[src] is not None
                 if not acc:
                     da[src] = torch.empty_like(outs[src].y)
-                ops.maxpool2_bwd(dp, ctx.extra["argmax"], H, W, da[src], acc)
+                st = bn2_state(src, bi)
+                part = ops.maxpool2_bwd(dp, ctx.extra["argmax"], H, W, da[src], acc, bnb=st)
+                if part is not None:
+                    ctxs[src].part2 = part
             else:
                 skip, low = blk.inputs
                 acc_s = da[skip] is not None

@@ -11,7 +11,7 @@ import os
 
 import torch
 
-from ._C import ConvDesc, PackItem, Src, WgradDesc, check, lib
+from ._C import Bnb, ConvDesc, PackItem, Src, WgradDesc, check, lib
 
 F32 = torch.float32
 
@@ -369,10 +369,31 @@ def maxpool2_fwd(a: Act):
     return out, am
 
 
-def maxpool2_bwd(dout, am, H, W, din, accumulate):
+def bnb_desc(bn_state, npix, c, like):
+    """(ugpg_bnb_t, partials tensor) for a kernel that last writes da of relu(bn(y)):
+    bn_state = (y, mean, invstd, scale, shift)."""
+    n = lib.ugpg_bnb_slots(npix, c)
+    if n <= 0:
+        raise ValueError(f"no BatchNorm-backward partials for C={c}")
+    part = empty(3 * c * n, like=like)
+    d = Bnb()
+    d.y, d.mean, d.invstd, d.scale, d.shift = (ptr(t) for t in bn_state)
+    d.part, d.nslots = ptr(part), n
+    return d, part
+
+
+def maxpool2_bwd(dout, am, H, W, din, accumulate, bnb=None):
+    """bnb: (y, mean, invstd, scale, shift) of the BatchNorm whose output was pooled ->
+    also returns its backward partials (for bn_relu_bwd(part=...))."""
     B, _, _, c = dout.shape
+    if bnb is not None:
+        d, part = bnb_desc(bnb, B * H * W, c, din)
+        check(lib.ugpg_maxpool2_bwd_bnb(ptr(dout), ptr(am), B, H, W, c, ptr(din), int(accumulate),
+                                        C.byref(d), stream()), "maxpool2_bwd_bnb")
+        return part
     check(lib.ugpg_maxpool2_bwd(ptr(dout), ptr(am), B, H, W, c, ptr(din), int(accumulate),
                                 stream()), "maxpool2_bwd")
+    return None
 
 
 def bilinear_nhwc_fwd(a: Act, Ho, Wo):
@@ -457,13 +478,26 @@ def heads_split_bwd(dlogits, hres):
     return dhs
 
 
-def head_bwd(a: Act, w, dh, dw, db, da, accumulate):
+def head_bwd(a: Act, w, dh, dw, db, da, accumulate, bnb=None):
+    """bnb: (mean, invstd) of the BatchNorm behind `a` (its scale/shift are a's) -> also
+    returns the BatchNorm-backward partials of da (for bn_relu_bwd(part=...))."""
     B, H, W, c = a.shape
     nc = w.shape[0]
     npix = B * H * W
     ws = workspace(lib.ugpg_head_bwd_workspace(npix, c, nc), dh.device)
+    if bnb is not None:
+        n = lib.ugpg_head_bwd_bnb_slots(npix)
+        part = empty(3 * c * n, like=da)
+        d = Bnb()
+        d.y, d.mean, d.invstd, d.scale, d.shift = (ptr(t) for t in (a.y, *bnb, a.scale, a.shift))
+        d.part, d.nslots = ptr(part), n
+        check(lib.ugpg_head_bwd_bnb(a.src(), npix, _f32(w), nc, ptr(dh), ptr(dw), ptr(db),
+                                    ptr(da), int(accumulate), ptr(ws), ws.numel(), C.byref(d),
+                                    stream()), "head_bwd_bnb")
+        return part
     check(lib.ugpg_head_bwd(a.src(), npix, _f32(w), nc, ptr(dh), ptr(dw), ptr(db), ptr(da),
                             int(accumulate), ptr(ws), ws.numel(), stream()), "head_bwd")
+    return None
 
 
 # ------------------------------------------------------------------ loss / metrics
