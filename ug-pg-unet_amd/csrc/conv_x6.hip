@@ -743,10 +743,12 @@ template <int NP, bool M16, int TWT = 32, int NCW = 4, int THT = 256 / TWT>
 __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) {
     static_assert(!M16 || NP == 3, "the 16x16x32 form pairs the split-bf16 products");
     static_assert(TWT == 32 || (M16 && TWT == 16), "16-wide tiles only in the 16x16x32 form");
-    static_assert(THT * TWT == 256 || (M16 && THT * TWT == 128), "256- or 128-pixel items");
+    static_assert(THT * TWT == 256 || (M16 && THT * TWT == 128) || (!M16 && THT * TWT == 512),
+                  "256-pixel items; 128 (16x16x32 form) or 512 (32x32x16 form) pixels");
     static_assert(NCW == 4 || (NCW == 8 && M16), "two compute waves per SIMD: 16x16x32 form only");
     // 256-pixel items: 8 x 32 (images >= 32 wide) or 16 x 16 (16-31 wide, 16x16x32 form)
-    constexpr int TW = TWT, TH = THT, BN = 64, BKC = 16, MT = 4;
+    // MT: 32-pixel image rows per compute wave in the 32x32x16 form (two pixel halves)
+    constexpr int TW = TWT, TH = THT, BN = 64, BKC = 16, MT = TH / 2;
     constexpr int HWD = TW + 2, HS = HWD;
     constexpr int NHALO = (TH + 2) * HWD;                   // 340 / 324 halo pixels
     // spare slot NHALO; plane pitch 348 = 4 (mod 8) for the 32x32 fragment pattern, 352
@@ -1150,6 +1152,34 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
     Pos cp = pos_of(item0);
     for (int k = 0; k < total; ++k) {
         const u32x4* Ac = smem + (k & 1) * A_VECS;
+        if constexpr (MT > 4) {
+            // 512-pixel items (single piece): one A fragment set, each m-tile's next-tap
+            // fragment read right after its MFMA (registers: 8 accumulator blocks)
+            static_assert(NP == 1, "512-pixel items: single-piece form only");
+            u32x4 fa[MT][NP], fb[2][NP];
+            ldfrag(Ac, Bring + ((3 * k) % NSLOT) * R_STR, 0, 0, fa, fb[0]);
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                const int ky1 = (t + 1) / 3, kx1 = (t + 1) % 3;
+                const u32x4* Bn = Bring + ((3 * k + ky1) % NSLOT) * R_STR;
+                if (t + 1 < 9) fb[(t + 1) & 1][0] = Bn[boff + kx1 * BN];
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt) {
+                    acc[mt] = mfma_xn<NP>(fa[mt], fb[t & 1], acc[mt]);
+                    if (t + 1 < 9) fa[mt][0] = Ac[aoff + (mt + ky1) * HS + kx1];
+                }
+#pragma unroll
+                for (int i = 0; i < MT; ++i) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+                    if (t + 1 < 9) {
+                        if (i == 0) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                        else __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                if (t % 3 == 2) read_barrier();
+            }
+        } else {
         u32x4 fa[2][MT][NP], fb[2][NP];
         ldfrag(Ac, Bring + ((3 * k) % NSLOT) * R_STR, 0, 0, fa[0], fb[0]);
 #pragma unroll
@@ -1174,6 +1204,7 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
             }
             __builtin_amdgcn_sched_barrier(0);  // taps do not mix
             if (t % 3 == 2) read_barrier();
+        }
         }
         if (++cc == nchunk) {
             x6_epilogue_wave<TH, TW, MT>(a, acc, cp.tile, cp.b, cp.ty0, cp.tx0, cp.nb * BN, wm, wn);
@@ -1944,11 +1975,18 @@ int g_x6_pipe = X6_PIPE_DEFAULT;   // tuning knob "x6_pipe" (see launch_fwd_x6)
 // down4 of S4).
 // x6_pipe = 4: 8 x 16-pixel (128-pixel) items for 16 <= W < 32, so that bs16's 16-wide
 // layers have 256 items for 256 CUs.
+// single-piece (bf16) persistent form: X6R_NP1_TH = 16 gives 16 x 32 = 512-pixel items
+// (x 64 channels), halving the weight bytes staged per MFMA of that loader-bound form;
+// measured 4 % slower over the Stage-4 layers (its 8-block epilogue spills), so 8
+#ifndef X6R_NP1_TH
+#define X6R_NP1_TH 8
+#endif
 static bool use_x6r(int W, int np) {
     return g_x6_pipe && (W >= 32 || (g_x6_pipe >= 3 && np == 3 && W >= 16));
 }
 int fwd_x6_tile_w(int W, int np) { return W >= 32 ? 32 : 16; }
 int fwd_x6_tile_h(int W, int np) {
+    if (use_x6r(W, np) && np == 1 && W >= 32) return X6R_NP1_TH;
     if (use_x6r(W, np)) return W >= 32 ? 8 : (g_x6_pipe == 4 ? 8 : 16);
     return W >= 32 ? 4 : 8;
 }
@@ -2279,6 +2317,9 @@ bool launch_fwd_x6(const ConvFwdArgs& a_in, int np, hipStream_t st) {
         else if (np == 3)
             hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<3, false>), dim3((unsigned)g), dim3(512), 0,
                                st, a);
+        else if (X6R_NP1_TH == 16)
+            hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 4, 16>), dim3((unsigned)g),
+                               dim3(512), 0, st, a);
         else
             hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false>), dim3((unsigned)g), dim3(512), 0,
                                st, a);
