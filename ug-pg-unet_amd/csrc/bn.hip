@@ -23,34 +23,53 @@ __global__ void bn_finalize_kernel(const float* __restrict__ stats, int ntiles, 
     // no cancellation): with e_t = sum_t - n_t K,  m = K + sum e_t / N  and
     // M2 = sum M2_t + sum e_t^2 / n_t - (sum e_t)^2 / N.  1024 threads per channel.
     const int c = blockIdx.x;
-    __shared__ double sn[1024], se[1024], sq[1024];
+    __shared__ double sn[16], se[16], sq[16];
     const float* cnt = stats + (size_t)c * ntiles;
     const float* sum = stats + ((size_t)C + c) * ntiles;
     const float* m2 = stats + ((size_t)2 * C + c) * ntiles;
+    // this thread's first 8 tiles' partials are loaded together with the shift tile
+    // (latency: the kernel is a few load round trips long)
+    constexpr int PF = 8;
+    float pc[PF], ps[PF], pm[PF];
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+        const int t = threadIdx.x + u * blockDim.x;
+        const bool ok = t < ntiles;
+        pc[u] = ok ? cnt[t] : 0.f;
+        ps[u] = ok ? sum[t] : 0.f;
+        pm[u] = ok ? m2[t] : 0.f;
+    }
     int t0 = 0;
     while (t0 < ntiles && !(cnt[t0] > 0.f)) ++t0;  // uniform: the first tile is normally full
     const double K = t0 < ntiles ? (double)sum[t0] / (double)cnt[t0] : 0.0;
     double n = 0, E = 0, M = 0;
-    for (int t = threadIdx.x; t < ntiles; t += blockDim.x) {
-        const float nb = cnt[t];
-        if (nb <= 0.f) continue;
-        const double e = (double)sum[t] - (double)nb * K;
+    auto one = [&](float nb, float sm, float mm) {
+        if (nb <= 0.f) return;
+        const double e = (double)sm - (double)nb * K;
         n += nb;
         E += e;
-        M += (double)m2[t] + e * e * (double)(1.0f / nb);
+        M += (double)mm + e * e * (double)(1.0f / nb);
+    };
+#pragma unroll
+    for (int u = 0; u < PF; ++u) one(pc[u], ps[u], pm[u]);
+    for (int t = threadIdx.x + PF * blockDim.x; t < ntiles; t += blockDim.x) one(cnt[t], sum[t], m2[t]);
+    // fixed-order reduction: wave shuffles, then the 16 wave sums in order by thread 0
+    n = wave_sum_d(n);
+    E = wave_sum_d(E);
+    M = wave_sum_d(M);
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        sn[wv] = n;
+        se[wv] = E;
+        sq[wv] = M;
     }
-    sn[threadIdx.x] = n;
-    se[threadIdx.x] = E;
-    sq[threadIdx.x] = M;
     __syncthreads();
-    for (int s2 = blockDim.x / 2; s2 > 0; s2 >>= 1) {
-        if (threadIdx.x < s2) {
-            sn[threadIdx.x] += sn[threadIdx.x + s2];
-            se[threadIdx.x] += se[threadIdx.x + s2];
-            sq[threadIdx.x] += sq[threadIdx.x + s2];
+    if (threadIdx.x == 0)
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+            sn[0] += sn[w];
+            se[0] += se[w];
+            sq[0] += sq[w];
         }
-        __syncthreads();
-    }
     const double Ntot = sn[0];
     const double mean = Ntot > 0 ? K + se[0] / Ntot : 0.0;
     if (threadIdx.x == 0 && Ntot > 0) sq[0] -= se[0] * se[0] / Ntot;
@@ -151,25 +170,47 @@ __global__ void bn_bwd_finalize_kernel(const float* part, int nblk, int C, int64
                                        const float* scale, float* dgamma, float* dbeta,
                                        float* dbias, int acc, float* coef) {
     const int c = blockIdx.x;
-    __shared__ double s1[256], s2[256], s3[256];
+    __shared__ double s1[4], s2[4], s3[4];
     double a = 0, b = 0, x = 0;
-    for (int i = threadIdx.x; i < nblk; i += blockDim.x) {
+    int i = threadIdx.x;
+    // four slots' loads in flight per thread (the kernel is a few load round trips long)
+    for (; i + 3 * (int)blockDim.x < nblk; i += 4 * blockDim.x) {
+        float va[4], vb[4], vx[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = i + u * blockDim.x;
+            va[u] = part[(size_t)c * nblk + j];
+            vb[u] = part[((size_t)C + c) * nblk + j];
+            vx[u] = part[((size_t)2 * C + c) * nblk + j];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            a += va[u];
+            b += vb[u];
+            x += vx[u];
+        }
+    }
+    for (; i < nblk; i += blockDim.x) {
         a += part[(size_t)c * nblk + i];
         b += part[((size_t)C + c) * nblk + i];
         x += part[((size_t)2 * C + c) * nblk + i];
     }
-    s1[threadIdx.x] = a;
-    s2[threadIdx.x] = b;
-    s3[threadIdx.x] = x;
-    __syncthreads();
-    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-        if (threadIdx.x < s) {
-            s1[threadIdx.x] += s1[threadIdx.x + s];
-            s2[threadIdx.x] += s2[threadIdx.x + s];
-            s3[threadIdx.x] += s3[threadIdx.x + s];
-        }
-        __syncthreads();
+    a = wave_sum_d(a);
+    b = wave_sum_d(b);
+    x = wave_sum_d(x);
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        s1[wv] = a;
+        s2[wv] = b;
+        s3[wv] = x;
     }
+    __syncthreads();
+    if (threadIdx.x == 0)
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+            s1[0] += s1[w];
+            s2[0] += s2[w];
+            s3[0] += s3[w];
+        }
     if (threadIdx.x == 0) {
         const float sg = (float)s1[0], sgx = (float)s2[0];
         if (dgamma) dgamma[c] = acc ? dgamma[c] + sgx : sgx;
