@@ -219,6 +219,10 @@ int ugpg_bilinear_nhwc_fwd(ugpg_src_t src, int B, int Hi, int Wi, float* out, in
                            void* stream);
 int ugpg_bilinear_nhwc_bwd(const float* dout, int B, int Ho, int Wo, int C, float* din, int Hi,
                            int Wi, int accumulate, void* stream);
+/* The same, also writing the BatchNorm-backward partials of din (see ugpg_bnb_t). */
+int ugpg_bilinear_nhwc_bwd_bnb(const float* dout, int B, int Ho, int Wo, int C, float* din,
+                               int Hi, int Wi, int accumulate, const ugpg_bnb_t* bnb,
+                               void* stream);
 
 /* ---- NCHW resize (F.interpolate at uncertainty_guided_trainer.py:208-209,
  * UG_unet.py:36-53, 419-424; K12/K13)

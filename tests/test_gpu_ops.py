@@ -359,6 +359,31 @@ def test_head_bwd_fused_bn_partials(dev, C, nc, acc):
         close(a_, b_, 1e-5, f"head-fused partials: {name}")
 
 
+@pytest.mark.parametrize("h,C,acc", [(16, 512, 0), (32, 256, 1), (13, 64, 1)])
+def test_bilinear_bwd_fused_bn_partials(dev, h, C, acc):
+    """bilinear_nhwc_bwd(bnb=...) writes a bit-identical din plus the BatchNorm-backward
+    partials that make bn_relu_bwd(part=...) equal the standalone reduction."""
+    from ugpg import ops
+    B, H = 2, 2 * h
+    dout = nhwc(rnd((B, C, H, H), 70, "du")).to(dev)
+    base = nhwc(rnd((B, C, h, h), 71, "base")).to(dev)
+    y = nhwc(rnd((B, C, h, h), 72, "y") * 2 + 0.3).to(dev)
+    st = [rnd((C,), 73 + i, f"s{i}").abs().to(dev) + 0.1 for i in range(4)]
+    st[3] = st[3] - 0.5
+    d1, d2 = base.clone(), base.clone()
+    part = ops.bilinear_nhwc_bwd(dout, h, h, d1, acc, bnb=(y, *st))
+    ops.bilinear_nhwc_bwd(dout, h, h, d2, acc)
+    assert torch.equal(d1, d2)
+    outs = []
+    for p in (part, None):
+        dy = torch.empty_like(d1)
+        dg, dbt, dcb = (torch.empty(C, device=dev) for _ in range(3))
+        ops.bn_relu_bwd(d1, y, *st, dy, dg, dbt, dcb, part=p)
+        outs.append((dy.cpu(), dg.cpu(), dbt.cpu()))
+    for name, a_, b_ in zip(("dy", "dgamma", "dbeta"), outs[0], outs[1]):
+        close(a_, b_, 1e-5, f"bilinear-fused partials: {name}")
+
+
 def test_bn_eval_params_cache(dev):
     """Eval-mode BN (scale, shift) cached on the module: reused while gamma, beta and the
     running stats are unchanged, recomputed after any in-place write (torch ops, the

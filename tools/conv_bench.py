@@ -21,8 +21,9 @@ def load_lib(path):
     import ctypes
     L = ctypes.CDLL(str(Path(path).resolve()))
     for name, (res, args) in _C.SIGNATURES.items():
-        fn = getattr(L, name)
-        fn.restype, fn.argtypes = res, args
+        fn = getattr(L, name, None)  # an older build may lack newer entries
+        if fn is not None:
+            fn.restype, fn.argtypes = res, args
     return L
 
 B = 16

@@ -297,6 +297,49 @@ __global__ void bilinear_nhwc_bwd_kernel(const float* dout, int B, int Ho, int W
     }
 }
 
+// bilinear backward fused with the BatchNorm-backward partials of din (the BN of the
+// block whose activation was upsampled: this gather is the last writer of its da).
+// Block = a contiguous range of input pixels, thread = 4 channels of every slots-th
+// pixel; each pixel gathers exactly the terms, in exactly the order, of
+// bilinear_nhwc_bwd_kernel (bit-identical din).
+__global__ void __launch_bounds__(256)
+    bilinear_nhwc_bwd_bnb_kernel(const float* dout, int B, int Ho, int Wo, int C, float* din,
+                                 int Hi, int Wi, int acc, BnbArgs bnb) {
+    const int c4n = C / 4, slots = 256 / c4n;
+    const int tid = threadIdx.x, q = tid % c4n, slot = tid / c4n, c = 4 * q;
+    const int64_t npix = (int64_t)B * Hi * Wi;
+    BnbAcc st;
+    st.init(bnb, c);
+    if (slot < slots) {
+        const int64_t p0 = blockIdx.x * bnb.ppb, p1 = min(npix, p0 + bnb.ppb);
+        for (int64_t p = p0 + slot; p < p1; p += slots) {
+            const int ix = (int)(p % Wi);
+            const int64_t r = p / Wi;
+            const int iy = (int)(r % Hi), b = (int)(r / Hi);
+            int ylo, yhi, xlo, xhi;
+            ac_range_tight(iy, Hi, Ho, ylo, yhi);
+            ac_range_tight(ix, Wi, Wo, xlo, xhi);
+            f32x4 s = {0.f, 0.f, 0.f, 0.f};
+            for (int oy = ylo; oy <= yhi; ++oy) {
+                const float wyk = ac_weight(oy, iy, Hi, Ho);
+                if (wyk == 0.f) continue;
+                for (int ox = xlo; ox <= xhi; ++ox) {
+                    const float wx = ac_weight(ox, ix, Wi, Wo);
+                    if (wx == 0.f) continue;
+                    const f32x4 d = *reinterpret_cast<const f32x4*>(
+                        dout + ((size_t)(b * Ho + oy) * Wo + ox) * C + c);
+                    s += (wyk * wx) * d;
+                }
+            }
+            f32x4* dst = reinterpret_cast<f32x4*>(din + p * C + c);
+            if (acc) s += *dst;
+            *dst = s;
+            st.add(s, *reinterpret_cast<const f32x4*>(bnb.y + p * C + c));
+        }
+    }
+    st.write(bnb, C);
+}
+
 // ------------------------------------------------------------- NCHW resize
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
@@ -1239,6 +1282,18 @@ extern "C" int ugpg_bilinear_nhwc_bwd(const float* dout, int B, int Ho, int Wo, 
     hipLaunchKernelGGL(bilinear_nhwc_bwd_kernel, dim3(gx, (unsigned)(B * Hi)), dim3(256), 0,
                        as_stream(stream), dout, B, Ho, Wo, C, din, Hi, Wi, acc);
     return check_launch("bilinear_nhwc_bwd");
+}
+
+extern "C" int ugpg_bilinear_nhwc_bwd_bnb(const float* dout, int B, int Ho, int Wo, int C,
+                                          float* din, int Hi, int Wi, int acc,
+                                          const ugpg_bnb_t* bnb, void* stream) {
+    BnbArgs b;
+    UGPG_REQUIRE(dout && din && B > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0 &&
+                     bnb_args(bnb, (int64_t)B * Hi * Wi, C, b),
+                 "bilinear_nhwc_bwd_bnb");
+    hipLaunchKernelGGL(bilinear_nhwc_bwd_bnb_kernel, dim3(b.nblk), dim3(256), 0,
+                       as_stream(stream), dout, B, Ho, Wo, C, din, Hi, Wi, acc, b);
+    return check_launch("bilinear_nhwc_bwd_bnb");
 }
 
 extern "C" int ugpg_resize_nchw(const float* in, int B, int C, int Hi, int Wi, float* out, int Ho,

@@ -72,6 +72,7 @@ SIGNATURES = {
     "ugpg_bnb_slots": (_i, [_i64, _i]),
     "ugpg_bilinear_nhwc_fwd": (_i, [Src, _i, _i, _i, _p, _i, _i, _p]),
     "ugpg_bilinear_nhwc_bwd": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _i, _p]),
+    "ugpg_bilinear_nhwc_bwd_bnb": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _i, C.POINTER(Bnb), _p]),
     "ugpg_resize_nchw": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _i, _p]),
     "ugpg_resize_nchw_bwd": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _p]),
     "ugpg_nchw_to_nhwc": (_i, [_p, _i, _i, _i, _i, _p, _i, _p]),

@@ -337,7 +337,9 @@ class UNetGraph:
                 acc_l = da[low] is not None
                 if not acc_l:
                     da[low] = torch.empty_like(outs[low].y)
-                ops.bilinear_nhwc_bwd(du, h, w, da[low], acc_l)
+                part = ops.bilinear_nhwc_bwd(du, h, w, da[low], acc_l, bnb=bn2_state(low, bi))
+                if part is not None:
+                    ctxs[low].part2 = part
             if on_done is not None:
                 on_done([grads.get(p) for p in blk.mod.parameters()])
             da[bi] = None

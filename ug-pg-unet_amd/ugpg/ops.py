@@ -404,10 +404,19 @@ def bilinear_nhwc_fwd(a: Act, Ho, Wo):
     return out
 
 
-def bilinear_nhwc_bwd(dout, Hi, Wi, din, accumulate):
+def bilinear_nhwc_bwd(dout, Hi, Wi, din, accumulate, bnb=None):
+    """bnb: (y, mean, invstd, scale, shift) of the BatchNorm whose output was upsampled
+    -> also returns its backward partials (for bn_relu_bwd(part=...))."""
     B, Ho, Wo, c = dout.shape
+    if bnb is not None:
+        d, part = bnb_desc(bnb, B * Hi * Wi, c, din)
+        check(lib.ugpg_bilinear_nhwc_bwd_bnb(ptr(dout), B, Ho, Wo, c, ptr(din), Hi, Wi,
+                                             int(accumulate), C.byref(d), stream()),
+              "bilinear_nhwc_bwd_bnb")
+        return part
     check(lib.ugpg_bilinear_nhwc_bwd(ptr(dout), B, Ho, Wo, c, ptr(din), Hi, Wi, int(accumulate),
                                      stream()), "bilinear_nhwc_bwd")
+    return None
 
 
 RESIZE_BILINEAR, RESIZE_NEAREST, RESIZE_UNCERTAINTY = 0, 1, 2
