@@ -224,6 +224,11 @@ int ugpg_bilinear_nhwc_bwd_bnb(const float* dout, int B, int Ho, int Wo, int C, 
                                int Hi, int Wi, int accumulate, const ugpg_bnb_t* bnb,
                                void* stream);
 
+/* fp32 <-> bf16 (round to nearest even) casts of n elements: the bf16 gradient exchange
+ * of BASELINE configs[2] (gradient buckets all-reduced in bf16). */
+int ugpg_cast_f32_bf16(const float* in, uint16_t* out, int64_t n, void* stream);
+int ugpg_cast_bf16_f32(const uint16_t* in, float* out, int64_t n, void* stream);
+
 /* ---- NCHW resize (F.interpolate at uncertainty_guided_trainer.py:208-209,
  * UG_unet.py:36-53, 419-424; K12/K13)
  *  mode 0: bilinear align_corners;  mode 1: nearest;

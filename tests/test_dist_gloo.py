@@ -43,10 +43,11 @@ def _grads_for(rank):
     return [g[k] for k in param_keys(state)]
 
 
-def _worker(rank, port, outdir, flat):
+def _worker(rank, port, outdir, flat, bf16=False):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "ug-pg-unet_amd")]
+    os.environ["UGPG_GRAD_BF16"] = "1" if bf16 else "0"
     import torch.distributed as dist
     from ugpg.dist import allreduce_gradients, world
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -69,12 +70,16 @@ def _worker(rank, port, outdir, flat):
     dist.destroy_process_group()
 
 
-def _run(flat):
+def _run(flat, bf16=False):
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(_free_port(), d, flat), nprocs=WORLD, join=True)
+        mp.spawn(_worker, args=(_free_port(), d, flat, bf16), nprocs=WORLD, join=True)
         res = [torch.load(os.path.join(d, f"rank{r}.pt"), weights_only=True) for r in range(WORLD)]
     per = [_grads_for(r) for r in range(WORLD)]
-    mean = [(a + b) / WORLD for a, b in zip(*per)]
+    if bf16:  # each rank's bucket rounded to bf16, summed in bf16, cast back
+        bq = lambda t: t.to(torch.bfloat16)
+        mean = [(bq(a) + bq(b)).float() / WORLD for a, b in zip(*per)]
+    else:
+        mean = [(a + b) / WORLD for a, b in zip(*per)]
     for r in range(WORLD):
         for got, want in zip(res[r], mean):
             assert torch.allclose(got, want, rtol=1e-6, atol=1e-9)
@@ -88,6 +93,12 @@ def test_dp_allreduce_flat_buffer():
 
 def test_dp_allreduce_per_tensor_fallback():
     _run(flat=False)
+
+
+def test_dp_allreduce_bf16_exchange():
+    """BASELINE configs[2]'s bf16 DP: gradient buckets exchanged in bf16 (UGPG_GRAD_BF16,
+    on by default with the bf16 conv arithmetic), summed back into the fp32 buffer."""
+    _run(flat=True, bf16=True)
 
 
 def _reducer_worker(rank, port, outdir):

@@ -384,6 +384,27 @@ def test_bilinear_bwd_fused_bn_partials(dev, h, C, acc):
         close(a_, b_, 1e-5, f"bilinear-fused partials: {name}")
 
 
+def test_bf16_casts(dev):
+    """The bf16 gradient exchange's casts: round to nearest even exactly as torch's
+    .to(bfloat16) (ties, subnormals, inf, NaN), and back exactly."""
+    from ugpg import ops
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(100003, generator=g) * torch.exp(torch.randn(100003, generator=g) * 20)
+    ties = torch.tensor([1.0 + 2 ** -8, 1.0 + 3 * 2 ** -8, -1.0 - 2 ** -8, 2 ** -130, -2 ** -133,
+                         float("inf"), -float("inf"), 3.0e38, -3.4e38], dtype=torch.float32)
+    x = torch.cat([x, ties]).to(dev)
+    h = torch.empty(x.numel(), dtype=torch.bfloat16, device=dev)
+    ops.cast_f32_bf16(x, h)
+    assert torch.equal(h.view(torch.int16).cpu(), x.cpu().to(torch.bfloat16).view(torch.int16))
+    y = torch.empty_like(x)
+    ops.cast_bf16_f32(h, y)
+    assert torch.equal(y.cpu(), h.cpu().float())
+    n = torch.tensor([float("nan")], device=dev)
+    hn = torch.empty(1, dtype=torch.bfloat16, device=dev)
+    ops.cast_f32_bf16(n, hn)
+    assert torch.isnan(hn.float()).all()
+
+
 def test_bn_eval_params_cache(dev):
     """Eval-mode BN (scale, shift) cached on the module: reused while gamma, beta and the
     running stats are unchanged, recomputed after any in-place write (torch ops, the

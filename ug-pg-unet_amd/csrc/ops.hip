@@ -114,6 +114,23 @@ __global__ void __launch_bounds__(256)
     st.write(bnb, C);
 }
 
+// fp32 <-> bf16 casts of a gradient bucket (the bf16 gradient exchange of config 3):
+// round to nearest even, NaN kept quiet
+__global__ void cast_f32_bf16_kernel(const float* in, uint16_t* out, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t u = __float_as_uint(in[i]);
+        out[i] = (u & 0x7fffffffu) > 0x7f800000u
+                     ? (uint16_t)((u >> 16) | 0x40u)
+                     : (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+    }
+}
+__global__ void cast_bf16_f32_kernel(const uint16_t* in, float* out, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = __uint_as_float((uint32_t)in[i] << 16);
+}
+
 // ------------------------------------------------- bilinear (align_corners)
 // gather-form backward: input index i collects from outputs o with i0(o)==i or i1(o)==i
 __device__ __forceinline__ void ac_range(int i, int in, int out, int& lo, int& hi) {
@@ -1294,6 +1311,22 @@ extern "C" int ugpg_bilinear_nhwc_bwd_bnb(const float* dout, int B, int Ho, int 
     hipLaunchKernelGGL(bilinear_nhwc_bwd_bnb_kernel, dim3(b.nblk), dim3(256), 0,
                        as_stream(stream), dout, B, Ho, Wo, C, din, Hi, Wi, acc, b);
     return check_launch("bilinear_nhwc_bwd_bnb");
+}
+
+extern "C" int ugpg_cast_f32_bf16(const float* in, uint16_t* out, int64_t n, void* stream) {
+    UGPG_REQUIRE(in && out && n >= 0, "cast_f32_bf16");
+    if (n == 0) return UGPG_OK;
+    hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(stream_grid(n)), dim3(256), 0, as_stream(stream),
+                       in, out, n);
+    return check_launch("cast_f32_bf16");
+}
+
+extern "C" int ugpg_cast_bf16_f32(const uint16_t* in, float* out, int64_t n, void* stream) {
+    UGPG_REQUIRE(in && out && n >= 0, "cast_bf16_f32");
+    if (n == 0) return UGPG_OK;
+    hipLaunchKernelGGL(cast_bf16_f32_kernel, dim3(stream_grid(n)), dim3(256), 0, as_stream(stream),
+                       in, out, n);
+    return check_launch("cast_bf16_f32");
 }
 
 extern "C" int ugpg_resize_nchw(const float* in, int B, int C, int Hi, int Wi, float* out, int Ho,

@@ -73,6 +73,8 @@ SIGNATURES = {
     "ugpg_bilinear_nhwc_fwd": (_i, [Src, _i, _i, _i, _p, _i, _i, _p]),
     "ugpg_bilinear_nhwc_bwd": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _i, _p]),
     "ugpg_bilinear_nhwc_bwd_bnb": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _i, C.POINTER(Bnb), _p]),
+    "ugpg_cast_f32_bf16": (_i, [_p, _p, _i64, _p]),
+    "ugpg_cast_bf16_f32": (_i, [_p, _p, _i64, _p]),
     "ugpg_resize_nchw": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _i, _p]),
     "ugpg_resize_nchw_bwd": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _p]),
     "ugpg_nchw_to_nhwc": (_i, [_p, _i, _i, _i, _i, _p, _i, _p]),

@@ -253,10 +253,45 @@ class _NativeWork:
 _SIDE = None
 
 
-def _all_reduce_async(t):
+def grad_bf16() -> bool:
+    """Exchange gradient buckets in bf16 (BASELINE configs[2], 'bf16 DP')?  UGPG_GRAD_BF16
+    = 1 / 0, default: with the bf16 conv arithmetic (ops.set_conv_math("bf16"))."""
+    v = os.environ.get("UGPG_GRAD_BF16", "auto")
+    if v == "auto":
+        from . import ops
+        return ops.conv_math() == "bf16"
+    return v == "1"
+
+
+class _Bf16Work:
+    """async handle of a bucket exchanged in bf16: the sum is cast back into the fp32
+    bucket on the current stream at wait()"""
+
+    def __init__(self, t):
+        self.t = t
+        if t.is_cuda:
+            from . import ops
+            self.h = torch.empty(t.numel(), dtype=torch.bfloat16, device=t.device)
+            ops.cast_f32_bf16(t, self.h)
+        else:  # gloo rehearsal on CPU tensors (tests)
+            self.h = t.to(torch.bfloat16)
+        self.w = _all_reduce_async(self.h, bf16=False)
+
+    def wait(self):
+        self.w.wait()
+        if self.t.is_cuda:
+            from . import ops
+            ops.cast_bf16_f32(self.h, self.t)
+        else:
+            self.t.copy_(self.h.to(torch.float32))
+
+
+def _all_reduce_async(t, bf16=None):
     """SUM all-reduce of a gradient bucket: RCCL through torch.distributed (async work), or
-    libugpg's communicator on a side stream (UGPG_COMM=native)."""
+    libugpg's communicator on a side stream (UGPG_COMM=native); in bf16 when grad_bf16()."""
     global _SIDE
+    if (grad_bf16() if bf16 is None else bf16) and t.dtype == torch.float32:
+        return _Bf16Work(t)
     comm = native_comm() if t.is_cuda else None
     if comm is None:
         return dist.all_reduce(t, async_op=True)

@@ -419,6 +419,14 @@ def bilinear_nhwc_bwd(dout, Hi, Wi, din, accumulate, bnb=None):
     return None
 
 
+def cast_f32_bf16(src, dst):
+    check(lib.ugpg_cast_f32_bf16(ptr(src), ptr(dst), src.numel(), stream()), "cast_f32_bf16")
+
+
+def cast_bf16_f32(src, dst):
+    check(lib.ugpg_cast_bf16_f32(ptr(src), ptr(dst), src.numel(), stream()), "cast_bf16_f32")
+
+
 RESIZE_BILINEAR, RESIZE_NEAREST, RESIZE_UNCERTAINTY = 0, 1, 2
 
 
