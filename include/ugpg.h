@@ -56,6 +56,9 @@ typedef struct {
     const float* scale;
     const float* shift;
     int C;
+    /* optional bf16 copy of data (round to nearest even), read instead of data by the
+     * single-piece (UGPG_WFMT_BF16) persistent conv forms; NULL: none */
+    const void* data_bf16;
 } ugpg_src_t;
 
 /* ---- 3x3 convolution, padding 1, stride 1 (UG_unet_parts.py:10,13) ---------
@@ -103,6 +106,9 @@ typedef struct {
     const float* bnb_scale;
     const float* bnb_shift;
     float* bnb_part;
+    /* optional bf16 copy of out[0] (one output, no accumulate): written beside it, for
+     * the next conv's ugpg_src_t.data_bf16 (the bf16 arithmetic's activation storage) */
+    void* out_bf16;
 } ugpg_conv_t;
 
 #define UGPG_WFMT_F32 0
@@ -219,7 +225,8 @@ int ugpg_bilinear_nhwc_fwd(ugpg_src_t src, int B, int Hi, int Wi, float* out, in
                            void* stream);
 int ugpg_bilinear_nhwc_bwd(const float* dout, int B, int Ho, int Wo, int C, float* din, int Hi,
                            int Wi, int accumulate, void* stream);
-/* The same, also writing the BatchNorm-backward partials of din (see ugpg_bnb_t). */
+/* The same, also writing the BatchNorm-backward partials of din (see ugpg_bnb_t), one
+ * slot per input row: nslots = B * Hi (C/4 must divide 256). */
 int ugpg_bilinear_nhwc_bwd_bnb(const float* dout, int B, int Ho, int Wo, int C, float* din,
                                int Hi, int Wi, int accumulate, const ugpg_bnb_t* bnb,
                                void* stream);

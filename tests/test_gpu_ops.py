@@ -405,6 +405,38 @@ def test_bf16_casts(dev):
     assert torch.isnan(hn.float()).all()
 
 
+@pytest.mark.parametrize("case", [(2, 32, 40, 64, 0, 128), (1, 36, 64, 64, 64, 64),
+                                  (2, 24, 20, 64, 0, 64), (2, 40, 48, 8, 0, 64)])
+def test_conv_bf16_activation_copies(dev, case):
+    """bf16 arithmetic with bf16 activation copies: out16 == bf16(out) for every kernel
+    form (persistent epilogue, image kernel, cast pass), and a source read through its
+    bf16 copy gives the same output as the fp32 source when y is bf16-exact."""
+    from ugpg import ops
+    B, H, W, C0, C1, Cout = case
+    old = ops.conv_math()
+    ops.set_conv_math("bf16")
+    try:
+        cin = C0 + C1
+        y0 = nhwc(rnd((B, C0, H, W), 80, "y0")).to(torch.bfloat16).float().to(dev)
+        y1 = nhwc(rnd((B, C1, H, W), 81, "y1")).to(dev) if C1 else None
+        sc = (rnd((C0,), 82, "s", 0.5) + 1).to(dev) if C0 % 16 == 0 else None
+        sh = rnd((C0,), 83, "h", 0.2).to(dev) if sc is not None else None
+        w = rnd((Cout, cin, 3, 3), 84, "w", 0.05).to(dev)
+        wpk = ops.pack_conv3x3(w, ops.conv_pack_k(cin), 0)
+        outs = []
+        for use16 in (False, True):
+            a0 = ops.Act(y0, sc, sh, y0.to(torch.bfloat16) if use16 else None)
+            srcs = [a0] + ([ops.Act(y1)] if C1 else [])
+            out = torch.empty(B, H, W, Cout, device=dev)
+            o16 = torch.empty(B, H, W, Cout, device=dev, dtype=torch.bfloat16)
+            ops.conv3x3_fwd(srcs, wpk, None, Cout, [out], out16=o16)
+            assert torch.equal(o16, out.to(torch.bfloat16)), "out16 must be bf16(out)"
+            outs.append(out)
+        assert torch.equal(outs[0], outs[1]), "bf16 copy read must equal the fp32 read"
+    finally:
+        ops.set_conv_math(old)
+
+
 def test_bn_eval_params_cache(dev):
     """Eval-mode BN (scale, shift) cached on the module: reused while gamma, beta and the
     running stats are unchanged, recomputed after any in-place write (torch ops, the

@@ -860,6 +860,18 @@ extern "C" int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream) {
     a.bnb_scale = p->bnb_scale;
     a.bnb_shift = p->bnb_shift;
     a.bnb_part = p->bnb_part;
+    a.src0_16 = static_cast<const __bf16*>(p->src[0].data_bf16);
+    a.src1_16 = p->src[1].data ? static_cast<const __bf16*>(p->src[1].data_bf16) : nullptr;
+    a.out0_16 = static_cast<__bf16*>(p->out_bf16);
+    if (p->out_bf16 && (p->out_split != p->Cout || p->accumulate[0])) {
+        set_error("conv3x3_fwd: out_bf16 needs one output without accumulate");
+        return UGPG_ERR_INVALID;
+    }
+    // forms that do not write the bf16 copy themselves: a cast pass after the conv
+    auto out16_pass = [&]() {
+        return ugpg_cast_f32_bf16(p->out[0], static_cast<uint16_t*>(p->out_bf16),
+                                  (int64_t)p->B * p->H * p->W * p->Cout, stream);
+    };
     // forms that do not fuse the partials: the same reduction as a pass after the conv
     auto bnb_pass = [&]() {
         const int nslots = ugpg_conv3x3_fwd_ntiles(p->B, p->H, p->W, Cin, p->Cout, p->wfmt);
@@ -894,16 +906,17 @@ extern "C" int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream) {
         a.tiles_x = (int)cdiv(p->W, fwd_x6_tile_w(p->W, np));
         a.tiles_y = (int)cdiv(p->H, fwd_x6_tile_h(p->W, np));
         a.ntiles = p->B * a.tiles_x * a.tiles_y;
-        const bool fused = launch_fwd_x6(a, np, st);
-        if (bnb && !fused) bnb_pass();
-        return check_launch("conv3x3_fwd_x6");
+        const int wrote = launch_fwd_x6(a, np, st);
+        if (bnb && !(wrote & FWD_WROTE_BNB)) bnb_pass();
+        if (int e = check_launch("conv3x3_fwd_x6")) return e;
+        return p->out_bf16 && !(wrote & FWD_WROTE_OUT16) ? out16_pass() : UGPG_OK;
     }
     if (img_fwd_eligible(p->W, C0, C1, p->Cout)) {
         // the image layer in fp32 / bf16 mode: the direct fp32 kernel on the fp32 pack
         a.tiles_x = (int)cdiv(p->W, 32);
         a.tiles_y = (int)cdiv(p->H, 8);
         a.ntiles = p->B * a.tiles_x * a.tiles_y;
-        if (launch_img_fwd(a, true, st)) return check_launch("conv3x3_img_fwd");
+        if (launch_img_fwd(a, true, st)) return check_launch("conv3x3_img_fwd");  // + out16
         if (p->stats) {  // ugpg_conv3x3_fwd_ntiles counted the image kernel's slots
             set_error("conv3x3_fwd: BatchNorm partials of an 8-channel source need one "
                       "output without accumulate");
@@ -935,7 +948,8 @@ extern "C" int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream) {
             break;
     }
     if (bnb) bnb_pass();
-    return check_launch("conv3x3_fwd");
+    if (int e = check_launch("conv3x3_fwd")) return e;
+    return p->out_bf16 ? out16_pass() : UGPG_OK;
 }
 
 extern "C" size_t ugpg_pack_conv3x3_bytes(int Cout, int Cin_pad, int wfmt) {

@@ -34,6 +34,11 @@ struct ConvFwdArgs {
     const float* bnb_scale;
     const float* bnb_shift;
     float* bnb_part;
+    // bf16 copies (ugpg_src_t.data_bf16, ugpg_conv_t.out_bf16): read by / written beside
+    // the single-piece persistent form; nullptr: none
+    const __bf16* src0_16;
+    const __bf16* src1_16;
+    __bf16* out0_16;
 };
 
 // Output pixel (row*TW + col inside the tile) of GEMM row m.  PERM16 is the
@@ -169,14 +174,15 @@ struct WgradArgs {
 };
 
 // split-bf16 path (conv_x6.hip)
-// np: bf16 pieces (3 or 1); returns whether the launched form wrote the BatchNorm-backward
-// partials (a.bnb_part) itself
-bool launch_fwd_x6(const ConvFwdArgs& a, int np, hipStream_t st);
+// np: bf16 pieces (3 or 1); returns which of the optional outputs the launched form wrote
+// itself: FWD_WROTE_BNB (a.bnb_part), FWD_WROTE_OUT16 (a.out0_16)
+constexpr int FWD_WROTE_BNB = 1, FWD_WROTE_OUT16 = 2;
+int launch_fwd_x6(const ConvFwdArgs& a, int np, hipStream_t st);
 // the image layer's direct fp32 forward (conv_x6.hip, knob "x6_img"): shape predicate,
 // BatchNorm slot count (nwm row groups per 8 x 32 tile), launch (false: not applicable)
 bool img_fwd_eligible(int W, int C0, int C1, int Cout);
 int img_fwd_slots(int B, int H, int W, int nwm);
-bool launch_img_fwd(const ConvFwdArgs& a, bool wf32, hipStream_t st);
+bool launch_img_fwd(const ConvFwdArgs& a, bool wf32, hipStream_t st);  // writes out0_16 too
 // bn.hip: the per-slot BatchNorm-backward reduction (partials layout of ugpg_conv_t.bnb_part)
 void launch_bn_bwd_reduce(const float* da, const float* y, int64_t npix, int C, const float* mean,
                           const float* invstd, const float* scale, const float* shift, float* part,

@@ -414,6 +414,8 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
                     float* p = rowp + pxc * ostride;
                     if constexpr (ACC) *p += v;
                     else *p = v;
+                    if (!ACC && a.out0_16)  // bf16 copy (one output: ostride == Cout)
+                        a.out0_16[p - a.out0] = (__bf16)v;
                     psum += v;
                 }
             }
@@ -812,6 +814,7 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
         unsigned avalid[2] = {0u, 0u};
         Act4 r0[2], r1[2];
         float lo[2] = {0.f, 0.f};
+        bool b16[2] = {false, false};
         // cursor over loader steps (clamped to the last one): chunk, item, column block
         // and tile position, advanced without divisions except at item changes
         struct Cur {
@@ -852,6 +855,10 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
             const int cb0 = c * BKC;
             const bool second = cb0 >= a.C0;
             const float* src = second ? a.src1 : a.src0;
+            // single-piece form: a source's bf16 copy is read instead (half the bytes; the
+            // second load repeats the first address, so the load count stays fixed)
+            const __bf16* s16 = NP == 1 ? (second ? a.src1_16 : a.src0_16) : nullptr;
+            b16[st] = s16 != nullptr;
             const float* sc = second ? a.sc1 : a.sc0;
             const float* sh = second ? a.sh1 : a.sh0;
             const int Cs = second ? a.C1 : a.C0;
@@ -873,9 +880,12 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
                 const int gy = p.ty0 - 1 + hy[v], gx = p.tx0 - 1 + hx[v];
                 const bool ok = cok && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
                 const int cy = min(max(gy, 0), a.H - 1), cx = min(max(gx, 0), a.W - 1);
-                const float* gp = src + ((size_t)(p.b * a.H + cy) * a.W + cx) * Cs + cc;
-                ra[st][v][0] = gld16(gp);
-                ra[st][v][1] = gld16(gp + 4);
+                const size_t off = ((size_t)(p.b * a.H + cy) * a.W + cx) * Cs + cc;
+                const void* g0 = s16 ? static_cast<const void*>(s16 + off)
+                                     : static_cast<const void*>(src + off);
+                const void* g1 = s16 ? g0 : static_cast<const void*>(src + off + 4);
+                ra[st][v][0] = gld16(g0);
+                ra[st][v][1] = gld16(g1);
                 av |= (ok ? 1u : 0u) << v;
             }
             avalid[st] = av;
@@ -887,8 +897,19 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
 #pragma unroll
             for (int v = v0; v < v1; ++v) {
                 const int hp = item_px(lt + v * 256), hh = hhl;
-                const f32x4 lo4 = act_floor4(ra[st][v][0], r0[st], lo[st]),
-                            hi4 = act_floor4(ra[st][v][1], r1[st], lo[st]);
+                f32x4 raw0 = ra[st][v][0], raw1 = ra[st][v][1];
+                if (NP == 1 && b16[st]) {  // 8 bf16 in the first load: widen (exact)
+                    const u32x4 w = __builtin_bit_cast(u32x4, raw0);
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        raw0[2 * i] = __uint_as_float(w[i] << 16);
+                        raw0[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+                        raw1[2 * i] = __uint_as_float(w[2 + i] << 16);
+                        raw1[2 * i + 1] = __uint_as_float(w[2 + i] & 0xffff0000u);
+                    }
+                }
+                const f32x4 lo4 = act_floor4(raw0, r0[st], lo[st]),
+                            hi4 = act_floor4(raw1, r1[st], lo[st]);
                 const bool ok = (avalid[st] >> v) & 1u;
                 const f32x8 x = {ok ? lo4.x : 0.f, ok ? lo4.y : 0.f, ok ? lo4.z : 0.f,
                                  ok ? lo4.w : 0.f, ok ? hi4.x : 0.f, ok ? hi4.y : 0.f,
@@ -2182,6 +2203,11 @@ __global__ void __launch_bounds__(4096 / PX) conv3x3_img_fwd_kernel(ConvFwdArgs 
             if (rok && c0 + p < vw) {
 #ifndef IMG_NOSTORE
                 *reinterpret_cast<f32x4*>(orow + (size_t)p * 64) = f32x4{v[p][0], v[p][1], v[p][2], v[p][3]};
+                if (a.out0_16) {
+                    typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+                    *reinterpret_cast<bf4*>(a.out0_16 + (orow - a.out0) + (size_t)p * 64) =
+                        bf4{(__bf16)v[p][0], (__bf16)v[p][1], (__bf16)v[p][2], (__bf16)v[p][3]};
+                }
 #endif
 #pragma unroll
                 for (int i = 0; i < 4; ++i) sj[i] += v[p][i];
@@ -2284,12 +2310,13 @@ bool launch_img_fwd(const ConvFwdArgs& a, bool wf32, hipStream_t st) {
     return true;
 }
 
-bool launch_fwd_x6(const ConvFwdArgs& a_in, int np, hipStream_t st) {
+int launch_fwd_x6(const ConvFwdArgs& a_in, int np, hipStream_t st) {
     ConvFwdArgs a = a_in;
     a.probe = g_x6_probe;
     a.order = g_x6_order;
     const int64_t items = (int64_t)a.ntiles * (a.Cout / 64);
-    if (np == 3 && use_x6r(a.W, np) && a.Cin == 16 && launch_img_fwd(a, false, st)) return false;
+    if (np == 3 && use_x6r(a.W, np) && a.Cin == 16 && launch_img_fwd(a, false, st))
+        return FWD_WROTE_OUT16;
     if (use_x6r(a.W, np)) {
         // persistent: one workgroup per CU (a multiple of 8: blockIdx % 8 = XCD), each
         // walking a strided share of its XCD's contiguous item range
@@ -2323,8 +2350,9 @@ bool launch_fwd_x6(const ConvFwdArgs& a_in, int np, hipStream_t st) {
         else
             hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false>), dim3((unsigned)g), dim3(512), 0,
                                st, a);
-        // every persistent form fuses the BatchNorm-backward partials into its epilogue
-        return true;
+        // every persistent form fuses the BatchNorm-backward partials into its epilogue;
+        // the 32x32x16 form also writes the bf16 copy of its output
+        return FWD_WROTE_BNB | (np == 3 && g_x6_pipe >= 2 ? 0 : FWD_WROTE_OUT16);
     }
     const unsigned grid = (unsigned)items;
     const bool wide = fwd_x6_tile_w(a.W, np) == 32;
@@ -2339,7 +2367,7 @@ bool launch_fwd_x6(const ConvFwdArgs& a_in, int np, hipStream_t st) {
         else
             hipLaunchKernelGGL((conv3x3_fwd_x6_kernel<8, 16, true, 1>), dim3(grid), dim3(256), 0, st, a);
     }
-    return false;
+    return 0;
 }
 
 void launch_pack_x6(const float* w, void* wpk, int Cout, int Cin, int Cin_pad, int mode, int np,

@@ -316,27 +316,47 @@ __global__ void bilinear_nhwc_bwd_kernel(const float* dout, int B, int Ho, int W
 
 // bilinear backward fused with the BatchNorm-backward partials of din (the BN of the
 // block whose activation was upsampled: this gather is the last writer of its da).
-// Block = a contiguous range of input pixels, thread = 4 channels of every slots-th
-// pixel; each pixel gathers exactly the terms, in exactly the order, of
-// bilinear_nhwc_bwd_kernel (bit-identical din).
+// The body of bilinear_nhwc_bwd_kernel (bit-identical din) with one workgroup per input
+// row (its partial slot: nslots = B * Hi), whose threads keep one 4-channel group each
+// (256 % (C/4) == 0).
 __global__ void __launch_bounds__(256)
     bilinear_nhwc_bwd_bnb_kernel(const float* dout, int B, int Ho, int Wo, int C, float* din,
                                  int Hi, int Wi, int acc, BnbArgs bnb) {
-    const int c4n = C / 4, slots = 256 / c4n;
-    const int tid = threadIdx.x, q = tid % c4n, slot = tid / c4n, c = 4 * q;
-    const int64_t npix = (int64_t)B * Hi * Wi;
+    const int C4 = C / 4;
+    const int row = blockIdx.x;  // b * Hi + iy
+    const int b = row / Hi, iy = row % Hi;
     BnbAcc st;
-    st.init(bnb, c);
-    if (slot < slots) {
-        const int64_t p0 = blockIdx.x * bnb.ppb, p1 = min(npix, p0 + bnb.ppb);
-        for (int64_t p = p0 + slot; p < p1; p += slots) {
-            const int ix = (int)(p % Wi);
-            const int64_t r = p / Wi;
-            const int iy = (int)(r % Hi), b = (int)(r / Hi);
-            int ylo, yhi, xlo, xhi;
-            ac_range_tight(iy, Hi, Ho, ylo, yhi);
-            ac_range_tight(ix, Wi, Wo, xlo, xhi);
-            f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    st.init(bnb, (threadIdx.x % C4) * 4);
+    int ylo, yhi;
+    ac_range_tight(iy, Hi, Ho, ylo, yhi);
+    const int n = Wi * C4;
+    float wy[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wy[j] = ylo + j <= yhi ? ac_weight(ylo + j, iy, Hi, Ho) : 0.f;
+    for (int t = threadIdx.x; t < n; t += blockDim.x) {
+        const int c = (t % C4) * 4, ix = t / C4;
+        int xlo, xhi;
+        ac_range_tight(ix, Wi, Wo, xlo, xhi);
+        f32x4 s = {0.f, 0.f, 0.f, 0.f};
+        if (yhi - ylo <= 3 && xhi - xlo <= 3) {
+            float wx[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) wx[k] = xlo + k <= xhi ? ac_weight(xlo + k, ix, Wi, Wo) : 0.f;
+            f32x4 d[4][4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    d[j][k] = wy[j] != 0.f && wx[k] != 0.f
+                                  ? *reinterpret_cast<const f32x4*>(
+                                        dout + ((size_t)(b * Ho + ylo + j) * Wo + xlo + k) * C + c)
+                                  : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (wy[j] != 0.f && wx[k] != 0.f) s += (wy[j] * wx[k]) * d[j][k];
+        } else {
             for (int oy = ylo; oy <= yhi; ++oy) {
                 const float wyk = ac_weight(oy, iy, Hi, Ho);
                 if (wyk == 0.f) continue;
@@ -348,11 +368,12 @@ __global__ void __launch_bounds__(256)
                     s += (wyk * wx) * d;
                 }
             }
-            f32x4* dst = reinterpret_cast<f32x4*>(din + p * C + c);
-            if (acc) s += *dst;
-            *dst = s;
-            st.add(s, *reinterpret_cast<const f32x4*>(bnb.y + p * C + c));
         }
+        const size_t o = ((size_t)row * Wi + ix) * C + c;
+        f32x4* dst = reinterpret_cast<f32x4*>(din + o);
+        if (acc) s += *dst;
+        *dst = s;
+        st.add(s, *reinterpret_cast<const f32x4*>(bnb.y + o));
     }
     st.write(bnb, C);
 }
@@ -1305,9 +1326,19 @@ extern "C" int ugpg_bilinear_nhwc_bwd_bnb(const float* dout, int B, int Ho, int 
                                           float* din, int Hi, int Wi, int acc,
                                           const ugpg_bnb_t* bnb, void* stream) {
     BnbArgs b;
-    UGPG_REQUIRE(dout && din && B > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0 &&
-                     bnb_args(bnb, (int64_t)B * Hi * Wi, C, b),
+    // one workgroup (= partial slot) per input row; its threads keep their channels
+    UGPG_REQUIRE(dout && din && B > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0 && C % 4 == 0 &&
+                     C <= 1024 && 256 % (C / 4) == 0 && bnb && bnb->nslots == B * Hi &&
+                     bnb->y && bnb->mean && bnb->invstd && bnb->scale && bnb->shift && bnb->part,
                  "bilinear_nhwc_bwd_bnb");
+    b.y = bnb->y;
+    b.mean = bnb->mean;
+    b.invstd = bnb->invstd;
+    b.scale = bnb->scale;
+    b.shift = bnb->shift;
+    b.part = bnb->part;
+    b.nblk = bnb->nslots;
+    b.ppb = Wi;
     hipLaunchKernelGGL(bilinear_nhwc_bwd_bnb_kernel, dim3(b.nblk), dim3(256), 0,
                        as_stream(stream), dout, B, Ho, Wo, C, din, Hi, Wi, acc, b);
     return check_launch("bilinear_nhwc_bwd_bnb");

@@ -18,7 +18,7 @@ _i, _i64, _f, _p, _sz = C.c_int, C.c_int64, C.c_float, C.c_void_p, C.c_size_t
 
 class Src(C.Structure):
     """ugpg_src_t: lazily-activated NHWC operand."""
-    _fields_ = [("data", _p), ("scale", _p), ("shift", _p), ("C", _i)]
+    _fields_ = [("data", _p), ("scale", _p), ("shift", _p), ("C", _i), ("data_bf16", _p)]
 
 
 class ConvDesc(C.Structure):
@@ -26,7 +26,8 @@ class ConvDesc(C.Structure):
     _fields_ = [("B", _i), ("H", _i), ("W", _i), ("src", Src * 2), ("wpk", _p), ("bias", _p),
                 ("Cout", _i), ("out", _p * 2), ("out_split", _i), ("accumulate", _i * 2),
                 ("stats", _p), ("wfmt", _i), ("bnb_y", _p), ("bnb_mean", _p),
-                ("bnb_invstd", _p), ("bnb_scale", _p), ("bnb_shift", _p), ("bnb_part", _p)]
+                ("bnb_invstd", _p), ("bnb_scale", _p), ("bnb_shift", _p), ("bnb_part", _p),
+                ("out_bf16", _p)]
 
 
 class Bnb(C.Structure):

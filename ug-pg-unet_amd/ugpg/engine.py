@@ -24,6 +24,11 @@ from .ops import Act
 # A/B switch: BN1's backward reduction fused into the data gradient of conv2
 _FUSE_BN_BWD = os.environ.get("UGPG_FUSE_BN_BWD", "1") != "0"
 _FUSE_BN_BWD_MIN_K = int(os.environ.get("UGPG_FUSE_BN_BWD_MIN_K", "64"))
+# bf16 copies of the conv outputs under the bf16 arithmetic (config 3), read by the next
+# convs' loaders: off by default -- measured 2.5 % slower (the single-piece form is not
+# bound by its halo bytes, and the copy's stores lengthen the epilogue); the oracle's
+# bf16 model follows oracle.ref_cpu.BF16_STORE
+_BF16_STORE = os.environ.get("UGPG_BF16_STORE", "0") == "1"
 
 
 def ceil_to(v: int, m: int) -> int:
@@ -83,8 +88,13 @@ def double_conv_forward(mod, srcs, ctx: BlockCtx, save: bool):
             ntiles = ops.conv_ntiles(B, H, W, cin, cout, wpk)
             stats = ops.empty(3 * cout * ntiles, like=y)
         bias = conv.bias.detach() if conv.bias is not None else None
+        # bf16 arithmetic: a bf16 copy of y for the next convs' loaders (the persistent
+        # single-piece form, images >= 32 wide), written beside y by the same epilogue
+        y16 = None
+        if _BF16_STORE and W >= 32 and ops.conv_math() == "bf16":
+            y16 = ops.empty(B, H, W, cout, like=y, dtype=torch.bfloat16)
         ops.conv3x3_fwd(cur, wpk, bias, cout, [y], stats=stats,
-                        flops=2.0 * B * H * W * cout * 9 * w.shape[1])
+                        flops=2.0 * B * H * W * cout * 9 * w.shape[1], out16=y16)
         if train:
             if bn.momentum is None:
                 raise NotImplementedError("BatchNorm2d(momentum=None) is not supported")
@@ -104,7 +114,7 @@ def double_conv_forward(mod, srcs, ctx: BlockCtx, save: bool):
                 ctx.y1, ctx.st1 = y, st
             else:
                 ctx.y2, ctx.st2 = y, st
-        cur = [Act(y, scale, shift)]
+        cur = [Act(y, scale, shift, y16)]
         cin = cout
     return cur[0]
 

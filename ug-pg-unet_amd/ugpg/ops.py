@@ -50,11 +50,12 @@ class Act:
 
     BatchNorm + ReLU of a DoubleConv (UG_unet_parts.py:11-12) is folded into the
     consumer's load, so the normalised activation is never written to HBM.
+    y16: optional bf16 copy of y, read by the bf16-arithmetic conv loaders.
     """
-    __slots__ = ("y", "scale", "shift")
+    __slots__ = ("y", "scale", "shift", "y16")
 
-    def __init__(self, y, scale=None, shift=None):
-        self.y, self.scale, self.shift = y, scale, shift
+    def __init__(self, y, scale=None, shift=None, y16=None):
+        self.y, self.scale, self.shift, self.y16 = y, scale, shift, y16
 
     @property
     def shape(self):
@@ -65,7 +66,7 @@ class Act:
         return self.y.shape[-1]
 
     def src(self) -> Src:
-        return Src(ptr(self.y), ptr(self.scale), ptr(self.shift), self.C)
+        return Src(ptr(self.y), ptr(self.scale), ptr(self.shift), self.C, ptr(self.y16))
 
     def materialize(self) -> torch.Tensor:
         if self.scale is None:
@@ -76,7 +77,7 @@ class Act:
         return out
 
 
-NULL_SRC = Src(None, None, None, 0)
+NULL_SRC = Src(None, None, None, 0, None)
 
 
 # ------------------------------------------------------------------ conv
@@ -262,12 +263,13 @@ def _timed(name, flops, fn):
 
 
 def conv3x3_fwd(srcs, wpk, bias, cout, outs, split=None, accumulate=(0, 0), stats=None,
-                flops=None, bnb=None):
+                flops=None, bnb=None, out16=None):
     """srcs: 1-2 Act; outs: 1-2 NHWC tensors (channel split at `split`).
     flops: algorithmic FLOPs of this call (for the optional KernelTimer).
     bnb: (y, mean, invstd, scale, shift, part) -- also write the BatchNorm-backward
     partials of outs[0] = dL/d(relu(bn(y))) into `part` (3*cout*conv_ntiles floats) for
-    bn_relu_bwd(..., part=part)."""
+    bn_relu_bwd(..., part=part).  out16: a bf16 tensor shaped like outs[0] that also
+    receives the output (the bf16 arithmetic's activation copy)."""
     B, H, W, _ = srcs[0].shape
     d = ConvDesc()
     d.B, d.H, d.W = B, H, W
@@ -283,6 +285,8 @@ def conv3x3_fwd(srcs, wpk, bias, cout, outs, split=None, accumulate=(0, 0), stat
     if bnb is not None:
         (d.bnb_y, d.bnb_mean, d.bnb_invstd, d.bnb_scale, d.bnb_shift,
          d.bnb_part) = (ptr(t) for t in bnb)
+    if out16 is not None:
+        d.out_bf16 = ptr(out16)
     _timed("conv3x3_fwd", flops,
            lambda: check(lib.ugpg_conv3x3_fwd(C.byref(d), stream()), "conv3x3_fwd"))
 
@@ -369,10 +373,11 @@ def maxpool2_fwd(a: Act):
     return out, am
 
 
-def bnb_desc(bn_state, npix, c, like):
+def bnb_desc(bn_state, npix, c, like, nslots=None):
     """(ugpg_bnb_t, partials tensor) for a kernel that last writes da of relu(bn(y)):
-    bn_state = (y, mean, invstd, scale, shift)."""
-    n = lib.ugpg_bnb_slots(npix, c)
+    bn_state = (y, mean, invstd, scale, shift); nslots: the kernel's own slot count
+    (default ugpg_bnb_slots)."""
+    n = lib.ugpg_bnb_slots(npix, c) if nslots is None else nslots
     if n <= 0:
         raise ValueError(f"no BatchNorm-backward partials for C={c}")
     part = empty(3 * c * n, like=like)
@@ -409,7 +414,7 @@ def bilinear_nhwc_bwd(dout, Hi, Wi, din, accumulate, bnb=None):
     -> also returns its backward partials (for bn_relu_bwd(part=...))."""
     B, Ho, Wo, c = dout.shape
     if bnb is not None:
-        d, part = bnb_desc(bnb, B * Hi * Wi, c, din)
+        d, part = bnb_desc(bnb, B * Hi * Wi, c, din, nslots=B * Hi)
         check(lib.ugpg_bilinear_nhwc_bwd_bnb(ptr(dout), B, Ho, Wo, c, ptr(din), Hi, Wi,
                                              int(accumulate), C.byref(d), stream()),
               "bilinear_nhwc_bwd_bnb")
