@@ -536,10 +536,12 @@ __device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a,
 #endif
     }
     f32x4 psum[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-    auto store_tiles = [&](auto accumulate) {
+    // the stores of m-tiles [m0, m1)
+    auto store_tiles = [&](auto accumulate, int m0, int m1) {
         constexpr bool ACC = decltype(accumulate)::value;
 #pragma unroll
         for (int mt = 0; mt < MTW; ++mt) {
+            if (mt < m0 || mt >= m1) continue;
             const int py = wm * WR + prow(mt), px = pcol(mt) + l16;
             if (py >= vh) break;  // uniform
             const bool ok = px < vw;
@@ -570,9 +572,10 @@ __device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a,
             }
         }
     };
-    if (oacc) store_tiles(std::integral_constant<bool, true>{});
-    else store_tiles(std::integral_constant<bool, false>{});
-    if (a.bnb_part != nullptr) {
+    const bool bnb = a.bnb_part != nullptr && !oacc;  // (the host refuses bnb + accumulate)
+    if (oacc) store_tiles(std::integral_constant<bool, true>{}, 0, MTW);
+    else if (!bnb) store_tiles(std::integral_constant<bool, false>{}, 0, MTW);
+    if (bnb) {
         // BatchNorm-backward partials of the stored output da (the reduction of
         // ugpg_bn_relu_bwd, bn.hip bn_bwd_reduce_kernel, on the tile still in registers):
         // g = da*[scale*y+shift > 0], xhat = (y-mean)*invstd; per slot sum g, g*xhat, xhat
@@ -586,7 +589,8 @@ __device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a,
             sh[nt] = *reinterpret_cast<const f32x4*>(a.bnb_shift + c);
             sg[nt] = sgx[nt] = sx[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
-        // y loads of 4 m-tiles issued before the first is used (registers: the cw8 forms)
+        // per batch of m-tiles: the y loads go out first, the batch's output stores issue
+        // while they are in flight, then the partials (batch: registers of the cw8 forms)
         constexpr int YB = NWM == 4 ? 1 : (MTW < 4 ? MTW : 4);
 #pragma unroll
         for (int m0 = 0; m0 < MTW; m0 += YB) {
@@ -600,6 +604,7 @@ __device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a,
 #pragma unroll
                 for (int nt = 0; nt < 2; ++nt) yv[u][nt] = *reinterpret_cast<const f32x4*>(yp + 16 * nt);
             }
+            store_tiles(std::integral_constant<bool, false>{}, m0, m0 + YB);
 #pragma unroll
             for (int u = 0; u < YB; ++u) {
                 const int mt = m0 + u;
