@@ -398,10 +398,12 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
     const float bv = a.bias ? a.bias[n0 + nl] : 0.f;
     const int lane_off = 4 * h * ostride + ocol0 + nl;
     float psum = 0.f;
-    auto store_rows = [&](auto accumulate) {
+    // the stores of m-tiles [m0, m1)
+    auto store_rows = [&](auto accumulate, int m0, int m1) {
         constexpr bool ACC = decltype(accumulate)::value;
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
+            if (mt < m0 || mt >= m1) continue;
             const int py = wm * MT + mt;
             if (py >= vh) break;  // uniform
             float* rowp = out + (size_t)((b * a.H + ty0 + py) * a.W + tx0) * ostride + lane_off;
@@ -421,9 +423,10 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
             }
         }
     };
-    if (oacc) store_rows(std::integral_constant<bool, true>{});
-    else store_rows(std::integral_constant<bool, false>{});
-    if (a.bnb_part != nullptr) {
+    const bool bnb = a.bnb_part != nullptr && !oacc;  // (the host refuses bnb + accumulate)
+    if (oacc) store_rows(std::integral_constant<bool, true>{}, 0, MT);
+    else if (!bnb) store_rows(std::integral_constant<bool, false>{}, 0, MT);
+    if (bnb) {
         // BatchNorm-backward partials of the stored output (as x6q_epilogue_wave): this
         // lane's channel over its pixels, the two pixel halves (h) combined by a shuffle
         const int n = n0 + nl;
@@ -442,6 +445,8 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
                 const int pxc = min((r & 3) + 8 * (r >> 2), vw - 1 - 4 * h);
                 yv[r] = yrow[(size_t)max(pxc, -4 * h) * a.Cout];
             }
+            // this row's output stores issue while its y loads are in flight
+            store_rows(std::integral_constant<bool, false>{}, mt, mt + 1);
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int pxc = (r & 3) + 8 * (r >> 2);
