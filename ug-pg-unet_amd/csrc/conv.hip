@@ -636,6 +636,40 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* part, co
     }
 }
 
+// The same reduction for few splits (<= 16: the wide-channel layers, large slabs): a
+// thread owns 4 consecutive (co, ci) elements for all 9 taps and sums the splits in
+// order, so its 36 results are one contiguous OIHW run (wgrad_reduce_kernel's writes
+// there are 4 B at a 36-B stride, each line assembled by blocks on different XCDs).
+__global__ void __launch_bounds__(256) wgrad_reduce_few_kernel(const float* part, int nsplit,
+                                                               int Cout, int Cin, float* dw,
+                                                               int accumulate) {
+    const int64_t m4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // 4 (co, ci) elements
+    const int64_t nm = (int64_t)Cout * Cin, n4 = nm / 4;
+    if (m4 >= n4) return;
+    const f32x4* p = reinterpret_cast<const f32x4*>(part);
+    f32x4 s[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) s[t] = p[(size_t)t * n4 + m4];
+    for (int k = 1; k < nsplit; ++k) {
+        const f32x4* q = p + (size_t)k * 9 * n4;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) s[t] += q[(size_t)t * n4 + m4];
+    }
+    // element e = 4*m4 + j, tap t -> dw[e*9 + t]: 36 consecutive floats
+    f32x4* o = reinterpret_cast<f32x4*>(dw + (size_t)m4 * 36);
+#pragma unroll
+    for (int v = 0; v < 9; ++v) {
+        f32x4 r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int f = 4 * v + i, j = f / 9, t = f % 9;
+            r[i] = s[t][j];
+        }
+        if (accumulate) r += o[v];
+        o[v] = r;
+    }
+}
+
 __global__ void pack_conv3x3_kernel(const float* w, float* wpk, int Cout, int Cin, int Cin_pad,
                                     int mode) {
     // mode 0: wpk[Cin_pad/8][9][Cout][8];  mode 1: wpk[Cout/8][9][Cin_pad][8] (rot180, transposed)
@@ -1113,6 +1147,13 @@ extern "C" int ugpg_conv3x3_wgrad(const ugpg_wgrad_t* p, void* ws, size_t ws_byt
     }
     if (int e = check_launch("conv3x3_wgrad")) return e;
     const int Cr = p->Cin_real > 0 ? p->Cin_real : Cin;
+    if (w.nsplit <= 16 && Cr == Cin && !p->db && ((int64_t)p->Cout * Cin) % 4 == 0 &&
+        reinterpret_cast<uintptr_t>(p->dw) % 16 == 0) {  // (dw may be a view of a flat buffer)
+        const int64_t n4 = (int64_t)p->Cout * Cin / 4;
+        hipLaunchKernelGGL(wgrad_reduce_few_kernel, dim3((unsigned)cdiv(n4, 256)), dim3(256), 0, st,
+                           a.part, w.nsplit, p->Cout, Cin, p->dw, p->accumulate);
+        return check_launch("conv3x3_wgrad_reduce");
+    }
     int64_t rblocks = cdiv((int64_t)9 * p->Cout * Cin / 4, 16);
     if (rblocks > 4096) rblocks = 4096;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)rblocks), dim3(256), 0, st, a.part,
