@@ -777,7 +777,16 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
     constexpr int R_VEC = NP * 2 * 3 * BN;                  // one kernel row of weights
     constexpr int R_PER = (R_VEC + 255) / 256;
     constexpr int R_STR = R_VEC;                            // ring slot pitch
-    constexpr int NSLOT = 4;
+    // weight rows DMA'd LA rows ahead of the row the compute waves read (ring NSLOT >=
+    // LA + 1).  Three rows = two phases of flight cover the DMA latency when a phase holds
+    // 3 x 6 split-bf16 MFMA groups; the single-piece form's phases are a sixth as long,
+    // so it runs six rows (five phases) ahead in a ring of eight (6 KiB slots)
+#ifndef X6R_NP1_LA
+#define X6R_NP1_LA 6
+#endif
+    constexpr int LA = NP == 1 ? X6R_NP1_LA : 3;
+    static_assert(LA == 3 || LA == 6, "row lookahead: one or two steps");
+    constexpr int NSLOT = LA == 3 ? 4 : 8;
     __shared__ __attribute__((aligned(16))) u32x4 smem[2 * A_VECS + NSLOT * R_STR + 1];
     u32x4* const Bring = smem + 2 * A_VECS;
     u32x4* const dummy = smem + 2 * A_VECS + NSLOT * R_STR;  // writes of idle lanes
@@ -958,13 +967,19 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
             dma_row(q0, 0, 0);
             dma_row(q0, 1, 1);
             dma_row(q0, 2, 2);
+            if constexpr (LA == 6) {
+                const Cur q1 = cur_at(1);
+                dma_row(q1, 0, 3);
+                dma_row(q1, 1, 4);
+                dma_row(q1, 2, 5);
+            }
             load_halo(cur_at(1), Set1{});
             load_halo(cur_at(2), Set0{});
             vm_wait<0>();
         }
         lds_barrier();
-        Cur cw = cur_at(1), ch = cur_at(3);  // weight rows of step k+1, halo of step k+3
-        int sl = 3;                          // ring slot of row 3(k+1)
+        Cur cw = cur_at(LA / 3), ch = cur_at(3);  // weight rows of step k+LA/3, halo of step k+3
+        int sl = LA % NSLOT;                      // ring slot of row 3k+LA
         // Phase ph of step k DMAs row j = 3(k+1)+ph into the slot of row j-4 (read in
         // the phase before, whose MFMAs consumed it before that phase's barrier) and
         // retires the previous phase's row before its own closing barrier, so every row
@@ -994,27 +1009,44 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
 #ifdef X6R_NOHALO
 #define load_halo(...) ((void)0)
 #endif
-        auto step = [&](int k, auto S) {  // S = set of halo(k+1); rows j = 3(k+1) + ph
+        auto step = [&](int k, auto S) {  // S = set of halo(k+1); rows j = 3k + LA + ph
+            // Each phase retires row 3k+ph+2 (read from the next phase on).  LA = 6: the
+            // loads issued after that row are the next four rows plus one or two halo
+            // batches, and phase 0 first retires halo(k+1) (issued right after row 3k+2)
+            // before writing it.
             // phase 0
             dma_row(cw, 0, sl);
-            store_halo(k + 1, S, 0, HA);
-            ST_WAIT(st_vm[0], vm_wait<H + R>());  // row j-1
+            if constexpr (LA == 3) {
+                store_halo(k + 1, S, 0, HA);
+                ST_WAIT(st_vm[0], vm_wait<H + R>());  // row j-1
+            } else {
+                ST_WAIT(st_vm[0], vm_wait<4 * R + H>());  // halo(k+1), row 3k+2
+                store_halo(k + 1, S, 0, HA);
+            }
             ST_WAIT(st_bar[0], lds_barrier());
             // phase 1
-            dma_row(cw, 1, (sl + 1) & 3);
+            dma_row(cw, 1, (sl + 1) % NSLOT);
             store_halo(k + 1, S, HA, A_PER);
-            ST_WAIT(st_vm[1], vm_wait<R>());  // row j (and halo(k+2))
+            if constexpr (LA == 3) {
+                ST_WAIT(st_vm[1], vm_wait<R>());  // row j (and halo(k+2))
+            } else {
+                ST_WAIT(st_vm[1], vm_wait<4 * R + H>());  // row 3k+3
+            }
             ST_WAIT(st_bar[1], lds_barrier());
             // phase 2
-            dma_row(cw, 2, (sl + 2) & 3);
+            dma_row(cw, 2, (sl + 2) % NSLOT);
             load_halo(ch, S);
             advance(cw);
             advance(ch);
-            sl = (sl + 3) & 3;
-            ST_WAIT(st_vm[2], vm_wait<R + H>());  // row j+1
+            sl = (sl + 3) % NSLOT;
+            if constexpr (LA == 3) {
+                ST_WAIT(st_vm[2], vm_wait<R + H>());  // row j+1
+            } else {
+                ST_WAIT(st_vm[2], vm_wait<4 * R + 2 * H>());  // row 3k+4
+            }
             ST_WAIT(st_bar[2], lds_barrier());
         };
-        static_assert(NSLOT == 4, "slot arithmetic mod 4");
+        static_assert((NSLOT & (NSLOT - 1)) == 0 && NSLOT >= LA + 1, "ring slot arithmetic");
         for (int k = 0; k < total; k += 2) {
             step(k, Set1{});
             if (k + 1 < total) step(k + 1, Set0{});
