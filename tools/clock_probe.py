@@ -30,7 +30,9 @@ def main():
     ap.add_argument("--stamps", action="store_true")
     ap.add_argument("--pipes", default="2")
     ap.add_argument("--wgrad", action="store_true", help="time the weight gradient instead")
+    ap.add_argument("--math", default="x6", help="conv arithmetic (x6 / bf16)")
     a = ap.parse_args()
+    ops.set_conv_math(a.math)
     dev = torch.device("cuda:0")
     fn = lib.ugpg_debug_stamps if a.stamps else lib.ugpg_debug_clock
     fn.argtypes = [ctypes.POINTER(ctypes.c_double)]

@@ -1206,6 +1206,12 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
     // one step ahead), so the fragments of the next phase's first tap are read BEFORE
     // the phase's barrier: the barriers only order the loaders' overwrites and expose
     // no LDS latency inside a step.
+    // single-piece pipeline state (fragments of the taps two ahead; see the loop)
+    u32x4 fa1[3][MT][NP], fb1[3][NP];
+    auto ldfrag1 = [&](int kk, int t, u32x4 (&af)[MT][NP], u32x4 (&bf)[NP]) {
+        const int ky = t / 3, kx = t % 3;
+        ldfrag(smem + (kk & 1) * A_VECS, Bring + ((3 * kk + ky) % NSLOT) * R_STR, ky, kx, af, bf);
+    };
     lds_barrier();  // step 0 staged
 #ifdef X6R_CLOCK
     const unsigned long long clk_t0 = __builtin_amdgcn_s_memtime(),
@@ -1213,6 +1219,10 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
 #endif
     int cc = 0, item = item0;
     Pos cp = pos_of(item0);
+    if constexpr (NP == 1 && MT <= 4) {
+        ldfrag1(0, 0, fa1[0], fb1[0]);
+        ldfrag1(0, 1, fa1[1], fb1[1]);
+    }
     for (int k = 0; k < total; ++k) {
         const u32x4* Ac = smem + (k & 1) * A_VECS;
         if constexpr (MT > 4) {
@@ -1236,6 +1246,28 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
                     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
                     if (t + 1 < 9) {
                         if (i == 0) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                        else __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                if (t % 3 == 2) read_barrier();
+            }
+        } else if constexpr (NP == 1) {
+            // single piece: 4 MFMAs per tap cannot cover the next tap's fragment reads, so
+            // the reads run two taps ahead, across the step boundary (the next step's first
+            // two taps are read in phase 2: halo(k+1) and row 3k+3 are visible from there)
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                if (t + 2 < 9) ldfrag1(k, t + 2, fa1[(t + 2) % 3], fb1[(t + 2) % 3]);
+                else ldfrag1(k + 1, t + 2 - 9, fa1[(t + 2) % 3], fb1[(t + 2) % 3]);
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma_xn<NP>(fa1[t % 3][mt], fb1[t % 3], acc[mt]);
+                constexpr int NM = MT, NR = MT + 1;
+#pragma unroll
+                for (int i = 0; i < NM; ++i) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+                    if (i < NR) {
+                        if (i == 0) __builtin_amdgcn_sched_group_barrier(0x100, NR - NM + 1, 0);
                         else __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                     }
                 }
