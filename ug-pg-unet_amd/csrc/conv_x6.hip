@@ -1003,6 +1003,12 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
 #else
 #define ST_WAIT(acc, stmt) stmt
 #endif
+#if defined(X6R_NODMA) || defined(X6R_NOHALO)
+// these builds drop loads under the counted vm waits, so a wait can leave a load in flight
+// past the point where hipcc reuses its destination register (an address register: a GPU
+// memory fault, seen with the six-row lookahead); audit the build before running one
+#error "stream-removal diagnostic builds are unsafe with counted vm waits (see comment)"
+#endif
 #ifdef X6R_NODMA  // diagnostic builds: drop a load stream (results are wrong)
 #define dma_row(...) ((void)0)
 #endif
