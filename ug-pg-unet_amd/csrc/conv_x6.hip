@@ -784,10 +784,19 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
 #ifndef X6R_NP1_LA
 #define X6R_NP1_LA 6
 #endif
+#ifndef X6R_CTAB_MAX  // channels of both sources the single-piece LDS coefficient table holds
+#define X6R_CTAB_MAX 2048
+#endif
     constexpr int LA = NP == 1 ? X6R_NP1_LA : 3;
     static_assert(LA == 3 || LA == 6, "row lookahead: one or two steps");
     constexpr int NSLOT = LA == 3 ? 4 : 8;
     __shared__ __attribute__((aligned(16))) u32x4 smem[2 * A_VECS + NSLOT * R_STR + 1];
+    // single-piece form: the activation coefficients of every input channel staged in LDS
+    // once per launch, so the loaders' steady-state global instructions are halo loads and
+    // weight DMAs only (that form is bound by its loaders' memory-instruction issue)
+    constexpr bool CTAB = NP == 1;
+    constexpr int CTAB_N = CTAB ? X6R_CTAB_MAX : 4;
+    __shared__ __attribute__((aligned(16))) float ctab[2][CTAB_N];
     u32x4* const Bring = smem + 2 * A_VECS;
     u32x4* const dummy = smem + 2 * A_VECS + NSLOT * R_STR;  // writes of idle lanes
 
@@ -867,8 +876,9 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
             hy[v] = hp < NHALO ? hp / HWD : -(1 << 20);  // never inside the image
             hx[v] = hp % HWD;
         }
-        auto load_halo = [&](const Cur& q, auto S) {
+        auto load_halo = [&](const Cur& q, auto S, auto TABC) {
             constexpr int st = decltype(S)::value;
+            constexpr bool TAB = decltype(TABC)::value;
             const int c = q.c;
             const Pos& p = q.p;
             const int cb0 = c * BKC;
@@ -889,10 +899,18 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
             // an 8-channel source is zero-extended to the 16-channel chunk
             const bool cok = cb + hhl * 8 < Cs;
             const int cc = cb + (cok ? hhl * 8 : 0);
-            r0[st].s = gld16(scp + cc);
-            r0[st].h = gld16(shp + cc);
-            r1[st].s = gld16(scp + cc + 4);
-            r1[st].h = gld16(shp + cc + 4);
+            if constexpr (TAB) {
+                const int tc = (second ? a.C0 : 0) + cc;
+                r0[st].s = *reinterpret_cast<const f32x4*>(&ctab[0][tc]);
+                r0[st].h = *reinterpret_cast<const f32x4*>(&ctab[1][tc]);
+                r1[st].s = *reinterpret_cast<const f32x4*>(&ctab[0][tc + 4]);
+                r1[st].h = *reinterpret_cast<const f32x4*>(&ctab[1][tc + 4]);
+            } else {
+                r0[st].s = gld16(scp + cc);
+                r0[st].h = gld16(shp + cc);
+                r1[st].s = gld16(scp + cc + 4);
+                r1[st].h = gld16(shp + cc + 4);
+            }
             unsigned av = 0;
 #pragma unroll
             for (int v = 0; v < A_PER; ++v) {
@@ -909,7 +927,7 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
             }
             avalid[st] = av;
         };
-        constexpr int HALO_LOADS = 4 + 2 * A_PER;
+        constexpr int HALO_LOADS = (CTAB ? 0 : 4) + 2 * A_PER;  // global loads per loop halo
         auto store_halo = [&](int k, auto S, int v0, int v1) {
             constexpr int st = decltype(S)::value;
             u32x4* As = smem + (k & 1) * A_VECS;
@@ -959,9 +977,24 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
             }
         };
         // prologue: step 0 in LDS (halo buffer 0, rows 0-2), halos 1 and 2 in registers
+        using TabOff = std::integral_constant<bool, false>;
+        using TabOn = std::integral_constant<bool, CTAB>;
+        if constexpr (CTAB) {
+            // plain (tracked) loads, before any untracked one: hipcc's own waits retire them
+            for (int i = lt * 4; i < a.C0 + a.C1; i += 256 * 4) {
+                const bool s1 = i >= a.C0;
+                const int c = s1 ? i - a.C0 : i;
+                const float* scx = s1 ? a.sc1 : a.sc0;
+                const float* shx = s1 ? a.sh1 : a.sh0;
+                const f32x4 vs = scx ? *reinterpret_cast<const f32x4*>(scx + c) : f32x4{1.f, 1.f, 1.f, 1.f};
+                const f32x4 vh = scx ? *reinterpret_cast<const f32x4*>(shx + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+                *reinterpret_cast<f32x4*>(&ctab[0][i]) = vs;
+                *reinterpret_cast<f32x4*>(&ctab[1][i]) = vh;
+            }
+        }
         {
             const Cur q0 = cur_at(0);
-            load_halo(q0, Set0{});
+            load_halo(q0, Set0{}, TabOff{});
             vm_wait<0>();
             store_halo(0, Set0{}, 0, A_PER);
             dma_row(q0, 0, 0);
@@ -973,8 +1006,8 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
                 dma_row(q1, 1, 4);
                 dma_row(q1, 2, 5);
             }
-            load_halo(cur_at(1), Set1{});
-            load_halo(cur_at(2), Set0{});
+            load_halo(cur_at(1), Set1{}, TabOff{});
+            load_halo(cur_at(2), Set0{}, TabOff{});
             vm_wait<0>();
         }
         lds_barrier();
@@ -1041,7 +1074,7 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
             ST_WAIT(st_bar[1], lds_barrier());
             // phase 2
             dma_row(cw, 2, (sl + 2) % NSLOT);
-            load_halo(ch, S);
+            load_halo(ch, S, TabOn{});
             advance(cw);
             advance(ch);
             sl = (sl + 3) % NSLOT;
