@@ -663,12 +663,16 @@ __device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a,
     const int rows = min(max(vh - wm * WR, 0), WR);
     const float cnt = (float)(rows * vw);
     f32x4 mu[2], q[2];
+    // the centring shift of the second moment: any value near the mean gives the same
+    // M2 to rounding (the finalize merges (count, sum, M2) exactly), so one reciprocal
+    // replaces eight fp32 divisions per wave and item
+    const float rcnt = cnt > 0.f ? 1.f / cnt : 0.f;
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             psum[nt][i] = row16_sum(psum[nt][i]);
-            mu[nt][i] = cnt > 0.f ? psum[nt][i] / cnt : 0.f;
+            mu[nt][i] = psum[nt][i] * rcnt;
         }
         q[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
