@@ -40,7 +40,7 @@ def main():
         print(f"bilinear_bwd {2 * h}->{h} C{c}: {us:7.1f} us  {gb:6.0f} GB/s", flush=True)
 
 
-if __name__ == "__main__" and (len(sys.argv) < 2 or sys.argv[1] != "bn"):
+if __name__ == "__main__" and (len(sys.argv) < 2 or sys.argv[1] not in ("bn", "heads")):
     main()
 
 
@@ -74,3 +74,23 @@ def bn_main(knobs):
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "bn":
     bn_main([("old", {"bn_bwd_blocks": 1024, "bn_bwd_ppt": 32}), ("new", {"bn_bwd_blocks": 2048, "bn_bwd_ppt": 4}),
              ("p8", {"bn_bwd_blocks": 2048, "bn_bwd_ppt": 8}), ("b4096", {"bn_bwd_blocks": 4096, "bn_bwd_ppt": 2})])
+
+
+def heads_main():
+    """1x1 deep-supervision head forward at the Stage-4 head shapes (bs16, 1 class)."""
+    dev = torch.device("cuda:0")
+    B = 16
+    tot = 0.0
+    for (h, c) in [(32, 256), (64, 128), (128, 64), (256, 64)]:
+        y = torch.randn(B, h, h, c, device=dev)
+        a = ops.Act(y, torch.rand(c, device=dev) + 0.5, torch.randn(c, device=dev) * 0.1)
+        w, b = torch.randn(1, c, device=dev), torch.randn(1, device=dev)
+        us = timeit(lambda: ops.head_fwd(a, w, b))
+        tot += us
+        gb = y.numel() * 4 / (us * 1e-6) / 1e9
+        print(f"head_fwd {h}^2 C{c}: {us:7.1f} us  {gb:6.0f} GB/s", flush=True)
+    print(f"head_fwd S4 total {tot:.1f} us")
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "heads":
+    heads_main()
