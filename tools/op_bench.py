@@ -40,7 +40,7 @@ def main():
         print(f"bilinear_bwd {2 * h}->{h} C{c}: {us:7.1f} us  {gb:6.0f} GB/s", flush=True)
 
 
-if __name__ == "__main__" and (len(sys.argv) < 2 or sys.argv[1] not in ("bn", "heads")):
+if __name__ == "__main__" and (len(sys.argv) < 2 or sys.argv[1] not in ("bn", "heads", "pack")):
     main()
 
 
@@ -94,3 +94,35 @@ def heads_main():
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "heads":
     heads_main()
+
+
+def pack_main():
+    """The Stage-4 per-step weight pack (every 3x3 conv: forward + data-gradient layouts)
+    as the trainer issues it: one ugpg_pack_conv3x3_batch launch."""
+    import ugpg
+    dev = torch.device("cuda:0")
+    m = ugpg.PGUNet4(3, 1).to(dev)
+    specs = []
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.Conv2d) and mod.kernel_size == (3, 3):
+            w = mod.weight
+            cin = w.shape[1]
+            specs.append((w, ops.conv_pack_k(8 if cin == 3 else cin), 0))
+            if cin != 3:
+                specs.append((w, cin, 1))
+    from ugpg._C import lib
+    items, outs = [], []
+    for w, k, mode in specs:
+        cout, cin = w.shape[0], w.shape[1]
+        fmt = ops.conv_weight_format(cout, k) if mode == 0 else ops.conv_weight_format(k, cout)
+        out = torch.empty(lib.ugpg_pack_conv3x3_bytes(cout, k, fmt), dtype=torch.uint8, device=dev)
+        outs.append(out)
+        items.append(ops.PackItem(ops.ptr(w.detach()), ops.ptr(out), cout, cin, int(k), int(mode)))
+    arr = (ops.PackItem * len(items))(*items)
+    fmt = ops._MATH_FMT[ops.conv_math()]
+    us = timeit(lambda: lib.ugpg_pack_conv3x3_batch(arr, len(items), fmt, ops.stream()), n=50)
+    print(f"pack S4 ({len(specs)} packs, one launch): {us:7.1f} us", flush=True)
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "pack":
+    pack_main()

@@ -2088,18 +2088,72 @@ __global__ void pack_x6_kernel(const float* w, __bf16* wpk, int Cout, int Cin, i
         pack_x6_elem(w, wpk, Cin, K, mode, np, e);
 }
 
-// Every weight of a step in one launch: item i owns blocks [first[i], first[i+1]) and
-// walks its N*K*9 elements with that block range (same element code as pack_x6_kernel).
-__global__ void pack_x6_batch_kernel(PackBatch pb, int np) {
+// The batched pack by (64-column block, 16-deep chunk) tiles: the tile's 64 x 16 x 9
+// weights are read as contiguous OIHW runs into LDS (144 floats per output channel in
+// the forward layout, 576 per input channel in the transposed data-gradient one), then
+// written as whole 16-byte groups of 8 k-values per piece in the pack order.  Same
+// element values and rounding as pack_x6_elem; the element-wise form read OIHW with a
+// 36-byte lane stride (2.4x the algorithmic bytes per launch, profiles/r2h).
+__global__ void __launch_bounds__(256) pack_x6_tile_kernel(PackBatch pb, int np) {
     int i = 0;
     while (i + 1 < pb.n && (int)blockIdx.x >= pb.first[i + 1]) ++i;  // uniform
     const PackItem& it = pb.item[i];
-    const int N = it.mode == 0 ? it.Cout : it.Cin_pad, K = it.mode == 0 ? it.Cin_pad : it.Cout;
-    const int64_t total = (int64_t)N * K * 9;
-    const int64_t nthr = (int64_t)(pb.first[i + 1] - pb.first[i]) * blockDim.x;
-    for (int64_t e = (blockIdx.x - pb.first[i]) * (int64_t)blockDim.x + threadIdx.x; e < total;
-         e += nthr)
-        pack_x6_elem(it.w, static_cast<__bf16*>(it.wpk), it.Cin, K, it.mode, np, e);
+    const int mode = it.mode, Cin = it.Cin;
+    const int K = mode == 0 ? it.Cin_pad : it.Cout, nchunk = K / 16;
+    const int tb = (int)blockIdx.x - pb.first[i], nb = tb / nchunk, chunk = tb % nchunk;
+    constexpr int RP = 145;  // row pitch (floats): odd, so the 64 rows hit distinct banks
+    __shared__ float tile[64 * RP];  // [column n][k 0..15][tap t]
+    const int tid = threadIdx.x;
+    if (mode == 0) {
+        // rows n = nb*64 + r: w[n][chunk*16 .. +16][0..8] = 144 contiguous floats
+        for (int e = tid; e < 64 * 144; e += 256) {
+            const int r = e / 144, c = e - r * 144;
+            const bool ok = chunk * 16 + c / 9 < Cin;
+            tile[r * RP + c] = ok ? it.w[((size_t)(nb * 64 + r) * Cin) * 9 + chunk * 144 + c] : 0.f;
+        }
+    } else {
+        // rows k = chunk*16 + kk (output channels): w[k][nb*64 .. +64][0..8] = 576 floats,
+        // stored at tap 8 - t (the rot180 of the data-gradient layout)
+        for (int e = tid; e < 16 * 576; e += 256) {
+            const int kk = e / 576, c = e - kk * 576, r = c / 9, ts = c - r * 9;
+            const bool ok = nb * 64 + r < Cin;
+            tile[r * RP + kk * 9 + (8 - ts)] =
+                ok ? it.w[((size_t)(chunk * 16 + kk) * Cin) * 9 + nb * 576 + c] : 0.f;
+        }
+    }
+    __syncthreads();
+    constexpr int64_t plane = 3 * 64 * 8;
+    __bf16* const out = static_cast<__bf16*>(it.wpk) + (size_t)((nb * nchunk + chunk) * 3) * np * 2 * plane;
+    // units (ky, h, kx, co) of 8 k-values, co fastest: consecutive lanes, consecutive 16 B
+    for (int u = tid; u < 3 * 2 * 3 * 64; u += 256) {
+        const int co = u & 63, kx = (u >> 6) % 3, h = (u / 192) & 1, ky = u / 384;
+        const float* src = tile + co * RP + h * 8 * 9 + ky * 3 + kx;
+        unsigned short q0[8], q1[8], q2[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float v = src[j * 9];
+            const __bf16 p0 = (__bf16)v;
+            const float r1 = v - (float)p0;
+            const __bf16 p1 = (__bf16)r1;
+            const __bf16 p2 = (__bf16)(r1 - (float)p1);
+            q0[j] = __builtin_bit_cast(unsigned short, p0);
+            q1[j] = __builtin_bit_cast(unsigned short, p1);
+            q2[j] = __builtin_bit_cast(unsigned short, p2);
+        }
+        auto pack8 = [](const unsigned short (&q)[8]) {
+            u32x4 r;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) r[k] = (unsigned)q[2 * k] | ((unsigned)q[2 * k + 1] << 16);
+            return r;
+        };
+        const size_t off = (size_t)(kx * 64 + co) * 8;
+        __bf16* o = out + (size_t)ky * np * 2 * plane + (size_t)h * plane + off;
+        *reinterpret_cast<u32x4*>(o) = pack8(q0);
+        if (np == 3) {
+            *reinterpret_cast<u32x4*>(o + 2 * plane) = pack8(q1);
+            *reinterpret_cast<u32x4*>(o + 4 * plane) = pack8(q2);
+        }
+    }
 }
 
 #ifndef X6_PIPE_DEFAULT
@@ -2504,11 +2558,10 @@ void launch_pack_x6_batch(const PackItem* items, int n, int np, hipStream_t st) 
             pb.item[i] = it;
             pb.first[i] = blocks;
             const int N = it.mode == 0 ? it.Cout : it.Cin_pad, K = it.mode == 0 ? it.Cin_pad : it.Cout;
-            // ~4 elements per thread
-            blocks += (int)std::min<int64_t>(cdiv((int64_t)N * K * 9, 1024), 2048);
+            blocks += (N / 64) * (K / 16);  // one workgroup per (64-column, 16-deep) tile
         }
         pb.first[pb.n] = blocks;
-        hipLaunchKernelGGL(pack_x6_batch_kernel, dim3((unsigned)blocks), dim3(256), 0, st, pb, np);
+        hipLaunchKernelGGL(pack_x6_tile_kernel, dim3((unsigned)blocks), dim3(256), 0, st, pb, np);
     }
 }
 
