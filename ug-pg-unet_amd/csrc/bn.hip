@@ -280,6 +280,7 @@ __global__ void bn_relu_apply_kernel(const float* x, const float* sc, const floa
     }
 }
 
+int g_bn_fin_auto = 1;      // tuning knob "bn_fin_auto": finalize block size from the slot count
 int g_bn_bwd_blocks = 2048;  // tuning knobs "bn_bwd_blocks" / "bn_bwd_ppt" (A/B timing)
 int g_bn_bwd_ppt = 8;
 namespace {
@@ -315,7 +316,14 @@ extern "C" int ugpg_bn_finalize(const float* stats, int ntiles, int C, const flo
         set_error("bn_finalize: bad arguments");
         return UGPG_ERR_INVALID;
     }
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(1024), 0, as_stream(stream), stats,
+    // threads per channel: one per PF = 8 slots, 64..1024 -- the narrow-image layers have
+    // 128-512 slots, and 1024-thread blocks of mostly idle lanes cost them ~4 us a launch
+    int nt = 1024;
+    if (g_bn_fin_auto) {
+        nt = 64;
+        while (nt < 1024 && (int64_t)nt * 8 < ntiles) nt *= 2;
+    }
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(nt), 0, as_stream(stream), stats,
                        ntiles, C, gamma, beta, running_mean, running_var, nbt, momentum, eps,
                        mean, invstd, scale, shift);
     return check_launch("bn_finalize");
