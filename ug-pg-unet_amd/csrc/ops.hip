@@ -15,6 +15,9 @@
 namespace ugpg {
 
 // ---------------------------------------------------------------- max-pool
+int g_pool_nt = 0;  // tuning knob "pool_nt": nontemporal window loads in maxpool2_fwd_kernel (measured neutral)
+
+template <bool NT>
 __global__ void maxpool2_fwd_kernel(const float* x, const float* sc, const float* sh, int B, int H,
                                     int W, int C, float* out, uint8_t* am) {
     const int Ho = H / 2, Wo = W / 2, C4 = C / 4;
@@ -28,11 +31,18 @@ __global__ void maxpool2_fwd_kernel(const float* x, const float* sc, const float
         const int oy = (int)(r % Ho), b = (int)(r / Ho);
         f32x4 best;
         uint8_t idx[4] = {0, 0, 0, 0};
+        f32x4 xv[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int y = 2 * oy + (k >> 1), xx = 2 * ox + (k & 1);
-            f32x4 v = *reinterpret_cast<const f32x4*>(x + ((size_t)(b * H + y) * W + xx) * C + c);
-            v = act_apply4(v, sc, sh, c);
+            const f32x4* src = reinterpret_cast<const f32x4*>(x + ((size_t)(b * H + y) * W + xx) * C + c);
+            // NT: the window is read once here; the skip connection re-reads the block's
+            // output only several layers later, long after it would have left the caches
+            xv[k] = NT ? __builtin_nontemporal_load(src) : *src;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            f32x4 v = act_apply4(xv[k], sc, sh, c);
             if (k == 0) {
                 best = v;
             } else {
@@ -1321,8 +1331,12 @@ extern "C" int ugpg_maxpool2_fwd(ugpg_src_t s, int B, int H, int W, float* out, 
                                  void* stream) {
     UGPG_REQUIRE(s.data && out && am && s.C % 4 == 0 && H >= 2 && W >= 2, "maxpool2_fwd");
     const int64_t total = (int64_t)B * (H / 2) * (W / 2) * (s.C / 4);
-    hipLaunchKernelGGL(maxpool2_fwd_kernel, dim3(stream_grid(total)), dim3(256), 0,
-                       as_stream(stream), s.data, s.scale, s.shift, B, H, W, s.C, out, am);
+    if (g_pool_nt)
+        hipLaunchKernelGGL(maxpool2_fwd_kernel<true>, dim3(stream_grid(total)), dim3(256), 0,
+                           as_stream(stream), s.data, s.scale, s.shift, B, H, W, s.C, out, am);
+    else
+        hipLaunchKernelGGL(maxpool2_fwd_kernel<false>, dim3(stream_grid(total)), dim3(256), 0,
+                           as_stream(stream), s.data, s.scale, s.shift, B, H, W, s.C, out, am);
     return check_launch("maxpool2_fwd");
 }
 
