@@ -288,6 +288,11 @@ __global__ void bn_relu_apply_kernel(const float* x, const float* sc, const floa
 
 int g_bn_apply_nt = 1;  // knob "bn_apply_nt": streaming (nontemporal) loads of da and y in the BN-backward apply (step -0.55%)
 int g_bn_fin_auto = 1;
+int g_bn_apply_blocks = 2048;  // tuning knob "bn_apply_blocks": grid cap of the apply
+static unsigned apply_grid(int64_t n4) {
+    int64_t g = cdiv(n4, 256);
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>(g, g_bn_apply_blocks));
+}
 void launch_bn_apply(unsigned ga, hipStream_t st, const float* da, const float* y, int64_t npix,
                      int C, const float* mean, const float* invstd, const float* scale,
                      const float* shift, const float* coef, float* dy) {
@@ -389,7 +394,7 @@ extern "C" int ugpg_bn_relu_bwd(const float* da, const float* y, int64_t npix, i
     if (int e = check_launch("bn_bwd_finalize")) return e;
     // the apply kernel keeps one channel group per thread: grid * 1024 must be a multiple of C
     const unsigned q = (unsigned)(C / std::gcd(1024, C));
-    const unsigned ga = (stream_grid(npix * C / 4) + q - 1) / q * q;
+    const unsigned ga = (apply_grid(npix * C / 4) + q - 1) / q * q;
     launch_bn_apply(ga, st, da, y, npix, C, mean, invstd, scale, shift, coef, dy);
     return check_launch("bn_bwd_apply");
 }
@@ -437,7 +442,7 @@ extern "C" int ugpg_bn_relu_bwd_partials(const float* part, int nslots, const fl
                        scale, dgamma, dbeta, dbias, acc, coef);
     if (int e = check_launch("bn_bwd_finalize")) return e;
     const unsigned q = (unsigned)(C / std::gcd(1024, C));
-    const unsigned ga = (stream_grid(npix * C / 4) + q - 1) / q * q;
+    const unsigned ga = (apply_grid(npix * C / 4) + q - 1) / q * q;
     launch_bn_apply(ga, st, da, y, npix, C, mean, invstd, scale, shift, coef, dy);
     return check_launch("bn_bwd_apply");
 }

@@ -786,7 +786,7 @@ void launch_fwd(const ConvFwdArgs& a, hipStream_t st) {
 using namespace ugpg;
 
 namespace ugpg {
-extern int g_bn_bwd_blocks, g_bn_bwd_ppt, g_bn_fin_auto, g_bn_apply_nt, g_pool_nt, g_x6_cw, g_x6_order, g_x6_img;
+extern int g_bn_bwd_blocks, g_bn_bwd_ppt, g_bn_fin_auto, g_bn_apply_nt, g_bn_apply_blocks, g_pool_nt, g_x6_cw, g_x6_order, g_x6_img;
 }
 
 #ifndef WG_IMG_DEFAULT
@@ -821,6 +821,10 @@ extern "C" int ugpg_set_tuning(const char* key, int value) {
     }
     if (key && std::string(key) == "x6_cw" && (value == 4 || value == 8)) {
         g_x6_cw = value;
+        return UGPG_OK;
+    }
+    if (key && std::string(key) == "bn_apply_blocks" && value >= 64 && value <= 65536) {
+        g_bn_apply_blocks = value;
         return UGPG_OK;
     }
     if (key && std::string(key) == "pool_nt" && (value == 0 || value == 1)) {
