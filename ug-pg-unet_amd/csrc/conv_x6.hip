@@ -2228,6 +2228,8 @@ __global__ void __launch_bounds__(4096 / PX) conv3x3_img_fwd_kernel(ConvFwdArgs 
     __shared__ int nci_s;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int tpi = a.tiles_x * a.tiles_y;
+    // output channels 64*nb .. 64*nb+63 of Cout = 64 * gridDim.y (64 or 128)
+    const int nb = blockIdx.y, n0 = 64 * nb;
     // lazy BN+ReLU of the source (the image itself has none): this thread's 4 channels
     // are fixed (piece q = tid & 1, NT even); zero padding stays zero
     const bool aon = a.sc0 != nullptr;
@@ -2271,7 +2273,7 @@ __global__ void __launch_bounds__(4096 / PX) conv3x3_img_fwd_kernel(ConvFwdArgs 
     unsigned hv;
     halo_fetch(blockIdx.x, hr, hv);
     // weights: pack layout of pack_x6_elem (mode 0, K = 16, nb = 0)
-    const __bf16* wp = static_cast<const __bf16*>(a.wpk);
+    const __bf16* wp = static_cast<const __bf16*>(a.wpk) + (size_t)nb * 3 * 6 * (3 * 64 * 8);
     constexpr int plane = 3 * 64 * 8;
     if (tid == 0) nci_s = 0;
     __syncthreads();
@@ -2282,7 +2284,10 @@ __global__ void __launch_bounds__(4096 / PX) conv3x3_img_fwd_kernel(ConvFwdArgs 
         const float* wf = static_cast<const float*>(a.wpk);
         float pv[NE];
 #pragma unroll
-        for (int k = 0; k < NE; ++k) pv[k] = wf[tid + NT * k];
+        for (int k = 0; k < NE; ++k) {
+            const int e = tid + NT * k, ci = e & 7, co = (e >> 3) & 63, t = e >> 9;
+            pv[k] = wf[((size_t)t * a.Cout + n0 + co) * 8 + ci];
+        }
 #pragma unroll
         for (int k = 0; k < NE; ++k) {
             const int e = tid + NT * k, ci = e & 7, co = (e >> 3) & 63, t = e >> 9;
@@ -2361,8 +2366,9 @@ __global__ void __launch_bounds__(4096 / PX) conv3x3_img_fwd_kernel(ConvFwdArgs 
         f32x4 bv = {0.f, 0.f, 0.f, 0.f};
         if (a.bias)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) bv[i] = a.bias[4 * cq + i];
-        float* orow = a.out0 + ((size_t)(b * a.H + ty0 + row) * a.W + tx0 + c0) * 64 + 4 * cq;
+            for (int i = 0; i < 4; ++i) bv[i] = a.bias[n0 + 4 * cq + i];
+        float* orow =
+            a.out0 + ((size_t)(b * a.H + ty0 + row) * a.W + tx0 + c0) * a.Cout + n0 + 4 * cq;
         float sj[4] = {0.f, 0.f, 0.f, 0.f};
         float v[PX][4];
 #pragma unroll
@@ -2373,10 +2379,10 @@ __global__ void __launch_bounds__(4096 / PX) conv3x3_img_fwd_kernel(ConvFwdArgs 
             v[p][3] = acc[p][1].y + bv[3];
             if (rok && c0 + p < vw) {
 #ifndef IMG_NOSTORE
-                *reinterpret_cast<f32x4*>(orow + (size_t)p * 64) = f32x4{v[p][0], v[p][1], v[p][2], v[p][3]};
+                *reinterpret_cast<f32x4*>(orow + (size_t)p * a.Cout) = f32x4{v[p][0], v[p][1], v[p][2], v[p][3]};
                 if (a.out0_16) {
                     typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
-                    *reinterpret_cast<bf4*>(a.out0_16 + (orow - a.out0) + (size_t)p * 64) =
+                    *reinterpret_cast<bf4*>(a.out0_16 + (orow - a.out0) + (size_t)p * a.Cout) =
                         bf4{(__bf16)v[p][0], (__bf16)v[p][1], (__bf16)v[p][2], (__bf16)v[p][3]};
                 }
 #endif
@@ -2430,9 +2436,9 @@ __global__ void __launch_bounds__(4096 / PX) conv3x3_img_fwd_kernel(ConvFwdArgs 
                 }
                 const int rows2 = min(max(vh - s2 * RPS, 0), RPS);
                 const size_t S = (size_t)NWM * a.ntiles, slot = (size_t)NWM * tile + s2;
-                a.stats[(0 * (size_t)a.Cout + c) * S + slot] = (float)(rows2 * vw);
-                a.stats[(1 * (size_t)a.Cout + c) * S + slot] = sum;
-                a.stats[(2 * (size_t)a.Cout + c) * S + slot] = m2;
+                a.stats[(0 * (size_t)a.Cout + n0 + c) * S + slot] = (float)(rows2 * vw);
+                a.stats[(1 * (size_t)a.Cout + n0 + c) * S + slot] = sum;
+                a.stats[(2 * (size_t)a.Cout + n0 + c) * S + slot] = m2;
             }
         }
         __syncthreads();  // halo buffer swap; wred reuse
@@ -2455,7 +2461,8 @@ int g_x6_img = X6_IMG_DEFAULT;
 #endif  // tuning knob "x6_img": direct fp32 kernel for the image layer
 
 bool img_fwd_eligible(int W, int C0, int C1, int Cout) {
-    return g_x6_img && W >= 32 && C0 == 8 && C1 == 0 && Cout == 64;
+    // PGUNet4's image layer is 3 -> 64, PGUNet3's 3 -> 128 (two 64-channel column blocks)
+    return g_x6_img && W >= 32 && C0 == 8 && C1 == 0 && (Cout == 64 || Cout == 128);
 }
 int img_fwd_slots(int B, int H, int W, int nwm) {
     return nwm * B * (int)cdiv(H, 8) * (int)cdiv(W, 32);
@@ -2471,7 +2478,7 @@ bool launch_img_fwd(const ConvFwdArgs& a, bool wf32, hipStream_t st) {
     int64_t g = std::min<int64_t>(IMG_BPC * (int64_t)cu_count(st), (int64_t)a.ntiles);
     g = std::max<int64_t>(1, g);
     constexpr int PX = IMG_PX;
-    const dim3 grid((unsigned)g), block(4096 / PX);
+    const dim3 grid((unsigned)g, (unsigned)(a.Cout / 64)), block(4096 / PX);
     if (wf32)
         hipLaunchKernelGGL((conv3x3_img_fwd_kernel<2, PX, true>), grid, block, 0, st, a);
     else if (x6r_cw(3) == 8)
