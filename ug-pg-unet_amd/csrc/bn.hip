@@ -288,6 +288,15 @@ __global__ void bn_relu_apply_kernel(const float* x, const float* sc, const floa
 
 int g_bn_apply_nt = 1;  // knob "bn_apply_nt": streaming (nontemporal) loads of da and y in the BN-backward apply (step -0.55%)
 int g_bn_fin_auto = 1;
+// backward finalize: one thread per 8 partial slots, 64..256 (as the forward finalize)
+static int bwd_fin_threads(int64_t nslots) {
+    int nt = 64;
+    if (g_bn_fin_auto)
+        while (nt < 256 && (int64_t)nt * 8 < nslots) nt *= 2;
+    else
+        nt = 256;
+    return nt;
+}
 int g_bn_apply_blocks = 2048;  // tuning knob "bn_apply_blocks": grid cap of the apply
 static unsigned apply_grid(int64_t n4) {
     int64_t g = cdiv(n4, 256);
@@ -389,8 +398,8 @@ extern "C" int ugpg_bn_relu_bwd(const float* da, const float* y, int64_t npix, i
     hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(p.nblk), dim3(256), 0, st, da, y, npix, C, mean,
                        invstd, scale, shift, p.ppb, part, p.nblk);
     if (int e = check_launch("bn_bwd_reduce")) return e;
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, part, p.nblk, C, npix,
-                       scale, dgamma, dbeta, dbias, acc, coef);
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(bwd_fin_threads(p.nblk)), 0, st, part,
+                       p.nblk, C, npix, scale, dgamma, dbeta, dbias, acc, coef);
     if (int e = check_launch("bn_bwd_finalize")) return e;
     // the apply kernel keeps one channel group per thread: grid * 1024 must be a multiple of C
     const unsigned q = (unsigned)(C / std::gcd(1024, C));
@@ -438,8 +447,8 @@ extern "C" int ugpg_bn_relu_bwd_partials(const float* part, int nslots, const fl
     }
     float* coef = static_cast<float*>(ws);
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, part, nslots, C, npix,
-                       scale, dgamma, dbeta, dbias, acc, coef);
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(bwd_fin_threads(nslots)), 0, st,
+                       part, nslots, C, npix, scale, dgamma, dbeta, dbias, acc, coef);
     if (int e = check_launch("bn_bwd_finalize")) return e;
     const unsigned q = (unsigned)(C / std::gcd(1024, C));
     const unsigned ga = (apply_grid(npix * C / 4) + q - 1) / q * q;
