@@ -55,6 +55,10 @@ def parse():
     ap.add_argument("--conv-math", choices=("x6", "bf16", "f32"), default="x6",
                     help="conv arithmetic: x6 = fp32-accurate split-bf16 (configs[1], default); "
                          "bf16 = bf16 operands, fp32 accumulation (configs[2] arithmetic)")
+    ap.add_argument("--workload", choices=("seg", "herlev"), default="seg",
+                    help="seg: the Stage-4 UG segmentation step (BASELINE metric, default); "
+                         "herlev: the Herlev Stage-4 classifier UG step (BASELINE configs[3])")
+    ap.add_argument("--classes", type=int, default=7, help="Herlev classes (--workload herlev)")
     return ap.parse_args()
 
 
@@ -115,6 +119,79 @@ def cpu_baseline(batch, res, steps, thread_counts):
                       f"{' and '.join(str(k) for k in thread_counts)} threads (= physical cores)"}
 
 
+def herlev_gflop(res):
+    """Algorithmic GFLOP per image of the Herlev UG step (at 256^2 the
+    Stage-4 encoder fwd+bwd is 80.18 GF, the Stage-3 prediction at 128^2 19.44 GF; the
+    encoder scales with the pixel count, the Stage-3 input is always 128^2)."""
+    return 80.18 * (res / 256) ** 2 + 19.44
+
+
+def cpu_baseline_herlev(batch, res, steps, thread_counts, classes):
+    """The CPU oracle's Herlev UG step (oracle.ref_cpu.herlev_train_step: the reference's
+    torch CPU ops -- model, dropout, Stage-3 prediction, UG CE, torch.optim.Adam), same
+    protocol as cpu_baseline."""
+    import torch
+    from oracle import detgen as G
+    from oracle import ref_cpu as O
+    spec4 = O.state_spec(4, 3, 1, key_prefix="unet.") + O.herlev_head_spec(512, classes)
+    spec3 = O.state_spec(3, 3, 1, key_prefix="unet.") + O.herlev_head_spec(512, classes)
+    cur0, prev = G.make_state(spec4, 0), G.make_state(spec3, 1)
+    x = G.randn(1, (batch, 3, res, res), "x")
+    y = G.randint(2, (batch,), classes, "y")
+    cw = torch.linspace(0.5, 2.0, classes)
+    rates = {}
+    for threads in thread_counts:
+        torch.set_num_threads(threads)
+        cur = {k: v.clone() for k, v in cur0.items()}
+        params = [v.requires_grad_(True) for k, v in cur.items()
+                  if v.is_floating_point() and not O._is_buffer(k)]
+        opt = torch.optim.Adam(params, lr=1e-4, weight_decay=1e-4)
+        O.herlev_train_step(cur, prev, x, y, opt, num_classes=classes, class_weights=cw)
+        times = []
+        for i in range(steps):
+            t0 = time.perf_counter()
+            O.herlev_train_step(cur, prev, x, y, opt, num_classes=classes, class_weights=cw)
+            times.append(time.perf_counter() - t0)
+            print(f"cpu baseline (herlev): {threads} threads, step {i + 1}/{steps}: "
+                  f"{times[-1]:.2f} s", file=sys.stderr, flush=True)
+        times.sort()
+        rates[threads] = round(batch / times[len(times) // 2], 4)
+    top = max(thread_counts)
+    return {"value": rates[top], "unit": "images/sec", "cores": top, "kind": "port",
+            "by_cores": {str(k): v for k, v in rates.items()},
+            "sample": f"oracle Herlev UG step (bs{batch} {res}^2, {classes} classes: S4 classifier "
+                      f"fwd+bwd with dropout + S3 prediction at 128^2 + UG CE + Adam), torch CPU "
+                      f"fp32, median of {steps} steps after 1 warm-up, at "
+                      f"{' and '.join(str(k) for k in thread_counts)} threads (= physical cores)"}
+
+
+def roofline_from(timer, steps, every, math):
+    """(roofline, kernels) of the live-timed conv launches: the dominant kernel's
+    algorithmic FLOPs / its HIP-event time, against the peak of the arithmetic it runs."""
+    summ = timer.summary()
+    sampled = len(range(0, steps, every))
+    kernels = {k: {"launches": v["launches"], "ms_per_step": round(v["ms"] / sampled, 3),
+                   "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2)}
+               for k, v in summ.items()}
+    dom = max(summ, key=lambda k: summ[k]["ms"])
+    d = summ[dom]
+    achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
+    peak = {"x6": BF16_PEAK_TFLOPS / X6_PRODUCTS, "bf16": BF16_PEAK_TFLOPS}.get(
+        math, FP32_PEAK_TFLOPS)
+    traffic, src = pmc_traffic(dom) if math == "x6" else (None, None)
+    roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2),
+            "peak": round(peak, 1), "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+            "traffic": traffic, "traffic_source": src,
+            "arithmetic": {"x6": "split-bf16 x6: fp32-accurate products from 6 bf16 MFMAs; "
+                                 "peak = dense bf16 MFMA peak / 6",
+                           "bf16": "bf16 operands, fp32 accumulation: dense bf16 MFMA peak"
+                           }.get(math, "fp32 MFMA"),
+            "flops_per_launch": round(d["flops"] / d["launches"]),
+            "avg_launch_ms": round(d["ms"] / d["launches"], 4),
+            "timed_steps": f"{sampled} of {steps} (every {every})"}
+    return roof, kernels
+
+
 def pmc_traffic(family):
     """HBM bytes per launch of a kernel family from the newest committed PMC summary
     (profiles/*_pmc.json, written by tools/pmc_summary.py from separate FETCH_SIZE /
@@ -135,6 +212,8 @@ def pmc_traffic(family):
 def main():
     args = parse()
     args.roofline_every = max(1, args.roofline_every)
+    if args.workload == "herlev":
+        return main_herlev(args)
     import torch
     import torch.distributed as dist
     import ugpg
@@ -230,31 +309,8 @@ def main():
                      "ms_per_step": round(1000 * el2 / args.secondary_steps, 3),
                      "steps": args.secondary_steps}
 
-    roof = None
-    kernels = None
-    if timer is not None:
-        summ = timer.summary()
-        sampled = len(range(0, args.steps, args.roofline_every))
-        kernels = {k: {"launches": v["launches"], "ms_per_step": round(v["ms"] / sampled, 3),
-                       "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2)}
-                   for k, v in summ.items()}
-        dom = max(summ, key=lambda k: summ[k]["ms"])
-        d = summ[dom]
-        achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
-        math = ops.conv_math()
-        peak = {"x6": BF16_PEAK_TFLOPS / X6_PRODUCTS, "bf16": BF16_PEAK_TFLOPS}.get(
-            math, FP32_PEAK_TFLOPS)
-        traffic, src = pmc_traffic(dom) if math == "x6" else (None, None)
-        roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2),
-                "peak": round(peak, 1), "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-                "traffic": traffic, "traffic_source": src,
-                "arithmetic": {"x6": "split-bf16 x6: fp32-accurate products from 6 bf16 MFMAs; "
-                                     "peak = dense bf16 MFMA peak / 6",
-                               "bf16": "bf16 operands, fp32 accumulation: dense bf16 MFMA peak"
-                               }.get(math, "fp32 MFMA"),
-                "flops_per_launch": round(d["flops"] / d["launches"]),
-                "avg_launch_ms": round(d["ms"] / d["launches"], 4),
-                "timed_steps": f"{sampled} of {args.steps} (every {args.roofline_every})"}
+    roof, kernels = (None, None) if timer is None else \
+        roofline_from(timer, args.steps, args.roofline_every, ops.conv_math())
 
     result = {
         "metric": METRIC, "value": round(value, 3), "unit": "images/sec", "n_gpus": world,
@@ -287,6 +343,91 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def main_herlev(args):
+    """BASELINE.json configs[3]: the Herlev Stage-4 classifier uncertainty-guided training
+    step (Herlev/train_herlev.py:298-325 with the UG forward pass :216-296) on one GPU:
+    ugpg's HerlevTrainer.train_step = PGUNet4 encoder + classifier fwd/bwd (dropout
+    active) + the Stage-3 classifier's eval prediction at 128^2 + UG CE + Adam.  bs16
+    synthetic N(0,1) images at --res (224 = the reference's Stage-4 resolution, 256 =
+    BASELINE's), labels ~ U{0..K-1}, random-init weights, fp32 (split-bf16 convs)."""
+    import torch
+    import ugpg  # noqa: F401
+    from ugpg import ops
+    from ugpg.dist import init_from_env, max_over_ranks
+    from ugpg.herlev import HerlevTrainer
+    ops.set_conv_math(args.conv_math)
+    rank, world = init_from_env(os.environ.get("UGPG_DIST_BACKEND", "nccl"))
+    local = int(os.environ.get("UGPG_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    torch.manual_seed(1234)
+    K, B, R = args.classes, args.batch, args.res
+    tr = HerlevTrainer({"device": dev, "epochs_per_stage": 1, "num_classes": K,
+                        "class_weights": torch.linspace(0.5, 2.0, K).tolist(),
+                        "uncertainty_alpha": 1.0, "weight_decay": 1e-4, "stage4_resolution": R})
+    tr.setup_optimizer_scheduler(4)
+    tr.models[4].train()
+    tr.models[3].eval()
+    g = torch.Generator().manual_seed(100 + rank)
+    x = torch.randn(B, 3, R, R, generator=g).to(dev)
+    y = torch.randint(0, K, (B,), generator=g).to(dev)
+
+    def run(n, timer=None):
+        last = None
+        for k in range(n):
+            ops.TIMER = timer if timer is not None and k % args.roofline_every == 0 else None
+            out = tr.train_step(x, y, 4)
+            if last is not None:
+                last.tolist()  # the trainer's per-batch host read, one step behind
+            last = out
+        return last.tolist()
+
+    run(args.warmup)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    timer = None if args.no_roofline else ops.KernelTimer()
+    t0 = time.perf_counter()
+    last = run(args.steps, timer)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0, dev)
+    ops.TIMER = None
+    value = world * B * args.steps / elapsed
+    gf = herlev_gflop(R)
+    roof, kernels = (None, None) if timer is None else \
+        roofline_from(timer, args.steps, args.roofline_every, ops.conv_math())
+    result = {
+        "metric": f"images/sec Herlev Stage-4 classifier UG train step {R}x{R} bs{B}",
+        "value": round(value, 3), "unit": "images/sec", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "bf16" if args.conv_math == "bf16" else "fp32",
+        "data": "synthetic (x~N(0,1), labels~U{0..K-1}; random-init weights)",
+        "config": {"workload": "Herlev Stage-4 classifier UG train step: PGUNet4 encoder + "
+                               "classifier fwd+bwd (dropout) + PGUNet3 classifier eval at 128^2 "
+                               "+ uncertainty-weighted CE + Adam",
+                   "per_gpu_batch": B, "global_batch": B * world, "resolution": R,
+                   "classes": K, "parallelism": f"dp{world}",
+                   "baseline_config": "BASELINE.json configs[3]"},
+        "step_roofline": {"gflop_per_image": round(gf, 3),
+                          "achieved_tflops_per_gpu": round(value / world * gf / 1e3, 2)},
+        "roofline": roof, "kernels": kernels,
+        "last_step_metrics": {"loss": last[0], "base_loss": last[1], "w_mean": last[2],
+                              "w_std": last[3]},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        phys = cpu_cores()
+        result["cpu_baseline"] = cpu_baseline_herlev(B, R, args.cpu_steps,
+                                                     sorted({phys, min(8, phys)}), K)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -35,18 +35,6 @@ extern "C" {
 
 const char* ugpg_version(void);
 const char* ugpg_last_error(void);
-/* Tuning knobs for benchmarking (process-global; not for production use):
- *   "fwd_cfg": force the 3x3 conv tile config (0 = 16x16x64, 1 = 8x16x128,
- *              2 = 8x8x64) where it is legal for the shape; -1 = heuristic.
- *   "x6_pipe": split-bf16 forward/data-gradient form for images >= 32 wide:
- *              2 = persistent warp-specialized, 16x16x32 MFMA tiles (default),
- *              1 = the same with 32x32x16 tiles, 3 = as 2 plus 16x16-pixel items
- *              for images 16-31 wide, 0 = one workgroup per tile.
- *   "x6_wgrad": split-bf16 weight gradient: 1 = persistent warp-specialized
- *              (default), 0 = one workgroup per item.
- *   "x6_probe": timing diagnostics of the single-stage form (bit 0: skip the
- *              in-loop prefetch, bit 1: skip the LDS staging) -- results are wrong. */
-int ugpg_set_tuning(const char* key, int value);
 
 /* A lazily-activated NHWC operand: value = relu(scale[c]*x + shift[c]) when
  * scale != NULL (train/eval BatchNorm + ReLU folded into the consumer's load,
@@ -79,8 +67,12 @@ typedef struct {
  * Output channels [0, out_split) go to out[0] (channel stride out_split) and
  * [out_split, Cout) to out[1] (stride Cout - out_split); out_split == Cout for one
  * output.  accumulate[i] != 0 adds into out[i].  When `stats` != NULL the kernel
- * also writes per-tile BatchNorm partials [3][Cout][ntiles] = (count, sum, M2)
- * for ugpg_bn_finalize. */
+ * also writes per-tile BatchNorm partials [3][Cout][n] = (count, sum, M2) for
+ * ugpg_bn_finalize, n = ugpg_conv3x3_fwd_ntiles(B, H, W, Cin, Cout, wfmt);
+ * `stats_slots` is the buffer's capacity in slots (it holds 3*Cout*stats_slots
+ * floats): a call whose n exceeds it fails with UGPG_ERR_WORKSPACE and writes nothing.
+ * The kernel form, its tiling and hence n depend only on the shape and wfmt (there are
+ * no runtime tuning knobs). */
 typedef struct {
     int B, H, W;
     ugpg_src_t src[2];
@@ -91,6 +83,7 @@ typedef struct {
     int out_split;
     int accumulate[2];
     float* stats;
+    int stats_slots;       /* capacity of stats in slots (see above) */
     int wfmt;              /* UGPG_WFMT_F32, UGPG_WFMT_X6 or UGPG_WFMT_BF16 */
     /* Optional BatchNorm-backward partials of the output, for a data gradient whose
      * output da = dL/d(relu(bn(y))) feeds ugpg_bn_relu_bwd_partials (the reduction half
@@ -98,14 +91,16 @@ typedef struct {
      * != NULL (one output, no accumulate, Cout % 4 == 0) the call also writes
      * bnb_part[3][Cout][slots] = per-slot (sum g, sum g*xhat, sum xhat) with
      * g = da*[scale*y+shift > 0], xhat = (y-mean)*invstd, y = bnb_y (NHWC, Cout
-     * channels), slots = ugpg_conv3x3_fwd_ntiles(...).  Forms whose epilogue does not
-     * fuse it run the reduction as a separate pass with the same layout. */
+     * channels), slots = ugpg_conv3x3_fwd_ntiles(...), which must not exceed bnb_slots
+     * (the capacity of bnb_part in slots; else UGPG_ERR_WORKSPACE).  Forms whose
+     * epilogue does not fuse it run the reduction as a separate pass, same layout. */
     const float* bnb_y;
     const float* bnb_mean;
     const float* bnb_invstd;
     const float* bnb_scale;
     const float* bnb_shift;
     float* bnb_part;
+    int bnb_slots;         /* capacity of bnb_part in slots */
     /* optional bf16 copy of out[0] (one output, no accumulate): written beside it, for
      * the next conv's ugpg_src_t.data_bf16 (the bf16 arithmetic's activation storage) */
     void* out_bf16;
@@ -118,7 +113,7 @@ typedef struct {
 /* Replaces aten::convolution forward (cuDNN/oneDNN) for DoubleConv's 3x3 convs. */
 int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream);
 /* number of BatchNorm partial slots the forward writes (size stats as 3*Cout*ntiles);
- * depends on the forward kernel form (tuning knob "x6_pipe") */
+ * a function of the shape and the weight format only */
 int ugpg_conv3x3_fwd_ntiles(int B, int H, int W, int Cin, int Cout, int wfmt);
 
 /* Weight repack from OIHW fp32 [Cout][Cin][3][3].

@@ -773,6 +773,131 @@ def g11(RU):
     print("wrote g11_checkpoint_interop.json")
 
 
+G12 = dict(n_train=4, n_val=2, bs=2, res=256, epochs=2, x_seed=150, t_seed=151, vx_seed=152,
+           vt_seed=153, w_seeds={1: 161, 2: 162, 3: 163, 4: 164}, p_t=0.3)
+
+
+def g12_data():
+    c = G12
+    x = G.randn(c["x_seed"], (c["n_train"], 3, c["res"], c["res"]), "x")
+    t = G.bernoulli(c["t_seed"], (c["n_train"], 1, c["res"], c["res"]), c["p_t"], "t")
+    vx = G.randn(c["vx_seed"], (c["n_val"], 3, c["res"], c["res"]), "vx")
+    vt = G.bernoulli(c["vt_seed"], (c["n_val"], 1, c["res"], c["res"]), c["p_t"], "vt")
+    return x, t, vx, vt
+
+
+def _g12_trainer(RT):
+    torch.manual_seed(0)
+    tr = RT.UncertaintyGuidedProgressiveTrainer(3, 1, device="cpu", uncertainty_alpha=1.0)
+    for s in range(1, 5):
+        tr.models[s].load_state_dict(det_state(s, 3, 1, seed=G12["w_seeds"][s]))
+        tr.stage_configs[s]["lr"] = 0.0
+        tr.stage_configs[s]["epochs_per_stage"] = G12["epochs"]
+    tr.setup_optimizer(1)
+    return tr
+
+
+def _buffers(model):
+    out = {}
+    for k, v in model.state_dict().items():
+        if O._is_buffer(k):
+            out[k] = v.numpy() if v.is_floating_point() else np.array(int(v))
+    return out
+
+
+def g12(RU):
+    """Config 5 (the progressive 1->4 driver, uncertainty_guided_trainer.py:316-398) run by
+    the reference itself: 4 train + 2 val images of 256^2 (bs2, no shuffle), 2 epochs per
+    stage, every stage lr = 0 -- so only the weight transfers and the BatchNorm running
+    statistics evolve and the trajectory is deterministic (VERDICT r2
+    "next" #1).  Recorded: the full history, every stage model's BatchNorm buffers at the
+    end, and each best-checkpoint's (stage, epoch, val_dice, train_dice)."""
+    import tempfile
+    import uncertainty_guided_trainer as RT  # noqa: E402
+    from torch.utils.data import DataLoader, TensorDataset
+    x, t, vx, vt = g12_data()
+    tr = _g12_trainer(RT)
+    bs = G12["bs"]
+    tl = DataLoader(TensorDataset(x, t), batch_size=bs, shuffle=False)
+    vl = DataLoader(TensorDataset(vx, vt), batch_size=bs, shuffle=False)
+    fx = {}
+    with tempfile.TemporaryDirectory() as d:
+        tr.train_progressive(tl, vl, max_stages=4, save_dir=d)
+        for s in range(1, 5):
+            ck = Path(d) / f"ug_pgunet_stage{s}_best.pth"
+            c = torch.load(ck, weights_only=True)
+            fx[f"ckpt/{s}"] = np.array([c["stage"], c["epoch"], c["val_dice"], c["train_dice"]])
+    for k, v in tr.history.items():
+        fx[f"history/{k}"] = np.array(v, dtype=np.float64)
+    for s in range(1, 5):
+        for k, v in _buffers(tr.models[s]).items():
+            fx[f"buf{s}/{k}"] = v
+    # params never move at lr 0: what the transfers produced is the weight state
+    for s in range(1, 5):
+        for k, v in tr.models[s].state_dict().items():
+            if not O._is_buffer(k):
+                fx[f"wsum{s}/{k}"] = np.array(v.double().sum().item())
+    save_npz("g12_progressive.npz", **fx)
+
+
+def g12b(RU):
+    """Config 5 under 2-rank data parallelism with local BatchNorm, driven
+    through the reference's own trainer methods: the global bs2 batches split into one
+    image per rank; rank 0's model (the one whose BatchNorm buffers every rank adopts
+    before validation and at each stage end) is the reference trained on shard 0; the
+    train tuple is the shard mean of the reference's per-shard metrics with U statistics
+    pooled over the global batch; validation is the reference's validate_epoch of rank
+    0's model on the whole val set.  lr = 0 as in G12."""
+    import uncertainty_guided_trainer as RT  # noqa: E402
+    from torch.utils.data import DataLoader, TensorDataset
+    x, t, vx, vt = g12_data()
+    tr = _g12_trainer(RT)
+    S, bs = 2, G12["bs"]
+    vl = DataLoader(TensorDataset(vx, vt), batch_size=bs, shuffle=False)
+    shard = [DataLoader(TensorDataset(x[r::S], t[r::S]), batch_size=bs // S, shuffle=False)
+             for r in range(S)]
+    hist = {k: [] for k in tr.history}
+    for stage in range(1, 5):
+        if stage > 1:
+            tr.transfer_weights(stage - 1, stage)
+        tr.current_stage, tr.current_model = stage, tr.models[stage]
+        tr.setup_optimizer(stage)
+        hist["stage_transitions"].append(len(hist["train_loss"]))
+        res = O.STAGE_RES[stage]
+        for _ in range(G12["epochs"]):
+            keep = {k: v.clone() for k, v in tr.models[stage].state_dict().items()}
+            rows = []
+            for r in range(S - 1, -1, -1):  # rank 0 last: its BN buffers are the ones kept
+                tr.models[stage].load_state_dict(keep)
+                rows.append(tr.train_epoch(shard[r], stage))
+            rows = np.array(rows)
+            # U statistics of each GLOBAL batch (pooled over ranks), averaged over batches
+            um, us = 0.0, 0.0
+            if stage > 1:
+                nb = 0
+                for i in range(0, x.shape[0], bs):
+                    d = torch.nn.functional.interpolate(x[i:i + bs], size=(res, res),
+                                                        mode="bilinear", align_corners=True)
+                    u = tr.uncertainty_loss.generate_uncertainty_map(
+                        d, tr.models[stage - 1], O.STAGE_RES[stage - 1], res)
+                    um, us, nb = um + u.mean().item(), us + u.std().item(), nb + 1
+                um, us = um / nb, us / nb
+            tup = list(rows[:, :4].mean(axis=0)) + [um, us]
+            va = tr.validate_epoch(vl, stage)
+            hist["train_loss"].append(tup[0])
+            hist["val_loss"].append(va[0])
+            hist["train_dice"].append(tup[2])
+            hist["val_dice"].append(va[2])
+            hist["uncertainty_weights_mean"].append(va[4])
+            hist["uncertainty_weights_std"].append(va[5])
+            hist["base_loss"].append(va[1])
+    fx = {f"history/{k}": np.array(v, dtype=np.float64) for k, v in hist.items()}
+    for s in range(1, 5):
+        for k, v in _buffers(tr.models[s]).items():
+            fx[f"buf{s}/{k}"] = v
+    save_npz("g12b_progressive_dp2.npz", **fx)
+
+
 def g0(RU):
     """state_dict keys/shapes/dtypes of every reference model (checkpoint format)."""
     out = {}

@@ -438,6 +438,28 @@ def herlev_ug_loss(logits, target, prev_logits, alpha, num_classes, class_weight
     return final, base, w
 
 
+def herlev_train_step(P_cur, P_prev, x, target, opt, alpha=1.0, num_classes=7,
+                      class_weights=None, prev_res=128):
+    """One HerlevTrainer training step (train_herlev.py:298-325 with the UG forward pass
+    :216-296): Stage-4 classifier forward in train mode (dropout 0.5/0.3/0.2 drawn from
+    torch's RNG, as nn.Dropout), the Stage-3 classifier in eval mode on the input resized
+    to `prev_res`, the uncertainty-weighted CE, backward, and `opt.step()` (the caller's
+    torch.optim.Adam over P_cur's parameters).  The CPU-baseline workload of
+    bench.py --workload herlev; returns (final, base)."""
+    params = [v for k, v in P_cur.items() if v.is_floating_point() and not _is_buffer(k)]
+    opt.zero_grad()
+    masks = [(torch.rand(x.shape[0], n) >= p).float() / (1 - p)
+             for n, p in ((512, 0.5), (512, 0.3), (256, 0.2))]
+    logits = herlev_forward(4, P_cur, x, training=True, dropout_masks=masks)
+    with torch.no_grad():
+        prev = herlev_forward(3, P_prev, resize_bilinear(x, prev_res), training=False)
+    final, base, _ = herlev_ug_loss(logits, target, prev, alpha, num_classes, class_weights)
+    final.backward()
+    opt.step()
+    del params
+    return final.item(), base.item()
+
+
 # ---------------------------------------------------------------------------
 # Inference / evaluation (MoNuSegImprove/test_monuseg.py)
 # ---------------------------------------------------------------------------

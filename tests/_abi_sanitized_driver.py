@@ -25,6 +25,34 @@ def bad_value(t):
     return None  # pointers, including POINTER(struct)
 
 
+def undersized_partial_buffers(lib):
+    """BatchNorm partial buffers whose capacity (ugpg_conv_t.stats_slots / bnb_slots) is
+    below the slot count the call would write are refused with UGPG_ERR_WORKSPACE before
+    any launch (the fault VERDICT r2 traced to an undersized bnb_part).  The pointers are
+    never dereferenced on the host, so stand-in addresses suffice."""
+    fake = 0x100000
+    d = _C.ConvDesc()
+    d.B, d.H, d.W = 2, 32, 32
+    d.src[0] = _C.Src(fake, None, None, 64, None)
+    d.wpk, d.Cout, d.out_split, d.wfmt = fake, 64, 64, 1  # UGPG_WFMT_X6
+    d.out[0] = fake
+    need = lib.ugpg_conv3x3_fwd_ntiles(2, 32, 32, 64, 64, 1)
+    assert need == 16, need  # 2 images x 4 tiles of 8 x 32 x 2 pixel halves
+    d.stats, d.stats_slots = fake, need - 1
+    assert lib.ugpg_conv3x3_fwd(C.byref(d), None) == -3
+    assert b"stats holds 15 slots" in lib.ugpg_last_error(), lib.ugpg_last_error()
+    d.stats, d.stats_slots = None, 0
+    d.bnb_y = d.bnb_mean = d.bnb_invstd = d.bnb_scale = d.bnb_shift = fake
+    d.bnb_part, d.bnb_slots = fake, 0
+    assert lib.ugpg_conv3x3_fwd(C.byref(d), None) == -3
+    assert b"bnb_part holds 0 slots" in lib.ugpg_last_error()
+    # stats with two outputs are refused (their slot count would depend on the split)
+    d.bnb_part = None
+    d.stats, d.stats_slots, d.out_split, d.Cout = fake, 1 << 20, 64, 128
+    d.out[1] = fake
+    assert lib.ugpg_conv3x3_fwd(C.byref(d), None) == -1
+
+
 def main():
     lib = _C.lib.load()
     assert _C.version().startswith("ugpg ")
@@ -46,16 +74,13 @@ def main():
         assert msg, f"{name}: no error message"
         checked += 1
     # a few targeted cases around the accepted range
-    assert lib.ugpg_set_tuning(b"no_such_knob", 1) < 0
+    undersized_partial_buffers(lib)
     buf = (C.c_ubyte * 8)()
     assert lib.ugpg_comm_unique_id(buf, 8) < 0 and b"comm_unique_id" in lib.ugpg_last_error()
     assert lib.ugpg_comm_destroy(None) == 0
     x = (C.c_float * 40)()
     assert lib.ugpg_metrics_pack(x, 40, -1, 1.0, None, None) < 0       # n > 32
     assert lib.ugpg_metrics_unpack(None, 8, 5, 0xF, x, None) < 0
-    long_name = b"k" * 5000                                                   # message buffer bound
-    lib.ugpg_set_tuning(long_name, 1)
-    assert len(lib.ugpg_last_error()) < 5000
     print(f"sanitized ABI driver: {checked} entries refused invalid arguments")
 
 

@@ -183,8 +183,15 @@ def _replica_worker(rank, port, outdir):
     samp = DataLoader(ds, batch_size=2, sampler=DistributedSampler(ds, WORLD, rank, shuffle=False))
     (xs, ys), *_ = list(samp)
     through = shard_batch(samp, xs, ys)
+    checked = shard_batch(plain, x, y, check=True)  # same global batch: passes
+    try:  # per-rank data (e.g. a per-rank seed without a DistributedSampler): refused
+        shard_batch(plain, x + rank, y, check=True)
+        mismatch = None
+    except RuntimeError as e:
+        mismatch = str(e)
     torch.save({"sums": sums, "part": part[0].view(-1).tolist(), "tiny": tiny,
-                "through": torch.equal(through[0], xs)}, os.path.join(outdir, f"r{rank}.pt"))
+                "through": torch.equal(through[0], xs), "checked": checked[0].view(-1).tolist(),
+                "mismatch": mismatch}, os.path.join(outdir, f"r{rank}.pt"))
     dist.destroy_process_group()
 
 
@@ -196,6 +203,8 @@ def test_trainers_start_from_rank0_weights_and_shard_batches():
     assert r[0]["part"] == [0.0, 1.0] and r[1]["part"] == [2.0, 3.0]
     assert r[0]["tiny"] is None and r[1]["tiny"] is None
     assert r[0]["through"] and r[1]["through"]
+    assert r[0]["checked"] == [0.0, 1.0] and r[1]["checked"] == [2.0, 3.0]
+    assert all("different global batches" in (x["mismatch"] or "") for x in r)
 
 
 def _mixed_worker(rank, port, outdir):

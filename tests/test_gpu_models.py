@@ -165,6 +165,37 @@ def test_trainer_epoch_golden(dev):
         assert abs(tup[4] - ref[4]) <= 1e-5 and abs(tup[5] - ref[5]) <= 1e-5
 
 
+@pytest.mark.parametrize("reduction", ["mean", "sum"])
+def test_trainer_epoch_reduced_criterion(dev, reduction):
+    """A subclass-style base_criterion with reduction='mean'/'sum' (not the fused kernel):
+    the epoch tuple's losses come from the trainer's device metrics buffer, which every
+    loss path must fill."""
+    import torch.nn as nn
+    from torch.utils.data import DataLoader, TensorDataset
+    import ugpg
+    stage, res = 2, 64
+    tr = ugpg.UncertaintyGuidedProgressiveTrainer(3, 1, device=dev, uncertainty_alpha=1.0)
+    states = {s: det_state(s, 3, 1, seed=60 + s) for s in (1, 2)}
+    for s in (1, 2):
+        tr.models[s].load_state_dict(states[s])
+    tr.base_criterion = nn.BCEWithLogitsLoss(pos_weight=torch.tensor([5.0], device=dev),
+                                             reduction=reduction)
+    tr.current_stage, tr.current_model = stage, tr.models[stage]
+    tr.setup_optimizer(stage)
+    x = G.randn(61, (4, 3, res, res), "x")
+    t = G.bernoulli(62, (4, 1, res, res), 0.5, "t")
+    tup = tr.train_epoch(DataLoader(TensorDataset(x, t), batch_size=4), stage)
+    P = {k: v.clone() for k, v in states[stage].items()}
+    with torch.no_grad():
+        logits = O.pgunet_forward(stage, P, x, training=True)
+        u = O.uncertainty_map(1, states[1], x, 32, 64)
+        crit = nn.BCEWithLogitsLoss(pos_weight=torch.tensor([5.0]), reduction=reduction)
+        final, base = O.weighted_loss(crit(logits, t), u, 1.0)
+    assert tup[0] != 0.0 and tup[1] != 0.0
+    assert abs(tup[0] - final.item()) <= 1e-5 * abs(final.item()), (tup, final.item())
+    assert abs(tup[1] - base) <= 1e-5 * abs(base), (tup, base)
+
+
 def test_train_progressive_pipeline(dev, tmp_path):
     """Config 5 in miniature: stages 1->4 with weight transfer, U-map from stage s-1,
     validation, best-Dice checkpoints in the reference's dict format."""

@@ -71,29 +71,16 @@ CONV_CASES = [
 BIG = {5, 6, 7}
 
 
-# x6 kernel forms: (x6_pipe, x6_wgrad) tuning knobs.  Default = persistent
-# warp-specialized forward/dgrad with 16x16x32 MFMA tiles (8 x 16-pixel items for images
-# 16-31 wide) and persistent wgrad; "x6q" the same without the 16-wide items; "x6w" the
-# forward/dgrad form with 32x32x16 tiles; "x6t" 16x16-pixel items for images 16-31 wide;
-# "x6p" the paired 16x16x32 weight gradient; "x6s" one workgroup per tile/item.
-X6_FORMS = {"x6": (4, 1), "x6q": (2, 1), "x6w": (1, 1), "x6t": (3, 1), "x6p": (4, 2), "x6s": (0, 0)}
-X6_DEFAULT = X6_FORMS["x6"]
-
-
-@pytest.fixture(params=["x6", "x6q", "x6w", "x6t", "x6p", "x6s", "f32", "bf16"])
+@pytest.fixture(params=["x6", "f32", "bf16"])
 def math(request):
-    """Every conv arithmetic form: split-bf16 (default, every kernel form), fp32
-    MFMA, and bf16 (BASELINE config 3: operands rounded to bf16, fp32 accumulation)."""
+    """Every conv arithmetic form: split-bf16 (default), fp32 MFMA, and bf16 (BASELINE
+    config 3: operands rounded to bf16, fp32 accumulation).  The kernel form within an
+    arithmetic is chosen by shape alone; CONV_CASES covers every form (persistent 8 x 32
+    and 8 x 16 items, the single-stage kernel, the direct image-layer kernel)."""
     from ugpg import ops
-    from ugpg._C import lib
     old = ops.conv_math()
-    ops.set_conv_math({"f32": "f32", "bf16": "bf16"}.get(request.param, "x6"))
-    pipe, wgrad = X6_FORMS.get(request.param, X6_DEFAULT)
-    lib.ugpg_set_tuning(b"x6_pipe", pipe)
-    lib.ugpg_set_tuning(b"x6_wgrad", wgrad)
+    ops.set_conv_math(request.param)
     yield request.param
-    lib.ugpg_set_tuning(b"x6_pipe", X6_DEFAULT[0])
-    lib.ugpg_set_tuning(b"x6_wgrad", X6_DEFAULT[1])
     ops.set_conv_math(old)
 
 

@@ -3,10 +3,11 @@ bench's workload, alternating blocks of steps between two settings so that clock
 (DVFS, temperature) hits both sides alike.
 
     python tools/ab_step.py --a "engine._FUSE_BN_BWD=0" --b "engine._FUSE_BN_BWD=1"
-    python tools/ab_step.py --a "tune:x6_img=0" --b "tune:x6_img=1"
+    python tools/ab_step.py --a "lib:exp/a.so" --b "lib:exp/b.so"
 
 A setting is `module._NAME=value` (an attribute of ugpg.<module>, int-valued) or
-`tune:key=value` (ugpg_set_tuning); several comma-separated.
+`lib:path` (a libugpg build, e.g. a `build.py -D ... --out` variant); several
+comma-separated.
 """
 import argparse
 import os
@@ -19,14 +20,26 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path[:0] = [str(ROOT), str(ROOT / "ug-pg-unet_amd")]
 
 
+_LIBS = {}
+
+
 def apply(setting):
+    import ctypes
     import importlib
-    from ugpg._C import lib
+    from ugpg import _C
     for item in filter(None, setting.split(",")):
-        k, v = item.split("=")
-        if k.startswith("tune:"):
-            assert lib.ugpg_set_tuning(k[5:].encode(), int(v)) == 0, item
+        if item.startswith("lib:"):  # swap the library every ugpg op calls through
+            path = str(Path(item[4:]).resolve())
+            if path not in _LIBS:
+                L = ctypes.CDLL(path)
+                for name, (res, args) in _C.SIGNATURES.items():
+                    fn = getattr(L, name, None)
+                    if fn is not None:
+                        fn.restype, fn.argtypes = res, args
+                _LIBS[path] = L
+            _C.lib._lib = _LIBS[path]
         else:
+            k, v = item.split("=")
             mod, attr = k.split(".")
             m = importlib.import_module(f"ugpg.{mod}")
             assert hasattr(m, attr), item

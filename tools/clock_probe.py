@@ -28,7 +28,6 @@ def main():
     ap.add_argument("--layers", default="inc.3,down1.3,down2.3,up4.0")
     ap.add_argument("--seconds", type=float, default=2.0)
     ap.add_argument("--stamps", action="store_true")
-    ap.add_argument("--pipes", default="2")
     ap.add_argument("--wgrad", action="store_true", help="time the weight gradient instead")
     ap.add_argument("--math", default="x6", help="conv arithmetic (x6 / bf16)")
     a = ap.parse_args()
@@ -50,8 +49,7 @@ def main():
         flops = 2.0 * B * H * H * Cout * 9 * (C0 + C1)
         dy = torch.randn(B, H, H, Cout, device=dev)
         dw = torch.empty_like(w)
-        for pipe in a.pipes.split(","):
-            lib.ugpg_set_tuning(b"x6_pipe", int(pipe))
+        for pipe in ("default",):
             n, t0 = 0, time.perf_counter()
             while time.perf_counter() - t0 < a.seconds:
                 for _ in range(20):
@@ -72,9 +70,8 @@ def main():
             else:
                 what = "loader vm_wait/barrier per phase " + " ".join(
                     f"p{q}:{v[q]:.1%}/{v[3 + q]:.1%}" for q in range(3))
-            print(f"{name} pipe {pipe}: {dt*1e3:.3f} ms/launch {flops/dt/1e12:.0f} TF  {what} "
+            print(f"{name}: {dt*1e3:.3f} ms/launch {flops/dt/1e12:.0f} TF  {what} "
                   f"(median of {nwg} workgroups)", flush=True)
-        lib.ugpg_set_tuning(b"x6_pipe", 2)
 
 
 if __name__ == "__main__":

@@ -1,8 +1,11 @@
 """Per-layer conv kernel micro-benchmark (Stage-4, bs16) -- all variants in one
 process, interleaved rounds (cdna_hip_programming.md §5.4 rule 24).
 
-    python tools/conv_bench.py [--rounds 3] [--cfgs -1,0,1,2] [--wgrad]
+    python tools/conv_bench.py [--rounds 3] [--maths x6,bf16,f32] [--wgrad]
     python tools/conv_bench.py --libs exp/a.so,exp/b.so ...   (A/B of builds, one process)
+
+Kernel variants are A/B'd as separate builds (`build.py -D ... --out`, then --libs): the
+library has no runtime tuning knobs.
 """
 import argparse
 import sys
@@ -53,19 +56,14 @@ def timeit(fn, iters=5):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--cfgs", default="-1", help="fp32 tile configs (-1 = heuristic)")
     ap.add_argument("--maths", default="x6,f32")
-    ap.add_argument("--pipes", default="4", help="x6 forward forms to time (x6_pipe knob)")
     ap.add_argument("--wgrad", action="store_true")
-    ap.add_argument("--orders", default="0", help="x6r item orders to time (x6_order knob)")
-    ap.add_argument("--cws", default="4", help="x6r compute waves to time (x6_cw knob: 4, 8)")
     ap.add_argument("--layers", default="", help="comma-separated layer names (default: all)")
     ap.add_argument("--nostats", action="store_true", help="forward without BatchNorm partials")
     ap.add_argument("--libs", default="", help="comma-separated libugpg builds to compare")
     a = ap.parse_args()
     libs = [(Path(p).stem, load_lib(p)) for p in a.libs.split(",")] if a.libs else [("", None)]
     dev = torch.device("cuda:0")
-    cfgs = [int(c) for c in a.cfgs.split(",")]
     rows = {}
     sel = set(a.layers.split(",")) if a.layers else None
     for name, H, C0, C1, Cout in LAYERS:
@@ -90,36 +88,22 @@ def main():
             wpk = ops.pack_conv3x3(w, ops.conv_pack_k(cin), 0)
             wpk1 = ops.pack_conv3x3(w, real_cin, 1) if real_cin % 64 == 0 else None
             nt = ops.conv_ntiles(B, H, H, cin, Cout, wpk)
-            # BatchNorm partial slots: the 8-compute-wave form writes twice as many per tile
-            # (ugpg_conv3x3_fwd_ntiles at x6_cw = 8); size for the largest variant timed
-            st = torch.empty(3 * Cout * nt * (2 if "8" in a.cws.split(",") else 1), device=dev)
-            variants = [(c, 1, 0, 4) for c in cfgs] if m == "f32" else \
-                [(-1, int(pp), int(o), int(w)) for pp in a.pipes.split(",") for o in a.orders.split(",")
-                 for w in a.cws.split(",")]
-            for c, pipe, order, cw in (v if len(v) == 4 else v + (4,) for v in variants):
-                tag = (m if c == -1 else f"{m}{c}") + (f"p{pipe}" if m == "x6" and "," in a.pipes else "") \
-                    + (f"o{order}" if "," in a.orders else "") + (f"w{cw}" if "," in a.cws else "")
+            st = torch.empty(3 * Cout * nt, device=dev)
 
-                def f(c=c, wpk=wpk, st=st, pipe=pipe, order=order, cw=cw):
-                    lib.ugpg_set_tuning(b"fwd_cfg", c)
-                    lib.ugpg_set_tuning(b"x6_pipe", pipe)
-                    lib.ugpg_set_tuning(b"x6_order", order)
-                    lib.ugpg_set_tuning(b"x6_cw", cw)
-                    ops.conv3x3_fwd(srcs, wpk, bias, Cout, [out], stats=None if a.nostats else st)
-                fns[f"fwd_{tag}"] = f
-                if wpk1 is not None:
-                    dy = torch.randn(B, H, H, Cout, device=dev)
-                    d0 = torch.empty(B, H, H, C0, device=dev)
-                    d1 = torch.empty(B, H, H, C1, device=dev) if C1 else None
+            def f(m=m, wpk=wpk, st=st):
+                ops.set_conv_math(m)
+                ops.conv3x3_fwd(srcs, wpk, bias, Cout, [out], stats=None if a.nostats else st)
+            fns[f"fwd_{m}"] = f
+            if wpk1 is not None:
+                dy = torch.randn(B, H, H, Cout, device=dev)
+                d0 = torch.empty(B, H, H, C0, device=dev)
+                d1 = torch.empty(B, H, H, C1, device=dev) if C1 else None
 
-                    def g(c=c, wpk1=wpk1, dy=dy, d0=d0, d1=d1, pipe=pipe, order=order, cw=cw):
-                        lib.ugpg_set_tuning(b"fwd_cfg", c)
-                        lib.ugpg_set_tuning(b"x6_pipe", pipe)
-                        lib.ugpg_set_tuning(b"x6_order", order)
-                        lib.ugpg_set_tuning(b"x6_cw", cw)
-                        ops.conv3x3_fwd([ops.Act(dy)], wpk1, None, real_cin,
-                                        [d0, d1] if C1 else [d0], split=C0 if C1 else None)
-                    fns[f"dgrad_{tag}"] = g
+                def g(m=m, wpk1=wpk1, dy=dy, d0=d0, d1=d1):
+                    ops.set_conv_math(m)
+                    ops.conv3x3_fwd([ops.Act(dy)], wpk1, None, real_cin,
+                                    [d0, d1] if C1 else [d0], split=C0 if C1 else None)
+                fns[f"dgrad_{m}"] = g
         ops.set_conv_math("x6")
         if a.wgrad:
             dy = torch.randn(B, H, H, Cout, device=dev)
@@ -143,10 +127,6 @@ def main():
                     res[k].append(timeit(f))
                 except RuntimeError as e:
                     res[k].append(float("nan"))
-        lib.ugpg_set_tuning(b"fwd_cfg", -1)
-        lib.ugpg_set_tuning(b"x6_pipe", 4)
-        lib.ugpg_set_tuning(b"x6_order", 0)
-        lib.ugpg_set_tuning(b"x6_cw", 4)
         ops.set_conv_math("x6")
         rows[name] = {k: (min(v), flops / (min(v) * 1e-3) / 1e12) for k, v in res.items()}
         print(name, " ".join(f"{k}={v[0]:.3f}ms/{v[1]:.0f}TF" for k, v in rows[name].items()),

@@ -44,10 +44,8 @@ if __name__ == "__main__" and (len(sys.argv) < 2 or sys.argv[1] not in ("bn", "h
     main()
 
 
-def bn_main(knobs):
-    """BatchNorm+ReLU backward (reduce, finalize, apply) at the 8 Stage-4 layer shapes;
-    `knobs`: list of (name, {tuning key: value}) to A/B in one process."""
-    from ugpg._C import lib
+def bn_main():
+    """BatchNorm+ReLU backward (reduce, finalize, apply) at the 8 Stage-4 layer shapes."""
     dev = torch.device("cuda:0")
     B = 16
     tot = {}
@@ -60,9 +58,7 @@ def bn_main(knobs):
         scale, shift = torch.rand(c, device=dev) + 0.5, torch.randn(c, device=dev) * 0.1
         dg, dbt, dbias = (torch.empty(c, device=dev) for _ in range(3))
         line = []
-        for name, kv in knobs:
-            for k, v in kv.items():
-                lib.ugpg_set_tuning(k.encode(), v)
+        for name in ("bn_bwd",):
             us = timeit(lambda: ops.bn_relu_bwd(da, y, mean, invstd, scale, shift, dy, dg, dbt, dbias))
             gb = 5 * y.numel() * 4 / (us * 1e-6) / 1e9
             tot[name] = tot.get(name, 0.0) + 2 * us
@@ -72,8 +68,7 @@ def bn_main(knobs):
 
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "bn":
-    bn_main([("old", {"bn_bwd_blocks": 1024, "bn_bwd_ppt": 32}), ("new", {"bn_bwd_blocks": 2048, "bn_bwd_ppt": 4}),
-             ("p8", {"bn_bwd_blocks": 2048, "bn_bwd_ppt": 8}), ("b4096", {"bn_bwd_blocks": 4096, "bn_bwd_ppt": 2})])
+    bn_main()
 
 
 def heads_main():

@@ -712,12 +712,7 @@ int64_t fwd_blocks(int cfg, int B, int H, int W, int Cout) {
     return (int64_t)B * cdiv(H, s.th) * cdiv(W, s.tw) * (Cout / s.bn);
 }
 
-int g_force_fwd_cfg = -1;  // tuning knob (ugpg_set_tuning("fwd_cfg", k)); -1 = heuristic
-
 int pick_fwd_cfg(int B, int H, int W, int Cout, int split) {
-    if (g_force_fwd_cfg >= 0 && g_force_fwd_cfg < NUM_CFG && Cout % kFwd[g_force_fwd_cfg].bn == 0 &&
-        split % kFwd[g_force_fwd_cfg].bn == 0)
-        return g_force_fwd_cfg;
     // prefer the larger tiles while they still give >= 2 blocks per CU; a block
     // must not straddle the output split (its BN must divide `split`)
     const int64_t want = 512;
@@ -785,76 +780,6 @@ void launch_fwd(const ConvFwdArgs& a, hipStream_t st) {
 
 using namespace ugpg;
 
-namespace ugpg {
-extern int g_bn_bwd_blocks, g_bn_bwd_ppt, g_bn_fin_auto, g_bn_apply_nt, g_bn_apply_blocks, g_pool_nt, g_x6_cw, g_x6_order, g_x6_img;
-}
-
-#ifndef WG_IMG_DEFAULT
-#define WG_IMG_DEFAULT 1
-#endif
-static int g_wg_img = WG_IMG_DEFAULT;  // tuning knob "wg_img": conv3x3_wgrad_img_kernel
-
-extern "C" int ugpg_set_tuning(const char* key, int value) {
-    if (key && std::string(key) == "fwd_cfg") {
-        g_force_fwd_cfg = value;
-        return UGPG_OK;
-    }
-    if (key && std::string(key) == "x6_pipe") {
-        g_x6_pipe = value;
-        return UGPG_OK;
-    }
-    if (key && std::string(key) == "x6_wgrad") {
-        g_x6_wgrad = value;
-        return UGPG_OK;
-    }
-    if (key && std::string(key) == "wg_img" && (value == 0 || value == 1)) {
-        g_wg_img = value;
-        return UGPG_OK;
-    }
-    if (key && std::string(key) == "x6_img" && (value == 0 || value == 1)) {
-        g_x6_img = value;
-        return UGPG_OK;
-    }
-    if (key && std::string(key) == "x6_order" && (value == 0 || value == 1)) {
-        g_x6_order = value;
-        return UGPG_OK;
-    }
-    if (key && std::string(key) == "x6_cw" && (value == 4 || value == 8)) {
-        g_x6_cw = value;
-        return UGPG_OK;
-    }
-    if (key && std::string(key) == "bn_apply_blocks" && value >= 64 && value <= 65536) {
-        g_bn_apply_blocks = value;
-        return UGPG_OK;
-    }
-    if (key && std::string(key) == "pool_nt" && (value == 0 || value == 1)) {
-        g_pool_nt = value;
-        return UGPG_OK;
-    }
-    if (key && std::string(key) == "bn_apply_nt" && (value == 0 || value == 1)) {
-        g_bn_apply_nt = value;
-        return UGPG_OK;
-    }
-    if (key && std::string(key) == "bn_fin_auto" && (value == 0 || value == 1)) {
-        g_bn_fin_auto = value;
-        return UGPG_OK;
-    }
-    if (key && std::string(key) == "bn_bwd_blocks" && value > 0) {
-        g_bn_bwd_blocks = value;
-        return UGPG_OK;
-    }
-    if (key && std::string(key) == "bn_bwd_ppt" && value > 0) {
-        g_bn_bwd_ppt = value;
-        return UGPG_OK;
-    }
-    if (key && std::string(key) == "x6_probe") {  // timing diagnostics; results are wrong
-        g_x6_probe = value;
-        return UGPG_OK;
-    }
-    set_error("set_tuning: unknown key '%s'", key ? key : "(null)");
-    return UGPG_ERR_INVALID;
-}
-
 extern "C" int ugpg_conv3x3_fwd_ntiles(int B, int H, int W, int Cin, int Cout, int wfmt) {
     if (wfmt == UGPG_WFMT_X6 || wfmt == UGPG_WFMT_BF16) {
         const int np = wfmt == UGPG_WFMT_X6 ? 3 : 1;
@@ -901,9 +826,26 @@ extern "C" int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream) {
                   "one output and no accumulate");
         return UGPG_ERR_INVALID;
     }
+    if (p->stats && (p->out_split != p->Cout || p->accumulate[0])) {
+        set_error("conv3x3_fwd: BatchNorm partials (stats) need one output and no accumulate");
+        return UGPG_ERR_INVALID;
+    }
+    // the caller's partial buffers must hold every slot the launched form writes (the
+    // form, hence the slot count, is a function of the shape and wfmt only)
+    if (p->stats || bnb) {
+        const int need = ugpg_conv3x3_fwd_ntiles(p->B, p->H, p->W, Cin, p->Cout, p->wfmt);
+        if (p->stats && p->stats_slots < need) {
+            set_error("conv3x3_fwd: stats holds %d slots, this call writes %d", p->stats_slots,
+                      need);
+            return UGPG_ERR_WORKSPACE;
+        }
+        if (bnb && p->bnb_slots < need) {
+            set_error("conv3x3_fwd: bnb_part holds %d slots, this call writes %d", p->bnb_slots,
+                      need);
+            return UGPG_ERR_WORKSPACE;
+        }
+    }
     ConvFwdArgs a;
-    a.probe = 0;
-    a.order = 0;
     a.bnb_y = p->bnb_y;
     a.bnb_mean = p->bnb_mean;
     a.bnb_invstd = p->bnb_invstd;
@@ -1075,7 +1017,7 @@ static int wgrad_check(const ugpg_wgrad_t* p) {
 enum WgradKind { WG_GENERIC, WG_C8, WG_X6, WG_IMG };
 
 static WgradKind wgrad_kind(const ugpg_wgrad_t* p, int C0, int C1) {
-    if (g_wg_img && C1 == 0 && C0 == 8 && !p->db && !p->src[0].scale && p->Cout == 64 &&
+    if (C1 == 0 && C0 == 8 && !p->db && !p->src[0].scale && p->Cout == 64 &&
         p->Cin_real > 0 && p->Cin_real <= WGI_NCI)
         return WG_IMG;
     if (wgrad_use_c8(C0, C1, p->db)) return WG_C8;
@@ -1097,13 +1039,10 @@ static WgradPlan wgrad_plan_for(const ugpg_wgrad_t* p, WgradKind k, int Cin) {
         return w;
     }
     if (k == WG_X6) {
-        // bf16 (1 piece) always runs the persistent kernel
-        const bool persist = g_x6_wgrad || p->math == UGPG_WFMT_BF16;
-        WgradPlan w = wgrad_plan(p->B, p->H, p->W, Cin, p->Cout, persist ? WGX6W_TH : WGX6_TH,
-                                 WGX6_TW);
+        WgradPlan w = wgrad_plan(p->B, p->H, p->W, Cin, p->Cout, WGX6W_TH, WGX6_TW);
         // persistent kernel: about one item per CU, planned for the MI355X's 256 CUs
         // (a fixed count keeps the split, hence the summation order, device-independent)
-        if (persist) wgrad_x6w_plan(w.ntiles, p->Cout, Cin, 256, w.nsplit, w.tps);
+        wgrad_x6w_plan(w.ntiles, p->Cout, Cin, 256, w.nsplit, w.tps);
         return w;
     }
     return wgrad_plan(p->B, p->H, p->W, Cin, p->Cout);
@@ -1153,8 +1092,7 @@ extern "C" int ugpg_conv3x3_wgrad(const ugpg_wgrad_t* p, void* ws, size_t ws_byt
     a.tps = w.tps;
     hipStream_t st = as_stream(stream);
     if (kind == WG_X6) {
-        launch_wgrad_x6(a, (unsigned)((p->Cout / 64) * (Cin / 64) * w.nsplit),
-                        p->math == UGPG_WFMT_BF16 ? 1 : 3, st);
+        launch_wgrad_x6(a, p->math == UGPG_WFMT_BF16 ? 1 : 3, st);
     } else if (kind == WG_IMG) {
         hipLaunchKernelGGL(conv3x3_wgrad_img_kernel, dim3((unsigned)w.nsplit), dim3(256), 0, st, a);
     } else if (kind == WG_C8) {

@@ -24,9 +24,6 @@ struct ConvFwdArgs {
     float* stats;
     int B, H, W, Cin, Cout;
     int tiles_x, tiles_y, ntiles;
-    int probe;  // diagnostics only (tuning knob "x6_probe"): bit0 skip prefetch, bit1 skip staging
-    int order;  // persistent x6r item order: 0 = tile-major (it = tile*NB + nb), 1 = column-
-                // block-major (it = nb*ntiles + tile: an XCD's range shares one weight slab)
     // BatchNorm-backward partials of out0 (ugpg_conv_t.bnb_*; bnb_part == nullptr: off)
     const float* bnb_y;
     const float* bnb_mean;
@@ -178,7 +175,7 @@ struct WgradArgs {
 // itself: FWD_WROTE_BNB (a.bnb_part), FWD_WROTE_OUT16 (a.out0_16)
 constexpr int FWD_WROTE_BNB = 1, FWD_WROTE_OUT16 = 2;
 int launch_fwd_x6(const ConvFwdArgs& a, int np, hipStream_t st);
-// the image layer's direct fp32 forward (conv_x6.hip, knob "x6_img"): shape predicate,
+// the image layer's direct fp32 forward (conv_x6.hip): shape predicate,
 // BatchNorm slot count (nwm row groups per 8 x 32 tile), launch (false: not applicable)
 bool img_fwd_eligible(int W, int C0, int C1, int Cout);
 int img_fwd_slots(int B, int H, int W, int nwm);
@@ -200,16 +197,13 @@ struct PackBatch {
     int n;
 };
 void launch_pack_x6_batch(const PackItem* items, int n, int np, hipStream_t st);
-extern int g_x6_pipe, g_x6_probe;
 int fwd_x6_tile_w(int W, int np);  // 32 or 16 (np = bf16 pieces: 3 split, 1 bf16)
 int fwd_x6_tile_h(int W, int np);  // 4, 8 or 16
 int fwd_x6_stat_slots(int ntiles, int W, int np);  // BatchNorm partial slots the forward writes
-void launch_wgrad_x6(const WgradArgs& a, unsigned grid, int np, hipStream_t st);
-extern int g_x6_wgrad;  // tuning knob "x6_wgrad"
+void launch_wgrad_x6(const WgradArgs& a, int np, hipStream_t st);
 // split plan of the persistent split-bf16 wgrad (deterministic: planned for `cus` CUs)
 void wgrad_x6w_plan(int ntiles, int Cout, int Cin, int cus, int& nsplit, int& tps);
-constexpr int WGX6_TH = 2, WGX6_TW = 16;  // pixel tile of the split-bf16 wgrad
-constexpr int WGX6W_TH = 4;                // rows of its persistent form's tile (x 16)
+constexpr int WGX6_TW = 16, WGX6W_TH = 4;  // pixel tile (4 x 16) of the split-bf16 wgrad
 void launch_pack_x6(const float* w, void* wpk, int Cout, int Cin, int Cin_pad, int mode, int np,
                     hipStream_t st);
 

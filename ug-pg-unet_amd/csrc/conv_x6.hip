@@ -289,7 +289,7 @@ __global__ void __launch_bounds__(256) conv3x3_fwd_x6_kernel(ConvFwdArgs a) {
     lstore(0);
     __syncthreads();
     for (int c = 0; c < nchunk; ++c) {
-        if (c + 1 < nchunk && !(a.probe & 1)) gload(c + 1);
+        if (c + 1 < nchunk) gload(c + 1);
         u32x4 fa[2][MT][NP], fb[2][NP];
         ldfrag(0, fa[0], fb[0]);
 #pragma unroll
@@ -298,7 +298,6 @@ __global__ void __launch_bounds__(256) conv3x3_fwd_x6_kernel(ConvFwdArgs a) {
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt) acc[mt][0] = mfma_xn<NP>(fa[t & 1][mt], fb[t & 1], acc[mt][0]);
         }
-        if (a.probe & 2) continue;
         __syncthreads();
         if (c + 1 < nchunk) {
             lstore(c + 1);
@@ -595,8 +594,8 @@ __device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a,
             sg[nt] = sgx[nt] = sx[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
         // per batch of m-tiles: the y loads go out first, the batch's output stores issue
-        // while they are in flight, then the partials (batch: registers of the cw8 forms)
-        constexpr int YB = NWM == 4 ? 1 : (MTW < 4 ? MTW : 4);
+        // while they are in flight, then the partials
+        constexpr int YB = MTW < 4 ? MTW : 4;
 #pragma unroll
         for (int m0 = 0; m0 < MTW; m0 += YB) {
             f32x4 yv[YB][2];
@@ -749,19 +748,18 @@ extern "C" int ugpg_debug_clock(double* mhz) {
     return n;
 }
 #endif
-// NCW = compute waves: 4 (one per SIMD) or 8 (two per SIMD, 16x16x32 form only: while one
-// waits on an LDS read or a barrier the other issues MFMAs; each covers a quarter of the
-// item's pixels, so a tile has NCW/2 BatchNorm stat slots)
 // THT: tile height; 256 / TWT (256-pixel items) by default, 8 with TWT = 16 for 128-pixel
 // items (8 x 16) on 16-wide images, whose 256-pixel items would leave half of the CUs idle
-// at bs16 (64 images' worth of 16 x 16 tiles x 8 column blocks = 128 items).
-template <int NP, bool M16, int TWT = 32, int NCW = 4, int THT = 256 / TWT>
-__global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) {
+// at bs16 (64 images' worth of 16 x 16 tiles x 8 column blocks = 128 items).  (Measured
+// and dropped: two compute waves per SIMD, 512-pixel single-piece items, column-block-major
+// item order.)
+template <int NP, bool M16, int TWT = 32, int THT = 256 / TWT>
+__global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) {
+    constexpr int NCW = 4;  // compute waves (one per SIMD) + 4 loader waves
     static_assert(!M16 || NP == 3, "the 16x16x32 form pairs the split-bf16 products");
     static_assert(TWT == 32 || (M16 && TWT == 16), "16-wide tiles only in the 16x16x32 form");
-    static_assert(THT * TWT == 256 || (M16 && THT * TWT == 128) || (!M16 && THT * TWT == 512),
-                  "256-pixel items; 128 (16x16x32 form) or 512 (32x32x16 form) pixels");
-    static_assert(NCW == 4 || (NCW == 8 && M16), "two compute waves per SIMD: 16x16x32 form only");
+    static_assert(THT * TWT == 256 || (M16 && THT * TWT == 128),
+                  "256-pixel items; 128 in the 16x16x32 form");
     // 256-pixel items: 8 x 32 (images >= 32 wide) or 16 x 16 (16-31 wide, 16x16x32 form)
     // MT: 32-pixel image rows per compute wave in the 32x32x16 form (two pixel halves)
     constexpr int TW = TWT, TH = THT, BN = 64, BKC = 16, MT = TH / 2;
@@ -825,8 +823,8 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
     };
     auto pos_of = [&](int it) {
         Pos p;
-        p.nb = a.order ? it / a.ntiles : it % NB;
-        p.tile = a.order ? it % a.ntiles : it / NB;
+        p.nb = it % NB;
+        p.tile = it / NB;
         p.b = p.tile / tpi;
         const int trem = p.tile % tpi;
         p.ty0 = (trem / a.tiles_x) * TH;
@@ -858,7 +856,7 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
             q.s = min(s, last);
             q.c = q.s % nchunk;
             q.itm = item0 + (q.s / nchunk) * nslots;
-            q.nb = a.order ? q.itm / a.ntiles : q.itm % NB;
+            q.nb = q.itm % NB;
             q.p = pos_of(q.itm);
             return q;
         };
@@ -868,7 +866,7 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
             if (++q.c == nchunk) {
                 q.c = 0;
                 q.itm += nslots;
-                q.nb = a.order ? q.itm / a.ntiles : q.itm % NB;
+                q.nb = q.itm % NB;
                 q.p = pos_of(q.itm);
             }
         };
@@ -1268,34 +1266,7 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
     }
     for (int k = 0; k < total; ++k) {
         const u32x4* Ac = smem + (k & 1) * A_VECS;
-        if constexpr (MT > 4) {
-            // 512-pixel items (single piece): one A fragment set, each m-tile's next-tap
-            // fragment read right after its MFMA (registers: 8 accumulator blocks)
-            static_assert(NP == 1, "512-pixel items: single-piece form only");
-            u32x4 fa[MT][NP], fb[2][NP];
-            ldfrag(Ac, Bring + ((3 * k) % NSLOT) * R_STR, 0, 0, fa, fb[0]);
-#pragma unroll
-            for (int t = 0; t < 9; ++t) {
-                const int ky1 = (t + 1) / 3, kx1 = (t + 1) % 3;
-                const u32x4* Bn = Bring + ((3 * k + ky1) % NSLOT) * R_STR;
-                if (t + 1 < 9) fb[(t + 1) & 1][0] = Bn[boff + kx1 * BN];
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt) {
-                    acc[mt] = mfma_xn<NP>(fa[mt], fb[t & 1], acc[mt]);
-                    if (t + 1 < 9) fa[mt][0] = Ac[aoff + (mt + ky1) * HS + kx1];
-                }
-#pragma unroll
-                for (int i = 0; i < MT; ++i) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-                    if (t + 1 < 9) {
-                        if (i == 0) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-                        else __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                    }
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                if (t % 3 == 2) read_barrier();
-            }
-        } else if constexpr (NP == 1) {
+        if constexpr (NP == 1) {
             // single piece: 4 MFMAs per tap cannot cover the next tap's fragment reads, so
             // the reads run two taps ahead, across the step boundary (the next step's first
             // two taps are read in phase 2: halo(k+1) and row 3k+3 are visible from there)
@@ -1365,8 +1336,8 @@ __global__ void __launch_bounds__((NCW + 4) * 64, 1) conv3x3_fwd_x6r_kernel(Conv
 }
 // ---------------------------------------------------------------------------
 // Split-bf16 weight gradient: dW[co][ci][t] = sum_p dy[p][co] * act(x)[p+t][ci].
-// Same block decomposition and partial layout as conv3x3_wgrad_kernel (64 co x
-// 64 ci x 9 taps per block, 4 waves as 2 (co) x 2 (ci) with nine 32x32
+// Same item decomposition and partial layout as conv3x3_wgrad_kernel (64 co x
+// 64 ci x 9 taps per item, 4 compute waves as 2 (co) x 2 (ci) with nine 32x32
 // accumulators, deterministic split-K), but the K = pixel reduction runs on
 // v_mfma_f32_32x32x16_bf16: one k-step = one 16-pixel row of the 4 x 16 tile.
 // Both operands are pixel-major in LDS -- one 448-B record per pixel holding the
@@ -1407,164 +1378,9 @@ __device__ __forceinline__ u32x2 ds_read_tr(const char* lds_byte_addr) {
 
 constexpr int WX_REC = 448;  // bytes per pixel record: 3 pieces x 64 ch x 2 B + 64 B pad
 
-template <int TH, int TW>
-__global__ void __launch_bounds__(256, 2) conv3x3_wgrad_x6_kernel(WgradArgs a) {
-    static_assert(TW == 16, "one 16-pixel row per MFMA k-step");
-    constexpr int P = TH * TW, HWD = TW + 2, NHALO = (TH + 2) * HWD;
-    constexpr int DY_Q = P * 16, X_Q = NHALO * 16;  // float4 quads to stage
-    constexpr int DY_PER = (DY_Q + 255) / 256, X_PER = (X_Q + 255) / 256;
-    static_assert(X_PER <= 32, "halo too large");
-    __shared__ __attribute__((aligned(16))) char smem[(P + NHALO) * WX_REC];
-    char* dys = smem;
-    char* xs = smem + P * WX_REC;
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave >> 1, wn = wave & 1;
-    const int NCO = a.Cout / 64, NCI = a.Cin / 64;
-    const int nb = blockIdx.x % NCO;
-    const int rest = blockIdx.x / NCO;
-    const int cb = rest % NCI, split = rest / NCI;
-    const int co0 = nb * 64, ci0 = cb * 64;
-    const int t_begin = split * a.tps, t_end = min(a.ntiles, t_begin + a.tps);
-
-    const float* xsrc = a.src0;
-    const float* xsc = a.sc0;
-    const float* xsh = a.sh0;
-    int Cs = a.C0, cbase = ci0;
-    if (ci0 >= a.C0) {
-        xsrc = a.src1;
-        xsc = a.sc1;
-        xsh = a.sh1;
-        Cs = a.C1;
-        cbase = ci0 - a.C0;
-    }
-    const int tpi = a.tiles_x * a.tiles_y;
-    const Act4 xact = act_load4(xsc, xsh, cbase + (tid & 15) * 4);  // q = idx & 15 = tid & 15
-    const bool xon = xsc != nullptr;
-
-    f32x4 rdy[DY_PER], rx[X_PER];
-    unsigned xvalid = 0;
-    auto gload = [&](int tile) {
-        const int b = tile / tpi, trem = tile % tpi;
-        const int ty0 = (trem / a.tiles_x) * TH, tx0 = (trem % a.tiles_x) * TW;
-#pragma unroll
-        for (int v = 0; v < DY_PER; ++v) {
-            const int idx = tid + v * 256;
-            f32x4 val = {0.f, 0.f, 0.f, 0.f};
-            if (idx < DY_Q) {
-                const int p = idx >> 4, q = idx & 15;
-                const int gy = ty0 + p / TW, gx = tx0 + p % TW;
-                if (gy < a.H && gx < a.W)
-                    val = *reinterpret_cast<const f32x4*>(
-                        a.dy + ((size_t)(b * a.H + gy) * a.W + gx) * a.Cout + co0 + q * 4);
-            }
-            rdy[v] = val;
-        }
-        xvalid = 0;
-#pragma unroll
-        for (int v = 0; v < X_PER; ++v) {
-            const int idx = tid + v * 256;
-            f32x4 val = {0.f, 0.f, 0.f, 0.f};
-            if (idx < X_Q) {
-                const int hp = idx >> 4, q = idx & 15;
-                const int gy = ty0 - 1 + hp / HWD, gx = tx0 - 1 + hp % HWD;
-                if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
-                    val = *reinterpret_cast<const f32x4*>(
-                        xsrc + ((size_t)(b * a.H + gy) * a.W + gx) * Cs + cbase + q * 4);
-                    xvalid |= 1u << v;
-                }
-            }
-            rx[v] = val;
-        }
-    };
-    // record layout: [piece][64 ch] bf16 at byte piece*128 + ch*2
-    auto put = [&](char* base, int rec, int q, f32x4 v) {
-        u32x2 p0, p1, p2;
-        split3_4(v, p0, p1, p2);
-        char* r = base + rec * WX_REC + q * 8;
-        *reinterpret_cast<u32x2*>(r) = p0;
-        *reinterpret_cast<u32x2*>(r + 128) = p1;
-        *reinterpret_cast<u32x2*>(r + 256) = p2;
-    };
-    auto lstore = [&]() {
-#pragma unroll
-        for (int v = 0; v < DY_PER; ++v) {
-            const int idx = tid + v * 256;
-            if (idx < DY_Q) put(dys, idx >> 4, idx & 15, rdy[v]);
-        }
-#pragma unroll
-        for (int v = 0; v < X_PER; ++v) {
-            const int idx = tid + v * 256;
-            if (idx < X_Q) {
-                f32x4 val = rx[v];
-                if ((xvalid >> v) & 1u) val = act_reg4(val, xact, xon);
-                put(xs, idx >> 4, idx & 15, val);
-            }
-        }
-    };
-
-    f32x16 acc[9];
-#pragma unroll
-    for (int t = 0; t < 9; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-
-    // transposed-read addresses: 16-lane group g = lane>>4 (h = g>>1 pixel half,
-    // g&1 channel half), lane li supplies row (pixel) li>>2, channels 4(li&3)..+3.
-    const int li = lane & 15, g = lane >> 4, hh = g >> 1;
-    const int pix_in = 8 * hh + (li >> 2);                  // + 4s for read s
-    const int ch_a = wm * 32 + 16 * (g & 1) + 4 * (li & 3);  // co within the block
-    const int ch_b = wn * 32 + 16 * (g & 1) + 4 * (li & 3);  // ci within the block
-    const char* abase = dys + pix_in * WX_REC + ch_a * 2;
-    const char* bbase = xs + pix_in * WX_REC + ch_b * 2;
-
-    if (t_begin < t_end) gload(t_begin);
-    for (int tile = t_begin; tile < t_end; ++tile) {
-        __syncthreads();
-        lstore();
-        __syncthreads();
-        if (tile + 1 < t_end) gload(tile + 1);
-#pragma unroll 1
-        for (int ks = 0; ks < TH; ++ks) {
-            u32x4 af[3];
-#pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                const char* pa = abase + ks * TW * WX_REC + q * 128;
-                const u32x2 lo = ds_read_tr(pa), hi = ds_read_tr(pa + 4 * WX_REC);
-                af[q] = u32x4{lo.x, lo.y, hi.x, hi.y};
-            }
-            auto ldb = [&](int t, u32x4 (&bf)[3]) {
-                const char* pb = bbase + ((ks + t / 3) * HWD + (t % 3)) * WX_REC;
-#pragma unroll
-                for (int q = 0; q < 3; ++q) {
-                    const u32x2 lo = ds_read_tr(pb + q * 128), hi = ds_read_tr(pb + q * 128 + 4 * WX_REC);
-                    bf[q] = u32x4{lo.x, lo.y, hi.x, hi.y};
-                }
-            };
-            u32x4 bfr[2][3];
-            ldb(0, bfr[0]);
-#pragma unroll
-            for (int t = 0; t < 9; ++t) {
-                if (t + 1 < 9) ldb(t + 1, bfr[(t + 1) & 1]);
-                acc[t] = mfma_x6(af, bfr[t & 1], acc[t]);
-            }
-        }
-    }
-
-    const int ci = ci0 + wn * 32 + (lane & 31);
-#pragma unroll
-    for (int t = 0; t < 9; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int co = co0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-            a.part[((size_t)(split * 9 + t) * a.Cout + co) * a.Cin + ci] = acc[t][r];
-        }
-}
-
 // ---------------------------------------------------------------------------
-// Persistent, warp-specialized form of the split-bf16 weight gradient ("x6w").
-// Same LDS records, transposed fragment reads and MFMA decomposition as
-// conv3x3_wgrad_x6_kernel, but one 8-wave workgroup per CU walks a contiguous
+// Persistent, warp-specialized form of the split-bf16 weight gradient ("x6w"),
+// one 8-wave workgroup per CU walking a contiguous
 // per-XCD range of items (64-co block, 64-ci block, pixel split); waves 0-3 only
 // read fragments and issue MFMAs, waves 4-7 stage: during step k (one 2 x 16
 // pixel tile) they write tile k+1 into the idle half of a double-buffered LDS
@@ -1576,13 +1392,9 @@ __global__ void __launch_bounds__(256, 2) conv3x3_wgrad_x6_kernel(WgradArgs a) {
 template <int NP>
 constexpr int wrec() { return NP == 3 ? WX_REC : 192; }
 
-// M16: the compute waves run v_mfma_f32_16x16x32_bf16 with the split-bf16 products paired
-// along k, as the forward's x6r form (3 MFMAs per 16 x 16 tile and tap instead of 6 half-
-// size products): k groups 0,1 of both operands carry the 16 pixels of one piece, groups
-// 2,3 of another, so dy01.x10 = a0b1 + a1b0, dy01.x01 = a0b0 + a1b1, dy02.x20 = a0b2 + a2b0.
-template <int TH, int TW, int NP, bool M16 = false>
+// (A paired 16x16x32 form, as the forward's, measured 2 % slower: 32x32x16 it is.)
+template <int TH, int TW, int NP>
 __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) {
-    static_assert(!M16 || NP == 3, "the paired 16x16x32 form needs the three pieces");
     constexpr int REC = wrec<NP>();
     static_assert(TW == 16, "one 16-pixel row per MFMA k-step");
     constexpr int P = TH * TW, HWD = TW + 2, NHALO = (TH + 2) * HWD;
@@ -1814,110 +1626,6 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
 
     // ---------------------------------------------------------------- compute waves
     const int wm = wave >> 1, wn = wave & 1;
-    if constexpr (M16) {
-        const int li = lane & 15, g = lane >> 4;
-        // transposed reads: 16-lane group g takes pixels 8(g&1) + (li>>2) (+4 for the
-        // second read), channels 4(li&3)..+3 of a 16-channel tile; lane li receives the
-        // 8 pixels of channel li = its row (co) or column (ci) of the 16 x 16 tile
-        const int pix_in = 8 * (g & 1) + (li >> 2);
-        const int s0 = g < 2 ? 0 : 1, s2 = g < 2 ? 0 : 2;  // piece of A01 / A02 (and B01)
-        const int s10 = g < 2 ? 1 : 0, s20 = g < 2 ? 2 : 0;  // piece of B10 / B20
-        f32x4 acc[9][2][2];
-#pragma unroll
-        for (int t = 0; t < 9; ++t)
-#pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-                for (int nt = 0; nt < 2; ++nt) acc[t][mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        Cur cc;
-        item_range(item0, cc);
-        lds_barrier();  // step 0 staged
-        for (int k = 0; k < total; ++k) {
-            const char* dys = smem + (k & 1) * RECS * REC;
-            const char* abase = dys + pix_in * REC + (wm * 32 + 4 * (li & 3)) * 2;
-            const char* bbase = dys + P * REC + pix_in * REC + (wn * 32 + 4 * (li & 3)) * 2;
-            auto trpair = [](const char* p) {
-                const u32x2 lo = ds_read_tr(p), hi = ds_read_tr(p + 4 * REC);
-                return u32x4{lo.x, lo.y, hi.x, hi.y};
-            };
-            auto lda = [&](int ks, u32x4 (&af)[2][2]) {  // [co tile][A01, A02]
-#pragma unroll
-                for (int mt = 0; mt < 2; ++mt) {
-                    const char* pa = abase + ks * TW * REC + 32 * mt;
-                    af[mt][0] = trpair(pa + s0 * 128);
-                    af[mt][1] = trpair(pa + s2 * 128);
-                }
-            };
-            auto ldb = [&](int ks, int t, u32x4 (&bf)[2][3]) {  // [ci tile][B10, B01, B20]
-                const char* pb = bbase + ((ks + t / 3) * HWD + (t % 3)) * REC;
-#pragma unroll
-                for (int nt = 0; nt < 2; ++nt) {
-                    const char* q = pb + 32 * nt;
-                    bf[nt][0] = trpair(q + s10 * 128);
-                    bf[nt][1] = trpair(q + s0 * 128);
-                    bf[nt][2] = trpair(q + s20 * 128);
-                }
-            };
-            u32x4 afr[2][2][2], bfr[2][2][3];
-            lda(0, afr[0]);
-            ldb(0, 0, bfr[0]);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int u = 0; u < 9 * TH; ++u) {
-                const int ks = u / 9, t = u % 9;
-                const bool more = u + 1 < 9 * TH, row = (u + 1) % 9 == 0;
-                if (more) {
-                    if (row) lda((u + 1) / 9, afr[((u + 1) / 9) & 1]);
-                    ldb((u + 1) / 9, (u + 1) % 9, bfr[(u + 1) & 1]);
-                }
-                const u32x4(&A)[2][2] = afr[ks & 1];
-                const u32x4(&B)[2][3] = bfr[u & 1];
-#pragma unroll
-                for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-                    for (int nt = 0; nt < 2; ++nt) {
-                        f32x4 c = acc[t][mt][nt];
-                        c = mfma16x16(A[mt][0], B[nt][0], c);  // a0b1 + a1b0
-                        c = mfma16x16(A[mt][0], B[nt][1], c);  // a0b0 + a1b1
-                        c = mfma16x16(A[mt][1], B[nt][2], c);  // a0b2 + a2b0
-                        acc[t][mt][nt] = c;
-                    }
-                // the next tap's 12 reads (20 at a row change) between the 12 MFMAs
-#pragma unroll
-                for (int i = 0; i < 12; ++i) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                    if (more) {
-                        if (row && i < 8) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-                        else __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                    }
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            read_barrier();
-            const bool item_end = cc.tile + 1 >= cc.tend;
-            if (item_end) {
-                const int nb = cc.item % NCO, rest = cc.item / NCO;
-                const int cb = rest % NCI, split = rest / NCI;
-#pragma unroll
-                for (int t = 0; t < 9; ++t)
-#pragma unroll
-                    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-                        for (int nt = 0; nt < 2; ++nt) {
-                            const int ci = cb * 64 + wn * 32 + 16 * nt + li;
-#pragma unroll
-                            for (int i = 0; i < 4; ++i) {
-                                const int co = nb * 64 + wm * 32 + 16 * mt + 4 * g + i;
-                                a.part[((size_t)(split * 9 + t) * a.Cout + co) * a.Cin + ci] =
-                                    acc[t][mt][nt][i];
-                            }
-                            acc[t][mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-                        }
-            }
-            advance(cc);
-        }
-        return;
-    }
     f32x16 acc[9];
 #pragma unroll
     for (int t = 0; t < 9; ++t)
@@ -2020,25 +1728,16 @@ void wgrad_x6w_plan(int ntiles, int Cout, int Cin, int cus, int& nsplit, int& tp
     nsplit = (int)cdiv(ntiles, tps);
 }
 
-int g_x6_wgrad = 1;  // tuning knob "x6_wgrad": 1 = persistent x6w kernel (32x32x16), 2 = its
-                     // paired 16x16x32 form, 0 = one block per item
-
-void launch_wgrad_x6(const WgradArgs& a, unsigned grid, int np, hipStream_t st) {
-    if (g_x6_wgrad || np == 1) {  // (the per-item kernel has no single-piece form)
-        const int64_t items = (int64_t)(a.Cout / 64) * (a.Cin / 64) * a.nsplit;
-        int64_t g = std::min<int64_t>(cu_count(st), (items + 7) / 8 * 8);
-        g = std::max<int64_t>(8, g / 8 * 8);
-        if (np == 3 && g_x6_wgrad == 2)
-            hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW, 3, true>), dim3((unsigned)g),
-                               dim3(512), 0, st, a);
-        else if (np == 3)
-            hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW, 3>), dim3((unsigned)g), dim3(512), 0, st, a);
-        else
-            hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW, 1>), dim3((unsigned)g), dim3(512), 0, st, a);
-        return;
-    }
-    hipLaunchKernelGGL((conv3x3_wgrad_x6_kernel<WGX6_TH, WGX6_TW>), dim3(grid), dim3(256), 0, st,
-                       a);
+void launch_wgrad_x6(const WgradArgs& a, int np, hipStream_t st) {
+    const int64_t items = (int64_t)(a.Cout / 64) * (a.Cin / 64) * a.nsplit;
+    int64_t g = std::min<int64_t>(cu_count(st), (items + 7) / 8 * 8);
+    g = std::max<int64_t>(8, g / 8 * 8);
+    if (np == 3)
+        hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW, 3>), dim3((unsigned)g),
+                           dim3(512), 0, st, a);
+    else
+        hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW, 1>), dim3((unsigned)g),
+                           dim3(512), 0, st, a);
 }
 
 // Weight pack for the split path.  mode 0 (forward): GEMM N = Cout, K channels =
@@ -2156,47 +1855,23 @@ __global__ void __launch_bounds__(256) pack_x6_tile_kernel(PackBatch pb, int np)
     }
 }
 
-#ifndef X6_PIPE_DEFAULT
-#define X6_PIPE_DEFAULT 4
-#endif
-int g_x6_pipe = X6_PIPE_DEFAULT;   // tuning knob "x6_pipe" (see launch_fwd_x6)
-// persistent form for this image width / piece count: 8x32 items for W >= 32; with
-// x6_pipe = 3 also 16x16 items for 16 <= W < 32 (16x16x32 split-bf16 form only).  Not
-// the default: at bs16 the 16-wide layers have 64-128 such items for 256 CUs and the
-// single-stage kernel's 128-pixel tiles fill the chip better (0.120 vs 0.124 ms,
-// down4 of S4).
-// x6_pipe = 4: 8 x 16-pixel (128-pixel) items for 16 <= W < 32, so that bs16's 16-wide
-// layers have 256 items for 256 CUs.
-// single-piece (bf16) persistent form: X6R_NP1_TH = 16 gives 16 x 32 = 512-pixel items
-// (x 64 channels), halving the weight bytes staged per MFMA of that loader-bound form;
-// measured 4 % slower over the Stage-4 layers (its 8-block epilogue spills), so 8
-#ifndef X6R_NP1_TH
-#define X6R_NP1_TH 8
-#endif
-static bool use_x6r(int W, int np) {
-    return g_x6_pipe && (W >= 32 || (g_x6_pipe >= 3 && np == 3 && W >= 16));
-}
+// Forward / data-gradient form by shape (no runtime knobs: the form, its tiling and hence
+// the BatchNorm slot count are functions of the shape and the piece count):
+//  - images >= 32 wide: conv3x3_fwd_x6r_kernel, 8 x 32-pixel items (16x16x32 MFMA tiles
+//    for split-bf16, 32x32x16 for single-piece bf16);
+//  - split-bf16 images 16-31 wide: the same with 8 x 16-pixel items, so that bs16's
+//    16-wide layers have 256 items for 256 CUs (152-166 -> 216-223 TF/s vs the
+//    single-stage kernel);
+//  - narrower images (and single-piece ones < 32 wide): conv3x3_fwd_x6_kernel, 8 x 16-pixel
+//    tiles, one workgroup per tile.
+// Measured and dropped (round 2): 16 x 16 items for the 16-wide layers, the 32x32x16 form
+// for split-bf16, 512-pixel single-piece items, two compute waves per SIMD.
+static bool use_x6r(int W, int np) { return W >= 32 || (np == 3 && W >= 16); }
 int fwd_x6_tile_w(int W, int np) { return W >= 32 ? 32 : 16; }
-int fwd_x6_tile_h(int W, int np) {
-    if (use_x6r(W, np) && np == 1 && W >= 32) return X6R_NP1_TH;
-    if (use_x6r(W, np)) return W >= 32 ? 8 : (g_x6_pipe == 4 ? 8 : 16);
-    return W >= 32 ? 4 : 8;
-}
-#ifndef X6R_CW_DEFAULT
-#define X6R_CW_DEFAULT 4
-#endif
-int g_x6_cw = X6R_CW_DEFAULT;  // tuning knob "x6_cw": compute waves of the 16x16x32 persistent form
-static int x6r_cw(int np) { return np == 3 && g_x6_pipe >= 2 && g_x6_cw == 8 ? 8 : 4; }
+int fwd_x6_tile_h(int W, int np) { return 8; }
 int fwd_x6_stat_slots(int ntiles, int W, int np) {
-    return use_x6r(W, np) ? x6r_cw(np) / 2 * ntiles : ntiles;
+    return use_x6r(W, np) ? 2 * ntiles : ntiles;  // persistent forms: one slot per pixel half
 }
-
-// tuning knob "x6_pipe": conv3x3_fwd_x6r_kernel for images >= 32 wide with 16x16x32
-// tiles (2) or 32x32x16 tiles (1); 3 = as 2 plus 16x16-pixel items for images 16-31
-// wide; 4 (default) = as 2 plus 8x16-pixel items for images 16-31 wide (bs16's 16-wide
-// layers: 256 items for 256 CUs, 152-166 -> 216-223 TF/s vs the single-stage kernel);
-// 0 = conv3x3_fwd_x6_kernel everywhere
-int g_x6_probe = 0;  // "x6_probe": timing diagnostics (see ugpg_set_tuning)
 
 // ---------------------------------------------------------------------------
 // Image layer (inc.conv_op.0: a 3-channel image zero-extended to 8 channels, one
@@ -2445,24 +2120,16 @@ __global__ void __launch_bounds__(4096 / PX) conv3x3_img_fwd_kernel(ConvFwdArgs 
     }
 }
 
-#ifndef X6R_ORDER_DEFAULT
-#define X6R_ORDER_DEFAULT 0
-#endif
-int g_x6_order = X6R_ORDER_DEFAULT;  // tuning knob "x6_order" (ConvFwdArgs::order)
-#ifndef X6_IMG_DEFAULT
-#define X6_IMG_DEFAULT 1
-#endif
-int g_x6_img = X6_IMG_DEFAULT;
 #ifndef IMG_PX
 #define IMG_PX 8
 #endif
 #ifndef IMG_BPC
 #define IMG_BPC 2
-#endif  // tuning knob "x6_img": direct fp32 kernel for the image layer
+#endif
 
 bool img_fwd_eligible(int W, int C0, int C1, int Cout) {
     // PGUNet4's image layer is 3 -> 64, PGUNet3's 3 -> 128 (two 64-channel column blocks)
-    return g_x6_img && W >= 32 && C0 == 8 && C1 == 0 && (Cout == 64 || Cout == 128);
+    return W >= 32 && C0 == 8 && C1 == 0 && (Cout == 64 || Cout == 128);
 }
 int img_fwd_slots(int B, int H, int W, int nwm) {
     return nwm * B * (int)cdiv(H, 8) * (int)cdiv(W, 32);
@@ -2481,17 +2148,12 @@ bool launch_img_fwd(const ConvFwdArgs& a, bool wf32, hipStream_t st) {
     const dim3 grid((unsigned)g, (unsigned)(a.Cout / 64)), block(4096 / PX);
     if (wf32)
         hipLaunchKernelGGL((conv3x3_img_fwd_kernel<2, PX, true>), grid, block, 0, st, a);
-    else if (x6r_cw(3) == 8)
-        hipLaunchKernelGGL((conv3x3_img_fwd_kernel<4, PX, false>), grid, block, 0, st, a);
     else
         hipLaunchKernelGGL((conv3x3_img_fwd_kernel<2, PX, false>), grid, block, 0, st, a);
     return true;
 }
 
-int launch_fwd_x6(const ConvFwdArgs& a_in, int np, hipStream_t st) {
-    ConvFwdArgs a = a_in;
-    a.probe = g_x6_probe;
-    a.order = g_x6_order;
+int launch_fwd_x6(const ConvFwdArgs& a, int np, hipStream_t st) {
     const int64_t items = (int64_t)a.ntiles * (a.Cout / 64);
     if (np == 3 && use_x6r(a.W, np) && a.Cin == 16 && launch_img_fwd(a, false, st))
         return FWD_WROTE_OUT16;
@@ -2500,51 +2162,25 @@ int launch_fwd_x6(const ConvFwdArgs& a_in, int np, hipStream_t st) {
         // walking a strided share of its XCD's contiguous item range
         int64_t g = std::min<int64_t>(cu_count(st), (items + 7) / 8 * 8);
         g = std::max<int64_t>(8, g / 8 * 8);
-        const bool cw8 = x6r_cw(np) == 8;
-        if (np == 3 && g_x6_pipe == 4 && a.W < 32 && cw8)
-            hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<3, true, 16, 8, 8>), dim3((unsigned)g),
-                               dim3(768), 0, st, a);
-        else if (np == 3 && g_x6_pipe == 4 && a.W < 32)
-            hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<3, true, 16, 4, 8>), dim3((unsigned)g),
+        if (np == 3 && a.W < 32)
+            hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<3, true, 16, 8>), dim3((unsigned)g),
                                dim3(512), 0, st, a);
-        else if (np == 3 && g_x6_pipe >= 2 && a.W < 32 && cw8)
-            hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<3, true, 16, 8>), dim3((unsigned)g), dim3(768),
-                               0, st, a);
-        else if (np == 3 && g_x6_pipe >= 2 && a.W < 32)
-            hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<3, true, 16>), dim3((unsigned)g), dim3(512),
-                               0, st, a);
-        else if (np == 3 && g_x6_pipe >= 2 && cw8)
-            hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<3, true, 32, 8>), dim3((unsigned)g), dim3(768),
-                               0, st, a);
-        else if (np == 3 && g_x6_pipe >= 2)
+        else if (np == 3)
             hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<3, true>), dim3((unsigned)g), dim3(512), 0,
                                st, a);
-        else if (np == 3)
-            hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<3, false>), dim3((unsigned)g), dim3(512), 0,
-                               st, a);
-        else if (X6R_NP1_TH == 16)
-            hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 4, 16>), dim3((unsigned)g),
-                               dim3(512), 0, st, a);
         else
             hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false>), dim3((unsigned)g), dim3(512), 0,
                                st, a);
         // every persistent form fuses the BatchNorm-backward partials into its epilogue;
-        // the 32x32x16 form also writes the bf16 copy of its output
-        return FWD_WROTE_BNB | (np == 3 && g_x6_pipe >= 2 ? 0 : FWD_WROTE_OUT16);
+        // the 32x32x16 (single-piece) form also writes the bf16 copy of its output
+        return FWD_WROTE_BNB | (np == 3 ? 0 : FWD_WROTE_OUT16);
     }
+    // single-stage kernel: 8 x 16-pixel tiles (fwd_x6_tile_*)
     const unsigned grid = (unsigned)items;
-    const bool wide = fwd_x6_tile_w(a.W, np) == 32;
-    if (np == 3) {
-        if (wide)
-            hipLaunchKernelGGL((conv3x3_fwd_x6_kernel<4, 32, false, 3>), dim3(grid), dim3(256), 0, st, a);
-        else
-            hipLaunchKernelGGL((conv3x3_fwd_x6_kernel<8, 16, true, 3>), dim3(grid), dim3(256), 0, st, a);
-    } else {
-        if (wide)
-            hipLaunchKernelGGL((conv3x3_fwd_x6_kernel<4, 32, false, 1>), dim3(grid), dim3(256), 0, st, a);
-        else
-            hipLaunchKernelGGL((conv3x3_fwd_x6_kernel<8, 16, true, 1>), dim3(grid), dim3(256), 0, st, a);
-    }
+    if (np == 3)
+        hipLaunchKernelGGL((conv3x3_fwd_x6_kernel<8, 16, true, 3>), dim3(grid), dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL((conv3x3_fwd_x6_kernel<8, 16, true, 1>), dim3(grid), dim3(256), 0, st, a);
     return 0;
 }
 

@@ -15,7 +15,7 @@
 namespace ugpg {
 
 // ---------------------------------------------------------------- max-pool
-int g_pool_nt = 0;  // tuning knob "pool_nt": nontemporal window loads in maxpool2_fwd_kernel (measured neutral)
+// (NT = nontemporal window loads: measured neutral, instantiated off)
 
 template <bool NT>
 __global__ void maxpool2_fwd_kernel(const float* x, const float* sc, const float* sh, int B, int H,
@@ -1331,12 +1331,8 @@ extern "C" int ugpg_maxpool2_fwd(ugpg_src_t s, int B, int H, int W, float* out, 
                                  void* stream) {
     UGPG_REQUIRE(s.data && out && am && s.C % 4 == 0 && H >= 2 && W >= 2, "maxpool2_fwd");
     const int64_t total = (int64_t)B * (H / 2) * (W / 2) * (s.C / 4);
-    if (g_pool_nt)
-        hipLaunchKernelGGL(maxpool2_fwd_kernel<true>, dim3(stream_grid(total)), dim3(256), 0,
-                           as_stream(stream), s.data, s.scale, s.shift, B, H, W, s.C, out, am);
-    else
-        hipLaunchKernelGGL(maxpool2_fwd_kernel<false>, dim3(stream_grid(total)), dim3(256), 0,
-                           as_stream(stream), s.data, s.scale, s.shift, B, H, W, s.C, out, am);
+    hipLaunchKernelGGL(maxpool2_fwd_kernel<false>, dim3(stream_grid(total)), dim3(256), 0,
+                       as_stream(stream), s.data, s.scale, s.shift, B, H, W, s.C, out, am);
     return check_launch("maxpool2_fwd");
 }
 

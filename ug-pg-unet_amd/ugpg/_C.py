@@ -25,9 +25,9 @@ class ConvDesc(C.Structure):
     """ugpg_conv_t."""
     _fields_ = [("B", _i), ("H", _i), ("W", _i), ("src", Src * 2), ("wpk", _p), ("bias", _p),
                 ("Cout", _i), ("out", _p * 2), ("out_split", _i), ("accumulate", _i * 2),
-                ("stats", _p), ("wfmt", _i), ("bnb_y", _p), ("bnb_mean", _p),
-                ("bnb_invstd", _p), ("bnb_scale", _p), ("bnb_shift", _p), ("bnb_part", _p),
-                ("out_bf16", _p)]
+                ("stats", _p), ("stats_slots", _i), ("wfmt", _i), ("bnb_y", _p),
+                ("bnb_mean", _p), ("bnb_invstd", _p), ("bnb_scale", _p), ("bnb_shift", _p),
+                ("bnb_part", _p), ("bnb_slots", _i), ("out_bf16", _p)]
 
 
 class Bnb(C.Structure):
@@ -51,7 +51,6 @@ class WgradDesc(C.Structure):
 SIGNATURES = {
     "ugpg_version": (C.c_char_p, []),
     "ugpg_last_error": (C.c_char_p, []),
-    "ugpg_set_tuning": (_i, [C.c_char_p, _i]),
     "ugpg_conv3x3_fwd": (_i, [C.POINTER(ConvDesc), _p]),
     "ugpg_conv3x3_fwd_ntiles": (_i, [_i, _i, _i, _i, _i, _i]),
     "ugpg_pack_conv3x3_bytes": (_sz, [_i, _i, _i]),
@@ -142,11 +141,6 @@ class _Lib:
                 fn.restype = res
                 fn.argtypes = args
             self._lib = lib
-            # UGPG_TUNE="key=value,...": kernel tuning knobs (ugpg_set_tuning) for A/B runs
-            for kv in filter(None, os.environ.get("UGPG_TUNE", "").split(",")):
-                k, _, v = kv.partition("=")
-                if lib.ugpg_set_tuning(k.strip().encode(), int(v)) != 0:
-                    raise ValueError(f"UGPG_TUNE: {lib.ugpg_last_error().decode()}")
         return self._lib
 
     def __getattr__(self, name):

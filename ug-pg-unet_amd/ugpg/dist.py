@@ -327,8 +327,10 @@ def _allreduce_runs(grads, bucket_bytes):
         for off in range(0, n, step):
             _all_reduce_async(base[off:off + step]).wait()
     if loose:
+        # through the same exchange as the flat runs (bf16 when grad_bf16(), the native
+        # communicator when selected)
         stage = torch.cat([g.reshape(-1) for g in loose])
-        dist.all_reduce(stage)
+        _all_reduce_async(stage).wait()
         off = 0
         for g in loose:
             g.copy_(stage[off:off + g.numel()].view_as(g))
@@ -349,10 +351,11 @@ def allreduce_gradients(params, bucket_bytes: int = 64 << 20):
     if pending:
         ptr = red.flat.untyped_storage().data_ptr()
         grads = [g for g in grads if g.untyped_storage().data_ptr() != ptr]
+        # the overlapped buckets finish first: with UGPG_COMM=native they run on a second
+        # communicator, and two communicators' collectives in flight at once can deadlock
+        red.wait()
     if grads:
         _allreduce_runs(grads, bucket_bytes)
-    if pending:
-        red.wait()
     return 1.0 / ws
 
 
@@ -407,17 +410,42 @@ def _has_distributed_sampler(loader) -> bool:
     return False
 
 
-def shard_batch(loader, *tensors):
+def check_same_batch(t: torch.Tensor):
+    """Raise unless every rank holds the same global batch `t` (a float64 checksum,
+    all-reduced MAX of (s, -s)).  Without a DistributedSampler the ranks must draw
+    identical batches (same shuffle seed and augmentation RNG); a per-rank seed would
+    otherwise train silently on overlapping shards.  One tiny collective per call."""
+    _, ws = world()
+    if ws <= 1:
+        return
+    s = float(t.detach().double().sum().item())
+    dev = torch.device("cuda", torch.cuda.current_device()) \
+        if dist.get_backend() == "nccl" else torch.device("cpu")
+    v = torch.tensor([s, -s], dtype=torch.float64, device=dev)
+    dist.all_reduce(v, op=dist.ReduceOp.MAX)
+    hi, lo = float(v[0]), -float(v[1])
+    if hi - lo > 1e-6 * max(1.0, abs(hi)):
+        raise RuntimeError(
+            "ugpg data parallel: ranks drew different global batches (checksums "
+            f"{lo!r} .. {hi!r}); seed the DataLoader / augmentation identically on every "
+            "rank or use a DistributedSampler")
+
+
+def shard_batch(loader, *tensors, check=False):
     """This rank's contiguous equal shard of a global batch drawn from `loader`.
 
     With a DistributedSampler the loader already yields per-rank batches, so they pass
     through.  Otherwise every rank draws the same global batch (same seed) and keeps
     rows [r*b, (r+1)*b), b = len // world_size; a remainder that does not divide is
     dropped (DistributedSampler(drop_last=True) semantics), and a batch smaller than
-    the world size yields None on every rank (skipped consistently)."""
+    the world size yields None on every rank (skipped consistently).  check=True (the
+    trainers pass it for the first batch of each epoch) verifies that every rank drew
+    the same global batch (check_same_batch)."""
     rank, ws = world()
     if ws <= 1 or _has_distributed_sampler(loader):
         return tensors
+    if check:
+        check_same_batch(tensors[0])
     n = tensors[0].shape[0]
     per = n // ws
     if per == 0:

@@ -304,8 +304,8 @@ class HerlevTrainer:
         if not train and ws > 1:
             broadcast_buffers(model)  # every rank validates rank 0's BatchNorm state
         tot, correct, total, skipped = [0.0] * 4, 0, 0, 0
-        for data, target in dataloader:
-            part = shard_batch(dataloader, data, target)
+        for batch_idx, (data, target) in enumerate(dataloader):
+            part = shard_batch(dataloader, data, target, check=batch_idx == 0)
             if part is None:
                 skipped += 1
                 continue

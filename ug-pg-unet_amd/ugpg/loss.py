@@ -89,7 +89,18 @@ class _WeightedMeanFn(torch.autograd.Function):
 
 def weighted_loss_tensors(loss_fn, output, target, uncertainty_map=None, alpha=1.0, out=None):
     """Device-side (final_loss, base_loss) -- no host synchronisation.  `out`: optional
-    2-float device buffer receiving [final, base] (fused BCE path).
+    2-float device buffer receiving [final, base] on every path (the trainer's metrics
+    buffer reads the losses from it)."""
+    final, base, filled = _weighted_loss(loss_fn, output, target, uncertainty_map, alpha, out)
+    if out is not None and not filled:
+        # non-fused criteria: a device-side copy, no host sync
+        out[0].copy_(final.detach().reshape(()))
+        out[1].copy_(base.detach().reshape(()))
+    return final, base
+
+
+def _weighted_loss(loss_fn, output, target, uncertainty_map, alpha, out):
+    """-> (final, base, filled): only the fused BCE path writes `out` itself.
 
     Semantics are the reference's (UG_unet.py:78-94) for any criterion:
     ``pixel = loss_fn(output, target)``; ``final = mean(pixel * (1 + alpha*U))`` (plain
@@ -103,23 +114,23 @@ def weighted_loss_tensors(loss_fn, output, target, uncertainty_map=None, alpha=1
         alpha_eff = 0.0
     if _fusable_bce(loss_fn, output, target, u):
         pw = _pos_weight_tensor(loss_fn, output)
-        return _UGBCEFn.apply(output, target, u, pw, alpha_eff, out)
+        return (*_UGBCEFn.apply(output, target, u, pw, alpha_eff, out), out is not None)
     pixel_loss = loss_fn(output, target)
     if pixel_loss.dim() == 0:
         # reduced criterion: torch.mean(s * w) == s * mean(w), w = 1 + alpha*U
         base = pixel_loss.detach()
         if u is None:
-            return pixel_loss, base
+            return pixel_loss, base, False
         w_mean = 1.0 + alpha_eff * ops.mean_std(u)[0]
-        return pixel_loss * w_mean, base
+        return pixel_loss * w_mean, base, False
     if _kernel_layout(pixel_loss, u):
-        return _WeightedMeanFn.apply(pixel_loss, u, alpha_eff)
+        return (*_WeightedMeanFn.apply(pixel_loss, u, alpha_eff), False)
     # any other broadcast between the criterion's output and U: the reference's
     # elementwise expression, evaluated by torch on the device
     base = torch.mean(pixel_loss.detach())
     if u is None:
-        return torch.mean(pixel_loss), base
-    return torch.mean(pixel_loss * (1.0 + alpha_eff * u)), base
+        return torch.mean(pixel_loss), base, False
+    return torch.mean(pixel_loss * (1.0 + alpha_eff * u)), base, False
 
 
 class UncertaintyGuidedLoss:

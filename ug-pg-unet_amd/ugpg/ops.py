@@ -89,12 +89,6 @@ if _conv_math not in _MATHS:
     raise ValueError(f"UGPG_CONV_MATH must be one of {_MATHS}, got {_conv_math!r}")
 
 
-for _knob in ("x6_pipe", "x6_wgrad", "fwd_cfg"):  # benchmarking knobs from the environment
-    _v = os.environ.get("UGPG_" + _knob.upper())
-    if _v is not None:
-        check(lib.ugpg_set_tuning(_knob.encode(), int(_v)), "set_tuning")
-
-
 def set_conv_math(math: str) -> None:
     """'x6': split-bf16 MFMA (fp32-accurate, 2.67x the fp32 MFMA rate) wherever the
     shape allows; 'f32': v_mfma_f32_32x32x2_f32 everywhere; 'bf16': bf16 arithmetic
@@ -281,10 +275,13 @@ def conv3x3_fwd(srcs, wpk, bias, cout, outs, split=None, accumulate=(0, 0), stat
     d.out_split = cout if split is None else split
     d.accumulate[0], d.accumulate[1] = int(accumulate[0]), int(accumulate[1])
     d.stats = ptr(stats)
+    if stats is not None:  # capacity in slots: the library refuses a call that would overflow
+        d.stats_slots = stats.numel() // (3 * cout)
     d.wfmt = wpk.ugpg_fmt
     if bnb is not None:
         (d.bnb_y, d.bnb_mean, d.bnb_invstd, d.bnb_scale, d.bnb_shift,
          d.bnb_part) = (ptr(t) for t in bnb)
+        d.bnb_slots = bnb[5].numel() // (3 * cout)
     if out16 is not None:
         d.out_bf16 = ptr(out16)
     _timed("conv3x3_fwd", flops,

@@ -86,7 +86,10 @@ class UncertaintyGuidedProgressiveTrainer:
         """Under torch.distributed (one process per GPU) make every rank's stage models
         equal to rank 0's: parameters and buffers at construction / after loading
         weights, BatchNorm buffers before validation and at stage end.
-        A no-op in a single process."""
+        A no-op in a single process.  COLLECTIVE: under data parallelism every rank must
+        call it (as it must call the constructor, load_stage_weights, train_epoch,
+        validate_epoch and train_progressive); an ``if rank == 0:`` around any of them
+        hangs the job."""
         if world()[1] <= 1:
             return
         for s in (stages or sorted(self.models)):
@@ -217,7 +220,7 @@ class UncertaintyGuidedProgressiveTrainer:
         pending = None  # batch k is read back after batch k+1 is enqueued
         skipped = 0
         for batch_idx, (data, target) in enumerate(dataloader):
-            part = shard_batch(dataloader, data, target)  # this rank's rows (DP)
+            part = shard_batch(dataloader, data, target, check=batch_idx == 0)  # this rank's rows
             if part is None:
                 skipped += 1
                 continue
@@ -255,8 +258,14 @@ class UncertaintyGuidedProgressiveTrainer:
         save_path.mkdir(exist_ok=True)
         rank, _ = world()
         print("Starting Uncertainty-Guided Progressive Growing U-Net Training")
+        print("=" * 60)
         for stage in range(1, max_stages + 1):
+            res = self.stage_configs[stage]["resolution"]
             print(f"\nStarting Stage {stage}")
+            print(f"Resolution: {res}x{res}")
+            if stage > 1:
+                print(f"Using uncertainty-guided loss weighting (alpha={self.uncertainty_alpha})")
+            print("-" * 40)
             if stage > 1:
                 self.transfer_weights(stage - 1, stage)
             self.current_stage = stage
@@ -279,6 +288,8 @@ class UncertaintyGuidedProgressiveTrainer:
                 print(f"Stage {stage}, Epoch {epoch + 1}/{epochs} ({time.time() - t0:.2f}s)")
                 print(f"Train - Loss: {tr[0]:.4f}, Base: {tr[1]:.4f}, Dice: {tr[2]:.4f}, Acc: {tr[3]:.4f}")
                 print(f"Val   - Loss: {va[0]:.4f}, Base: {va[1]:.4f}, Dice: {va[2]:.4f}, Acc: {va[3]:.4f}")
+                if stage > 1:
+                    print(f"Uncertainty - Mean: {va[4]:.4f}, Std: {va[5]:.4f}")
                 # validation used rank 0's BatchNorm buffers on every rank, so the
                 # checkpoint decision below is the same everywhere
                 if va[2] > best:
@@ -291,6 +302,7 @@ class UncertaintyGuidedProgressiveTrainer:
                                     "uncertainty_alpha": self.uncertainty_alpha,
                                     "history": self.history},
                                    save_path / f"ug_pgunet_stage{stage}_best.pth")
+                print("-" * 60)
             # the finished stage becomes the next stage's U-map producer: one BN state
             self.sync_replicas([stage], buffers_only=True)
         print("Uncertainty-guided progressive training completed!")
@@ -323,6 +335,9 @@ class UncertaintyGuidedProgressiveTrainer:
         plt.close(fig)
 
     def load_stage_weights(self, stage, checkpoint_path):
+        """Load a checkpoint (dict with model_state_dict, or a raw state_dict) into
+        models[stage] (uncertainty_guided_trainer.py:469-473).  COLLECTIVE under data
+        parallelism: every rank calls it, then rank 0's weights are broadcast."""
         ck = torch.load(checkpoint_path, map_location=self.device, weights_only=True)
         self.models[stage].load_state_dict(ck["model_state_dict"] if "model_state_dict" in ck else ck)
         self.sync_replicas([stage])
