@@ -44,8 +44,11 @@ typedef struct {
     const float* scale;
     const float* shift;
     int C;
-    /* optional bf16 copy of data (round to nearest even), read instead of data by the
-     * single-piece (UGPG_WFMT_BF16) persistent conv forms; NULL: none */
+    /* the same activation stored in bf16 (round to nearest even): with data == NULL the
+     * only storage (the bf16 arithmetic's activation storage, read by the single-piece
+     * persistent conv forms, their weight gradient, max-pool, bilinear x2, the heads,
+     * avgpool and BatchNorm backward); with data != NULL an optional copy the
+     * single-piece persistent conv forms read instead; NULL: none */
     const void* data_bf16;
 } ugpg_src_t;
 
@@ -95,14 +98,18 @@ typedef struct {
      * (the capacity of bnb_part in slots; else UGPG_ERR_WORKSPACE).  Forms whose
      * epilogue does not fuse it run the reduction as a separate pass, same layout. */
     const float* bnb_y;
+    const void* bnb_y_bf16;  /* the BN input stored in bf16 instead (bnb_y == NULL) */
     const float* bnb_mean;
     const float* bnb_invstd;
     const float* bnb_scale;
     const float* bnb_shift;
     float* bnb_part;
     int bnb_slots;         /* capacity of bnb_part in slots */
-    /* optional bf16 copy of out[0] (one output, no accumulate): written beside it, for
-     * the next conv's ugpg_src_t.data_bf16 (the bf16 arithmetic's activation storage) */
+    /* bf16 output (one output, no accumulate): with out[0] != NULL a copy written beside
+     * it; with out[0] == NULL the only storage of the output (the bf16 arithmetic's
+     * activation storage: the BatchNorm partials then describe the rounded values) --
+     * supported by the persistent single-piece form (images >= 32 wide) and the
+     * image-layer kernel */
     void* out_bf16;
 } ugpg_conv_t;
 
@@ -185,7 +192,8 @@ size_t ugpg_bn_relu_bwd_partials_workspace(int C);
  * upsampling and head backward entries *_bnb): same partial layout, nslots from
  * ugpg_bnb_slots(npix, C) (0 for unsupported shapes). */
 typedef struct {
-    const float* y;        /* NHWC [npix][C]: the BN input */
+    const float* y;        /* NHWC [npix][C]: the BN input (fp32) ... */
+    const void* y_bf16;    /* ... or stored in bf16 (y == NULL; the bf16 arithmetic) */
     const float* mean;
     const float* invstd;
     const float* scale;
@@ -194,15 +202,17 @@ typedef struct {
     int nslots;
 } ugpg_bnb_t;
 int ugpg_bnb_slots(int64_t npix, int C);
+/* (y: the BN input in fp32, or y == NULL and y_bf16 its bf16 storage) */
 int ugpg_bn_relu_bwd_partials(const float* part, int nslots, const float* da, const float* y,
-                              int64_t npix, int C, const float* mean, const float* invstd,
-                              const float* scale, const float* shift, float* dy, float* dgamma,
-                              float* dbeta, float* dconv_bias, int accumulate_params, void* ws,
-                              size_t ws_bytes, void* stream);
-int ugpg_bn_relu_bwd(const float* da, const float* y, int64_t npix, int C, const float* mean,
-                     const float* invstd, const float* scale, const float* shift,
-                     float* dy, float* dgamma, float* dbeta, float* dconv_bias,
-                     int accumulate_params, void* ws, size_t ws_bytes, void* stream);
+                              const void* y_bf16, int64_t npix, int C, const float* mean,
+                              const float* invstd, const float* scale, const float* shift,
+                              float* dy, float* dgamma, float* dbeta, float* dconv_bias,
+                              int accumulate_params, void* ws, size_t ws_bytes, void* stream);
+int ugpg_bn_relu_bwd(const float* da, const float* y, const void* y_bf16, int64_t npix, int C,
+                     const float* mean, const float* invstd, const float* scale,
+                     const float* shift, float* dy, float* dgamma, float* dbeta,
+                     float* dconv_bias, int accumulate_params, void* ws, size_t ws_bytes,
+                     void* stream);
 /* Materialise relu(scale*y+shift) (used only for the standalone block API). */
 int ugpg_bn_relu_apply(ugpg_src_t src, int64_t npix, float* out, void* stream);
 
@@ -216,8 +226,11 @@ int ugpg_maxpool2_bwd_bnb(const float* dout, const uint8_t* argmax, int B, int H
                           float* din, int accumulate, const ugpg_bnb_t* bnb, void* stream);
 
 /* ---- align_corners=True bilinear resize, NHWC (UG_unet_parts.py:78, K9) ---- */
+/* out == NULL: the result is stored in bf16 at out_bf16 (the bf16 arithmetic's storage of
+ * an Up conv's upsampled input -- which that conv and its weight gradient round to bf16
+ * anyway); else out_bf16 is ignored */
 int ugpg_bilinear_nhwc_fwd(ugpg_src_t src, int B, int Hi, int Wi, float* out, int Ho, int Wo,
-                           void* stream);
+                           void* out_bf16, void* stream);
 int ugpg_bilinear_nhwc_bwd(const float* dout, int B, int Ho, int Wo, int C, float* din, int Hi,
                            int Wi, int accumulate, void* stream);
 /* The same, also writing the BatchNorm-backward partials of din (see ugpg_bnb_t), one

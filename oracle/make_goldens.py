@@ -898,6 +898,56 @@ def g12b(RU):
     save_npz("g12b_progressive_dp2.npz", **fx)
 
 
+def bf16_oracle_step(state, prev, x, t, perturb=None):
+    """The config-2 UG step (bs16 x 256^2) in the build's bf16 arithmetic (config 3):
+    oracle.ref_cpu with CONV_MATH = "bf16" (bf16 conv operands, fp32 accumulation, conv
+    outputs of images >= 32 wide stored in bf16) for the current AND the U-map stage.
+    perturb = (seed, rel): every weight scaled by (1 + rel*N(0,1)) first."""
+    from tests._parity import oracle_run, perturbed_state
+    if perturb is not None:
+        state = perturbed_state(state, *perturb)
+    O.CONV_MATH = "bf16"
+    try:
+        u = O.uncertainty_map(3, prev, x, 128, 256)
+        logits, final, base, g, _ = oracle_run(4, state, x, t, umap=u)
+    finally:
+        O.CONV_MATH = "f32"
+    return logits, final, u, g
+
+
+def g4c(RU):
+    """Config 3's arithmetic at the benchmarked size: per-tensor spread of the bf16
+    oracle's own gradients under ulp-level weight perturbations (the §8d floor method
+    transplanted to bf16 -- an equally valid fp32 summation order moves bf16 roundings,
+    and train-mode BatchNorm amplifies them), plus logits / loss / U spreads.  The GPU
+    test bounds max|g_hip - g_oracle16| by 3x this floor per tensor.  (The bf16 arithmetic
+    is the build's, not the reference's: the reference is fp32-only; its fp32 step is
+    pinned by G4b.)"""
+    from tests._parity import FLOOR_PERTURBATIONS
+    c = G4B
+    state = det_state(4, 3, 1, seed=c["w_seed"])
+    prev = det_state(3, 3, 1, seed=c["prev_seed"])
+    x = G.randn(c["x_seed"], (c["B"], 3, c["res"], c["res"]), "x")
+    t = G.bernoulli(c["t_seed"], (c["B"], 1, c["res"], c["res"]), 0.5, "t")
+    l0, f0, u0, g0 = bf16_oracle_step(state, prev, x, t)
+    keys = param_keys(state)
+    floor = {k: 0.0 for k in keys}
+    lf = uf = ff = 0.0
+    for s, rel in FLOOR_PERTURBATIONS:
+        lp, fp, up, gp = bf16_oracle_step(state, prev, x, t, perturb=(s, rel))
+        for k in keys:
+            floor[k] = max(floor[k], (gp[k].double() - g0[k].double()).abs().max().item())
+        lf = max(lf, (lp - l0).abs().max().item())
+        ff = max(ff, abs(fp.item() - f0.item()))
+        print(f"g4c perturbation {s} {rel}: logits spread {lf:.3e}, loss {ff:.3e}", flush=True)
+    fx = {"loss": np.array([f0.item()]), "floor_logits": np.array([lf]),
+          "floor_loss": np.array([ff]), "u_stats": np.array([u0.mean().item(), u0.std().item()])}
+    for k in keys:
+        fx[f"floor16/{k}"] = np.array([floor[k], g0[k].abs().max().item()])
+        fx[f"grad16/{k}"] = tstats(k, g0[k])
+    save_npz("g4c_bf16_floor.npz", **fx)
+
+
 def g0(RU):
     """state_dict keys/shapes/dtypes of every reference model (checkpoint format)."""
     out = {}

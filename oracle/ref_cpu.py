@@ -142,49 +142,39 @@ def conv3x3(x, w, b):
     return F.conv2d(x, w, b, padding=1)
 
 
-def _bn_relu_q(P, pre, y, training):
-    """relu(bn(y)) with y's batch statistics (or the running ones in eval) applied to
-    bf16(y): what the build's bf16 arithmetic feeds a conv that reads the bf16 copy of a
-    conv output (images >= 32 wide, engine.double_conv_forward); no buffer updates."""
-    if training:
-        mean = y.mean((0, 2, 3))
-        var = y.var((0, 2, 3), unbiased=False)
-    else:
-        mean, var = P[pre + ".running_mean"], P[pre + ".running_var"]
-    r = lambda t: t[None, :, None, None]
-    xh = (_bq(y) - r(mean)) * r(torch.rsqrt(var + BN_EPS))
-    return F.relu(xh * r(P[pre + ".weight"]) + r(P[pre + ".bias"]))
+class _Bf16StoreST(torch.autograd.Function):
+    """A conv output stored in bf16 (value rounded to nearest even) whose gradient passes
+    straight through: the build's bf16 arithmetic keeps conv outputs in bf16 storage and
+    differentiates at the stored value, with fp32 gradients."""
+
+    @staticmethod
+    def forward(ctx, y):
+        return _bq(y)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
 
 
-# the build's bf16 activation copies (ugpg.engine._BF16_STORE, off by default: measured
-# slower, DESIGN §9)
-BF16_STORE = False
+# The build's bf16 arithmetic (BASELINE config 3) stores every conv output of an image
+# >= 32 wide in bf16 (ugpg.engine: torch.autocast's bf16 conv outputs): BatchNorm then sees
+# -- and its statistics describe -- the rounded values.  Off only for experiments.
+BF16_STORE = True
 
 
 def _bf16_store(y):
-    """Does the build keep a bf16 copy of this conv output for the next conv?"""
+    """Does the build store this conv output in bf16?"""
     return CONV_MATH == "bf16" and BF16_STORE and y.shape[-1] >= 32
 
 
 def double_conv(P, prefix, x, training):
     """Two conv -> BN -> ReLU.  Under CONV_MATH "bf16" a conv output of an image >= 32
-    wide reaches the next conv through its bf16 copy: conv1's input takes the value of
-    _bn_relu_q of conv0's output, and the block output carries that form in `._ugpg_q`
-    for an Up block's skip input (the max-pool, upsampling and heads read the fp32
-    output).  The build's backward differentiates relu(bn(y)) at the fp32 y (its BN
-    backward reads y), so the q form enters straight-through: value q, gradient of the
-    fp32 activation."""
-    xin = x
+    wide is stored in bf16 before its BatchNorm (see _bf16_store)."""
     for conv_i, bn_i in ((0, 1), (3, 4)):
-        y = conv3x3(xin, P[f"{prefix}.{conv_i}.weight"], P[f"{prefix}.{conv_i}.bias"])
-        x = F.relu(_bn(P, f"{prefix}.{bn_i}", y, training))
-        xin = x
+        y = conv3x3(x, P[f"{prefix}.{conv_i}.weight"], P[f"{prefix}.{conv_i}.bias"])
         if _bf16_store(y):
-            with torch.no_grad():
-                q = _bn_relu_q(P, f"{prefix}.{bn_i}", y, training)
-            xin = x + (q - x).detach()
-    if _bf16_store(x):
-        x._ugpg_q = xin
+            y = _Bf16StoreST.apply(y)
+        x = F.relu(_bn(P, f"{prefix}.{bn_i}", y, training))
     return x
 
 
@@ -194,7 +184,6 @@ def down(P, name, x, training):
 
 def up(P, name, low, skip, training):
     low = F.interpolate(low, scale_factor=2, mode="bilinear", align_corners=True)
-    skip = getattr(skip, "_ugpg_q", skip)  # the bf16 copy the skip conv reads (bf16 math)
     return double_conv(P, block_prefix(name), torch.cat([skip, low], dim=1), training)
 
 

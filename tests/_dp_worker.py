@@ -11,7 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "ug-pg-unet_amd")]
 
 
-def main(outdir):
+def main(outdir, math="x6"):
     import torch
     import torch.distributed as dist
     from torch.utils.data import DataLoader, TensorDataset
@@ -23,6 +23,8 @@ def main(outdir):
     dist.init_process_group("gloo")
     torch.manual_seed(1000 + rank)               # replicas start different on purpose
     import ugpg
+    from ugpg import ops
+    ops.set_conv_math(math)  # "bf16": config 3 -- bf16 convs AND bf16 gradient exchange
     tr = ugpg.UncertaintyGuidedProgressiveTrainer(3, 1, device="cuda", uncertainty_alpha=1.0)
     p0 = {k: v.detach().cpu().clone() for k, v in tr.models[3].state_dict().items()}
     stage = c["stage"]
@@ -40,7 +42,25 @@ def main(outdir):
     tup = tr.train_epoch(DataLoader(TensorDataset(x, t), batch_size=c["B"]), stage)
     torch.cuda.synchronize()
     m = tr.models[stage]
-    torch.save({"tuple": tup,
+    # this rank's own (pre-exchange) gradient: the same step on a fresh replica of the
+    # initial weights, outside any data-parallel exchange
+    local = {}
+    if math == "bf16":
+        import torch.nn as nn
+        fresh = ugpg.PGUNet2(3, 1).to("cuda")
+        fresh.load_state_dict(det_state(stage, 3, 1, seed=c["w_seed"]))
+        fresh.train()
+        per = c["B"] // 2
+        xs = x[rank * per:(rank + 1) * per].cuda()
+        ts = t[rank * per:(rank + 1) * per].cuda()
+        u = tr.uncertainty_loss.generate_uncertainty_map(xs, tr.models[stage - 1], 32, 64)
+        crit = nn.BCEWithLogitsLoss(pos_weight=torch.tensor([5.0], device="cuda"),
+                                    reduction="none")
+        f, _ = tr.uncertainty_loss.apply_uncertainty_weighted_loss(crit, fresh(xs), ts, u, 1.0)
+        f.backward()
+        torch.cuda.synchronize()
+        local = {k: p.grad.detach().cpu() for k, p in fresh.named_parameters()}
+    torch.save({"tuple": tup, "local": local,
                 "grads": {k: p.grad.detach().cpu() for k, p in m.named_parameters()},
                 "state": {k: v.detach().cpu() for k, v in m.state_dict().items()},
                 "ctor_s3": p0,
@@ -51,4 +71,4 @@ def main(outdir):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], *(sys.argv[2:3]))

@@ -45,12 +45,11 @@ def _oracle_avg(c, dtype, state=None):
     return {k: v / c["shards"] for k, v in acc.items()}
 
 
-def test_dp_two_ranks_match_shard_mean(tmp_path):
-    from oracle.make_goldens import G8 as c
+def _run_ranks(tmp_path, *args):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
                WORLD_SIZE="2", HSA_ENABLE_IPC_MODE_LEGACY="0")
     procs = [subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "_dp_worker.py"),
-                               str(tmp_path)], env=dict(env, RANK=str(r), LOCAL_RANK=str(r)),
+                               str(tmp_path), *args], env=dict(env, RANK=str(r), LOCAL_RANK=str(r)),
                               cwd=ROOT)
              for r in range(2)]
     try:
@@ -60,7 +59,12 @@ def test_dp_two_ranks_match_shard_mean(tmp_path):
             if p.poll() is None:
                 p.kill()
     assert rcs == [0, 0], rcs
-    res = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(2)]
+    return [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(2)]
+
+
+def test_dp_two_ranks_match_shard_mean(tmp_path):
+    from oracle.make_goldens import G8 as c
+    res = _run_ranks(tmp_path)
     # replicas: constructor broadcast, load_stage_weights broadcast, identical step
     for k, v in res[0]["ctor_s3_after"].items():
         assert torch.equal(v, res[1]["ctor_s3_after"][k]), k
@@ -104,3 +108,49 @@ def test_dp_two_ranks_match_shard_mean(tmp_path):
             continue  # noise-level gradient (true value 0): its RMSprop signs are arbitrary
         p = res[0]["state"][k].double()
         assert abs(p.norm().item() - fx[f"post/{k}"][0]) <= 1e-4 * fx[f"post/{k}"][0] + 1e-6, k
+
+
+def test_dp_two_ranks_bf16_exchange(tmp_path):
+    """Config 3's data parallelism on the HIP path: bf16 conv arithmetic AND the bf16
+    gradient exchange (dist._Bf16Work: RNE cast kernels around the all-reduce, summed back
+    into the fp32 flat buffer) in two fresh processes (gloo, both on cuda:0) on the halves
+    of the G8 batch.  The exchanged gradient must equal bf16(bf16(g_0) + bf16(g_1)) of the
+    two ranks' own gradients bit for bit, on both ranks; each rank's own gradient must be
+    the bf16 oracle's for its shard within the bf16 floor rule (the oracle's spread under
+    ulp-level weight perturbations, x3)."""
+    from oracle.make_goldens import G8 as c
+    from tests._parity import FLOOR_PERTURBATIONS
+    res = _run_ranks(tmp_path, "bf16")
+    for k, v in res[0]["grads"].items():
+        assert torch.equal(v, res[1]["grads"][k]), f"exchanged gradient differs across ranks: {k}"
+    for k, v in res[0]["grads"].items():
+        q = lambda t: t.to(torch.bfloat16)
+        want = (q(res[0]["local"][k]).float() + q(res[1]["local"][k]).float()).to(torch.bfloat16)
+        assert torch.equal(v, want.float()), f"bf16 exchange of {k}"
+    # each rank's own gradient vs the bf16 oracle on its shard
+    state = det_state(c["stage"], 3, 1, seed=c["w_seed"])
+    prev = det_state(c["stage"] - 1, 3, 1, seed=c["prev_seed"])
+    x = G.randn(c["x_seed"], (c["B"], 3, c["res"], c["res"]), "x")
+    t = G.bernoulli(c["t_seed"], (c["B"], 1, c["res"], c["res"]), 0.5, "t")
+    per = c["B"] // 2
+    O.CONV_MATH = "bf16"
+    try:
+        for r in range(2):
+            xs, ts = x[r * per:(r + 1) * per], t[r * per:(r + 1) * per]
+            u = O.uncertainty_map(1, prev, xs, 32, 64)
+            _, _, _, g16, _ = oracle_run(c["stage"], state, xs, ts, umap=u)
+            floor = {k: 0.0 for k in g16}
+            for sd, rel in FLOOR_PERTURBATIONS[:5]:
+                _, _, _, gp, _ = oracle_run(c["stage"], perturbed_state(state, sd, rel), xs, ts,
+                                            umap=u)
+                for k in floor:
+                    floor[k] = max(floor[k], (gp[k].double() - g16[k].double()).abs().max().item())
+            bad = []
+            for k in param_keys(state):
+                err = (res[r]["local"][k].double() - g16[k].double()).abs().max().item()
+                bound = 1e-5 if is_prebn_bias(k) else 3 * floor[k] + 1e-6 * g16[k].abs().max().item()
+                if err > bound:
+                    bad.append(f"rank {r} {k}: {err:.3e} > {bound:.3e}")
+            assert not bad, "\n".join(bad[:20])
+    finally:
+        O.CONV_MATH = "f32"

@@ -165,6 +165,41 @@ def test_trainer_epoch_golden(dev):
         assert abs(tup[4] - ref[4]) <= 1e-5 and abs(tup[5] - ref[5]) <= 1e-5
 
 
+def _steps_with_umap_stream(dev, side, nsteps=3, B=4, res=256):
+    import ugpg
+    tr = ugpg.UncertaintyGuidedProgressiveTrainer(3, 1, device=dev, uncertainty_alpha=1.0)
+    tr.models[3].load_state_dict(det_state(3, 3, 1, seed=13))
+    tr.models[4].load_state_dict(det_state(4, 3, 1, seed=0))
+    tr.current_stage, tr.current_model = 4, tr.models[4]
+    tr.setup_optimizer(4)
+    tr.umap_side_stream = side
+    x = G.randn(5, (B, 3, res, res), "x").to(dev)
+    t = G.bernoulli(6, (B, 1, res, res), 0.5, "t").to(dev)
+    rows = []
+    for _ in range(nsteps):
+        # a fresh (resized) input every step, as the epoch loop produces it
+        d, tt = tr._resize_batch(x * 1.0, t, res)
+        rows.append(tr.train_step(d, tt, 4))
+    torch.cuda.synchronize()
+    return ([r.cpu() for r in rows],
+            {k: v.detach().cpu().clone() for k, v in tr.models[4].state_dict().items()})
+
+
+def test_umap_side_stream_is_bit_identical(dev):
+    """The U map's previous-stage forward on a second HIP stream (trainer default) gives
+    results bit-identical to the one-stream order, run after run: metrics of every step,
+    every parameter and BatchNorm buffer after three RMSprop steps (a side-
+    stream experiment once varied at 5e-5; the ordering rules are in
+    UncertaintyGuidedProgressiveTrainer._umap_on_side)."""
+    ref_rows, ref_state = _steps_with_umap_stream(dev, False)
+    for rep in range(2):
+        rows, state = _steps_with_umap_stream(dev, True)
+        for i, (a, b) in enumerate(zip(ref_rows, rows)):
+            assert torch.equal(a, b), (rep, i, a.tolist(), b.tolist())
+        for k, v in ref_state.items():
+            assert torch.equal(v, state[k]), (rep, k)
+
+
 @pytest.mark.parametrize("reduction", ["mean", "sum"])
 def test_trainer_epoch_reduced_criterion(dev, reduction):
     """A subclass-style base_criterion with reduction='mean'/'sum' (not the fused kernel):
@@ -288,16 +323,16 @@ def test_backward_reports_gradients_back_to_front(dev, monkeypatch):
 @pytest.mark.parametrize("res", [64, 256])
 def test_bf16_train_step(dev, res):
     """bf16 arithmetic (BASELINE config 3): every 3x3 conv with bf16-rounded operands
-    (forward x, W; data gradient dy, W; weight gradient dy, x), fp32 accumulation and
-    storage.  Each conv is exact to that arithmetic (test_gpu_ops.py, math "bf16");
-    through the network, a few-ulp fp32 difference upstream (fmaf-folded BatchNorm
-    vs the oracle's (y-mean)*invstd*w+b, summation order) moves values across bf16
-    rounding boundaries, and train-mode BatchNorm's backward (g - mean(g) -
-    xhat*mean(g*xhat)) amplifies that noise, so the network is compared with
-    tolerances: vs the oracle in the same arithmetic (CONV_MATH = "bf16") logits
-    within 2 % of their range, loss 0.5 %, per-tensor gradient cosine median > 0.95
-    and min > 0.9; vs the fp32 reference loss within 1 %, Dice within 0.01."""
+    (forward x, W; data gradient dy, W; weight gradient dy, x), fp32 accumulation, conv
+    outputs of images >= 32 wide stored in bf16.  Each kernel is exact to that arithmetic
+    (test_gpu_ops.py); through the network an fp32 summation-order difference moves values
+    across bf16 rounding boundaries and train-mode BatchNorm's backward amplifies it, so
+    the network is held to the bf16 oracle's OWN spread: per tensor, max|g_hip - g16| <=
+    3 x max over ulp-perturbed bf16 oracle runs of |g16_perturbed - g16| + 1e-6 of scale
+    (the §8d floor method in bf16); logits and loss likewise; vs the fp32 reference loss
+    within 1 %, Dice within 0.01."""
     import torch.nn as nn
+    from tests._parity import FLOOR_PERTURBATIONS
     from ugpg import ops
     from ugpg.loss import UncertaintyGuidedLoss
     state = det_state(4, 3, 1)
@@ -307,6 +342,14 @@ def test_bf16_train_step(dev, res):
     O.CONV_MATH = "bf16"
     try:
         logits16, final16, _, g16, _ = oracle_run(4, state, x, t)
+        floor = {k: 0.0 for k in g16}
+        lfl = ffl = 0.0
+        for sd, rel in FLOOR_PERTURBATIONS[:5]:
+            lp, fp, _, gp, _ = oracle_run(4, perturbed_state(state, sd, rel), x, t)
+            for k in floor:
+                floor[k] = max(floor[k], (gp[k].double() - g16[k].double()).abs().max().item())
+            lfl = max(lfl, (lp - logits16).abs().max().item())
+            ffl = max(ffl, abs(fp.item() - final16.item()))
     finally:
         O.CONV_MATH = "f32"
     old = ops.conv_math()
@@ -321,25 +364,23 @@ def test_bf16_train_step(dev, res):
     finally:
         ops.set_conv_math(old)
     o = out.detach().cpu()
-    err16 = (o - logits16).abs().max().item() / (logits16.max() - logits16.min()).item()
-    err32 = (o - logits32).abs().max().item() / (logits32.max() - logits32.min()).item()
-    coss = {}
+    lerr = (o - logits16).abs().max().item()
+    assert lerr <= 3 * lfl + 1e-6 * logits16.abs().max().item(), (lerr, lfl)
+    assert abs(final.item() - final16.item()) <= 3 * ffl + 1e-6 * abs(final16.item())
+    bad, ratios = [], []
     for k, p in zip(param_keys(state), m.parameters()):
-        if is_prebn_bias(k):
-            continue
-        a, b = p.grad.detach().cpu().double().flatten(), g16[k].double().flatten()
-        coss[k] = (a @ b / (a.norm() * b.norm() + 1e-30)).item()
-    worst = min(coss, key=coss.get)
+        err = (p.grad.detach().cpu().double() - g16[k].double()).abs().max().item()
+        bound = 1e-5 if is_prebn_bias(k) else 3 * floor[k] + 1e-6 * g16[k].abs().max().item()
+        ratios.append((err / bound, k))
+        if err > bound:
+            bad.append(f"{k}: {err:.3e} > {bound:.3e}")
+    ratios.sort(reverse=True)
     d = O.dice(O.predictions(o), t).item()
     d32 = O.dice(O.predictions(logits32), t).item()
-    med = float(np.median(list(coss.values())))
-    print(f"bf16 res {res}: logits vs bf16 oracle {err16:.2e}, vs fp32 {err32:.2e}; loss "
-          f"{final.item():.6f} vs {final16.item():.6f} (bf16 oracle) {final32.item():.6f} (fp32); "
-          f"grad cosine vs bf16 oracle median {med:.4f} min {coss[worst]:.4f} ({worst}); "
-          f"dice {d:.4f} vs fp32 {d32:.4f}")
-    assert err16 < 2e-2, err16
-    assert abs(final.item() - final16.item()) <= 5e-3 * abs(final16.item())
-    assert med > 0.95 and coss[worst] > 0.9, (med, worst, coss[worst])
+    print(f"bf16 res {res}: logits err {lerr:.2e} (spread {lfl:.2e}); loss {final.item():.6f} vs "
+          f"{final16.item():.6f} (bf16 oracle) {final32.item():.6f} (fp32); gradient headroom "
+          f"worst {[(round(r, 3), k) for r, k in ratios[:3]]}; dice {d:.4f} vs fp32 {d32:.4f}")
+    assert not bad, "bf16 gradient parity failures:\n" + "\n".join(bad[:20])
     assert abs(final.item() - final32.item()) <= 1e-2 * abs(final32.item())
     assert abs(d - d32) <= 1e-2, (d, d32)
 

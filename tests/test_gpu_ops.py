@@ -393,33 +393,145 @@ def test_bf16_casts(dev):
 
 
 @pytest.mark.parametrize("case", [(2, 32, 40, 64, 0, 128), (1, 36, 64, 64, 64, 64),
-                                  (2, 24, 20, 64, 0, 64), (2, 40, 48, 8, 0, 64)])
-def test_conv_bf16_activation_copies(dev, case):
-    """bf16 arithmetic with bf16 activation copies: out16 == bf16(out) for every kernel
-    form (persistent epilogue, image kernel, cast pass), and a source read through its
-    bf16 copy gives the same output as the fp32 source when y is bf16-exact."""
+                                  (2, 40, 48, 8, 0, 64)])
+def test_conv_bf16_storage(dev, case):
+    """bf16 activation storage (the bf16 arithmetic's, config 3): a conv whose output is
+    stored in bf16 only writes exactly bf16(the fp32 output) -- persistent single-piece
+    epilogue and the image-layer kernel -- with BatchNorm statistics of the rounded values;
+    a source stored in bf16 gives the same output as its fp32 form (bf16-exact values)."""
     from ugpg import ops
     B, H, W, C0, C1, Cout = case
     old = ops.conv_math()
     ops.set_conv_math("bf16")
     try:
         cin = C0 + C1
-        y0 = nhwc(rnd((B, C0, H, W), 80, "y0")).to(torch.bfloat16).float().to(dev)
-        y1 = nhwc(rnd((B, C1, H, W), 81, "y1")).to(dev) if C1 else None
+        q = lambda t: t.to(torch.bfloat16).float()
+        y0 = q(nhwc(rnd((B, C0, H, W), 80, "y0"))).to(dev)
+        y1 = q(nhwc(rnd((B, C1, H, W), 81, "y1"))).to(dev) if C1 else None
         sc = (rnd((C0,), 82, "s", 0.5) + 1).to(dev) if C0 % 16 == 0 else None
         sh = rnd((C0,), 83, "h", 0.2).to(dev) if sc is not None else None
         w = rnd((Cout, cin, 3, 3), 84, "w", 0.05).to(dev)
+        b = rnd((Cout,), 85, "b", 0.1).to(dev)
         wpk = ops.pack_conv3x3(w, ops.conv_pack_k(cin), 0)
+        nt = ops.conv_ntiles(B, H, W, cin, Cout, wpk)
+        res = {}
+        for src16 in (False, True):
+            if src16 and C0 == 8:
+                continue  # the image is an fp32 input
+            s0 = ops.Act(y0.to(torch.bfloat16) if src16 else y0, sc, sh)
+            srcs = [s0] + ([ops.Act(y1.to(torch.bfloat16) if src16 else y1)] if C1 else [])
+            for out16 in (False, True):
+                out = torch.empty(B, H, W, Cout, device=dev,
+                                  dtype=torch.bfloat16 if out16 else torch.float32)
+                st = torch.empty(3 * Cout * nt, device=dev)
+                ops.conv3x3_fwd(srcs, wpk, b, Cout, [out], stats=st)
+                res[src16, out16] = (out, st)
+        ref, st_ref = res[False, False]
+        for (src16, out16), (out, st) in res.items():
+            want = ref.to(torch.bfloat16) if out16 else ref
+            assert torch.equal(out, want), (src16, out16)
+            # statistics of the stored values
+            gam, bet = torch.ones(Cout, device=dev), torch.zeros(Cout, device=dev)
+            mean, invstd, _, _ = ops.bn_finalize(st, nt, gam, bet, None, None, None, 0.1, 1e-5)
+            v = out.float().reshape(-1, Cout).double()
+            close(mean.cpu(), v.mean(0).cpu(), 1e-5, "bn mean of the stored values")
+            close(invstd.cpu(), (1 / torch.sqrt(v.var(0, unbiased=False) + 1e-5)).cpu(), 1e-5,
+                  "bn invstd of the stored values")
+    finally:
+        ops.set_conv_math(old)
+
+
+@pytest.mark.parametrize("math", ["bf16", "x6"])
+def test_bf16_stored_bn_input(dev, math):
+    """Every reader of a BatchNorm input y (a conv output) accepts its bf16 storage and
+    gives exactly the result of the fp32 form of the same (bf16-exact) values: max-pool,
+    bilinear x2 (also storing its result in bf16), the heads forward/backward, BatchNorm
+    backward (reduce, apply, and the partials fused into max-pool / bilinear / head
+    backward and the data gradient's epilogue) and the bf16 weight gradient."""
+    from ugpg import ops
+    old = ops.conv_math()
+    ops.set_conv_math(math)
+    try:
+        B, H, W, C = 2, 32, 40, 64
+        q = lambda t: t.to(torch.bfloat16).float()
+        y = q(nhwc(rnd((B, C, H, W), 90, "y") * 2 + 0.3)).to(dev)
+        y16 = y.to(torch.bfloat16)
+        sc, sh = (rnd((C,), 91, "s", 0.5) + 1).to(dev), rnd((C,), 92, "h", 0.3).to(dev)
+        mean, invstd = rnd((C,), 93, "m", 0.1).to(dev), (rnd((C,), 94, "i").abs() + 0.5).to(dev)
+        st = (mean, invstd, sc, sh)
+        eq = lambda a_, b_, what: (torch.equal(a_, b_) or pytest.fail(what))
+        # max-pool forward / backward with fused partials
+        (p32, am32), (p16, am16) = (ops.maxpool2_fwd(ops.Act(t, sc, sh)) for t in (y, y16))
+        eq(p32, p16, "maxpool fwd")
+        eq(am32, am16, "maxpool argmax")
+        dout = nhwc(rnd((B, C, H // 2, W // 2), 95, "dp")).to(dev)
+        parts = []
+        for t in (y, y16):
+            din = torch.empty(B, H, W, C, device=dev)
+            parts.append((din, ops.maxpool2_bwd(dout, am32, H, W, din, 0, bnb=(t, *st))))
+        eq(parts[0][0], parts[1][0], "maxpool bwd")
+        eq(parts[0][1], parts[1][1], "maxpool bwd partials")
+        # BatchNorm backward, standalone and from partials
         outs = []
-        for use16 in (False, True):
-            a0 = ops.Act(y0, sc, sh, y0.to(torch.bfloat16) if use16 else None)
-            srcs = [a0] + ([ops.Act(y1)] if C1 else [])
-            out = torch.empty(B, H, W, Cout, device=dev)
-            o16 = torch.empty(B, H, W, Cout, device=dev, dtype=torch.bfloat16)
-            ops.conv3x3_fwd(srcs, wpk, None, Cout, [out], out16=o16)
-            assert torch.equal(o16, out.to(torch.bfloat16)), "out16 must be bf16(out)"
-            outs.append(out)
-        assert torch.equal(outs[0], outs[1]), "bf16 copy read must equal the fp32 read"
+        for t in (y, y16):
+            dy = torch.empty(B, H, W, C, device=dev)
+            dg, dbt, dcb = (torch.empty(C, device=dev) for _ in range(3))
+            ops.bn_relu_bwd(parts[0][0], t, *st, dy, dg, dbt, dcb)
+            dy2 = torch.empty_like(dy)
+            ops.bn_relu_bwd(parts[0][0], t, *st, dy2, dg, dbt, dcb, part=parts[0][1])
+            outs.append((dy, dy2, dg, dbt))
+        for a_, b_ in zip(*outs):
+            eq(a_, b_, "bn_relu_bwd")
+        # bilinear x2: fp32 and bf16 results; backward partials
+        u32 = ops.bilinear_nhwc_fwd(ops.Act(y, sc, sh), 2 * H, 2 * W)
+        u16 = ops.bilinear_nhwc_fwd(ops.Act(y16, sc, sh), 2 * H, 2 * W, bf16=True)
+        eq(u16, u32.to(torch.bfloat16), "bilinear fwd bf16 output")
+        eq(ops.bilinear_nhwc_fwd(ops.Act(y16, sc, sh), 2 * H, 2 * W), u32, "bilinear fwd")
+        du = nhwc(rnd((B, C, 2 * H, 2 * W), 96, "du")).to(dev)
+        bp = []
+        for t in (y, y16):
+            din = torch.empty(B, H, W, C, device=dev)
+            bp.append((din, ops.bilinear_nhwc_bwd(du, H, W, din, 0, bnb=(t, *st))))
+        eq(bp[0][0], bp[1][0], "bilinear bwd")
+        eq(bp[0][1], bp[1][1], "bilinear bwd partials")
+        # heads
+        wh, bh = rnd((1, C), 97, "wh").to(dev), rnd((1,), 98, "bh").to(dev)
+        eq(ops.head_fwd(ops.Act(y, sc, sh), wh, bh), ops.head_fwd(ops.Act(y16, sc, sh), wh, bh),
+           "head fwd")
+        dh = nhwc(rnd((B, 1, H, W), 99, "dh")).to(dev)
+        hb = []
+        for t in (y, y16):
+            dw, db = torch.empty(1, C, device=dev), torch.empty(1, device=dev)
+            da = torch.empty(B, H, W, C, device=dev)
+            part = ops.head_bwd(ops.Act(t, sc, sh), wh, dh, dw, db, da, 0, bnb=(mean, invstd))
+            hb.append((dw, db, da, part))
+        for a_, b_ in zip(*hb):
+            eq(a_, b_, "head bwd")
+        # data gradient with the BN1 partials fused in its epilogue, y1 stored in bf16
+        wd = rnd((C, C, 3, 3), 100, "wd", 0.05).to(dev)
+        wpk = ops.pack_conv3x3(wd, C, 1)
+        nt = ops.conv_ntiles(B, H, W, C, C, wpk)
+        dg_ = []
+        for t in (y, y16):
+            part = torch.empty(3 * C * nt, device=dev)
+            da = torch.empty(B, H, W, C, device=dev)
+            ops.conv3x3_fwd([ops.Act(du[:, :H, :W].contiguous())], wpk, None, C, [da],
+                            bnb=(t, *st, part))
+            dg_.append((da, part))
+        eq(dg_[0][0], dg_[1][0], "dgrad")
+        eq(dg_[0][1], dg_[1][1], "dgrad fused partials")
+        if math == "bf16":  # the weight gradient of bf16-stored sources (one and two)
+            dyw = nhwc(rnd((B, 128, H, W), 101, "dyw")).to(dev)
+            for two in (False, True):
+                ws_ = []
+                for t in (y, y16):
+                    srcs = [ops.Act(t, sc, sh)] + ([ops.Act(t)] if two else [])
+                    dw = torch.empty(128, C * (2 if two else 1), 3, 3, device=dev)
+                    ops.conv3x3_wgrad(srcs, dyw, dw, None, C * (2 if two else 1))
+                    ws_.append(dw)
+                eq(ws_[0], ws_[1], f"bf16 wgrad of bf16-stored sources (two={two})")
+        # avgpool (Herlev)
+        eq(ops.avgpool_fwd(ops.Act(y, sc, sh)), ops.avgpool_fwd(ops.Act(y16, sc, sh)), "avgpool")
     finally:
         ops.set_conv_math(old)
 

@@ -9,6 +9,8 @@
 // relu(scale*y + shift) while loading (ugpg_src_t).
 #include <numeric>
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace ugpg {
@@ -106,7 +108,7 @@ __global__ void bn_eval_params_kernel(const float* gamma, const float* beta, con
 // Per-block partial sums of g and g*xhat over a contiguous pixel range.
 // Thread layout: C/4 threads per pixel (float4 channels), 256/(C/4) pixel slots.
 __global__ void __launch_bounds__(256)
-    bn_bwd_reduce_kernel(const float* __restrict__ da, const float* __restrict__ y, int64_t npix,
+    bn_bwd_reduce_kernel(const float* __restrict__ da, YRef y, int64_t npix,
                          int C, const float* mean, const float* invstd, const float* scale,
                          const float* shift, int64_t ppb, float* part, int nblk) {
     const int c4n = C / 4, slots = 256 / c4n;
@@ -138,14 +140,13 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 d[u] = *reinterpret_cast<const f32x4*>(da + (p + u * slots) * C + c);
-                v[u] = *reinterpret_cast<const f32x4*>(y + (p + u * slots) * C + c);
+                v[u] = y.ld4((p + u * slots) * C + c);
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) accum(d[u], v[u]);
         }
         for (; p < p1; p += slots)
-            accum(*reinterpret_cast<const f32x4*>(da + p * C + c),
-                  *reinterpret_cast<const f32x4*>(y + p * C + c));
+            accum(*reinterpret_cast<const f32x4*>(da + p * C + c), y.ld4(p * C + c));
     }
     rs[tid] = sg;
     rq[tid] = sgx;
@@ -230,8 +231,9 @@ __global__ void bn_bwd_finalize_kernel(const float* part, int nblk, int C, int64
 // The grid stride is a multiple of C/4 (2048 x 256 threads, C <= 1024), so each thread
 // keeps one 4-channel group: its per-channel coefficients are loaded once, and four
 // float4 pairs are in flight per thread.
-template <bool NT>
-__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const float* da, const float* __restrict__ y,
+// TY: the storage of y (float, or __bf16 under the bf16 arithmetic)
+template <bool NT, typename TY>
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const float* da, const TY* __restrict__ y,
                                                            int64_t npix, int C, const float* mean,
                                                            const float* invstd, const float* scale,
                                                            const float* shift, const float* coef,
@@ -255,34 +257,41 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const float* da, cons
         return o;
     };
     const f32x4* D = reinterpret_cast<const f32x4*>(da);
-    const f32x4* Y = reinterpret_cast<const f32x4*>(y);
     f32x4* O = reinterpret_cast<f32x4*>(dy);
+    auto Y = [&](int64_t k) {  // 4 values of y (a 16- or 8-byte vector)
+        if constexpr (std::is_same<TY, float>::value) {
+            const f32x4* q = reinterpret_cast<const f32x4*>(y) + k;
+            return NT ? __builtin_nontemporal_load(q) : *q;
+        } else {
+            const uint2* q = reinterpret_cast<const uint2*>(y) + k;
+            const uint2 u = NT ? uint2{__builtin_nontemporal_load(&q->x),
+                                       __builtin_nontemporal_load(&q->y)}
+                               : *q;
+            return f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                         __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
+        }
+    };
     int64_t i = i0;
     for (; i + 3 * stride < n4; i += 4 * stride) {
         f32x4 d[4], v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            if constexpr (NT) {  // da and y are read once: streaming loads
-                d[u] = __builtin_nontemporal_load(D + i + u * stride);
-                v[u] = __builtin_nontemporal_load(Y + i + u * stride);
-            } else {
-                d[u] = D[i + u * stride];
-                v[u] = Y[i + u * stride];
-            }
+            // da and y are read once: streaming loads (NT)
+            d[u] = NT ? __builtin_nontemporal_load(D + i + u * stride) : D[i + u * stride];
+            v[u] = Y(i + u * stride);
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) O[i + u * stride] = one(d[u], v[u]);
     }
-    for (; i < n4; i += stride) O[i] = one(D[i], Y[i]);
+    for (; i < n4; i += stride) O[i] = one(D[i], Y(i));
 }
 
-__global__ void bn_relu_apply_kernel(const float* x, const float* sc, const float* sh,
+__global__ void bn_relu_apply_kernel(YRef x, const float* sc, const float* sh,
                                      int64_t n4, int C, float* out) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
          i += (int64_t)gridDim.x * blockDim.x) {
         const int c = (int)((i * 4) % C);
-        reinterpret_cast<f32x4*>(out)[i] =
-            act_apply4(reinterpret_cast<const f32x4*>(x)[i], sc, sh, c);
+        reinterpret_cast<f32x4*>(out)[i] = act_apply4(x.ld4((size_t)i * 4), sc, sh, c);
     }
 }
 
@@ -299,11 +308,15 @@ static unsigned apply_grid(int64_t n4) {
 }
 // the apply reads da and y with streaming (nontemporal) loads -- their last use -- so dy,
 // read next by the data and weight gradients, stays in the caches (step -0.55 %)
-void launch_bn_apply(unsigned ga, hipStream_t st, const float* da, const float* y, int64_t npix,
+void launch_bn_apply(unsigned ga, hipStream_t st, const float* da, YRef y, int64_t npix,
                      int C, const float* mean, const float* invstd, const float* scale,
                      const float* shift, const float* coef, float* dy) {
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(ga), dim3(256), 0, st, da, y, npix, C,
-                       mean, invstd, scale, shift, coef, dy);
+    if (y.f)
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<true, float>), dim3(ga), dim3(256), 0, st, da, y.f,
+                           npix, C, mean, invstd, scale, shift, coef, dy);
+    else
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<true, __bf16>), dim3(ga), dim3(256), 0, st, da,
+                           y.h, npix, C, mean, invstd, scale, shift, coef, dy);
 }
 constexpr int64_t kBwdBlocks = 2048, kBwdPpt = 8;
 namespace {
@@ -366,11 +379,13 @@ extern "C" size_t ugpg_bn_relu_bwd_workspace(int64_t npix, int C) {
     return ((size_t)3 * C * p.nblk + (size_t)2 * C) * sizeof(float);
 }
 
-extern "C" int ugpg_bn_relu_bwd(const float* da, const float* y, int64_t npix, int C,
-                                const float* mean, const float* invstd, const float* scale,
-                                const float* shift, float* dy, float* dgamma, float* dbeta,
-                                float* dbias, int acc, void* ws, size_t ws_bytes, void* stream) {
-    if (!da || !y || !dy || !mean || !invstd || !scale || !shift || C % 4 || C > 1024 ||
+extern "C" int ugpg_bn_relu_bwd(const float* da, const float* y_f32, const void* y_bf16,
+                                int64_t npix, int C, const float* mean, const float* invstd,
+                                const float* scale, const float* shift, float* dy, float* dgamma,
+                                float* dbeta, float* dbias, int acc, void* ws, size_t ws_bytes,
+                                void* stream) {
+    const YRef y = yref(y_f32, y_bf16);
+    if (!da || (!y.f && !y.h) || !dy || !mean || !invstd || !scale || !shift || C % 4 || C > 1024 ||
         npix <= 0) {
         set_error("bn_relu_bwd: bad arguments (C=%d)", C);
         return UGPG_ERR_INVALID;
@@ -398,7 +413,7 @@ extern "C" int ugpg_bn_relu_bwd(const float* da, const float* y, int64_t npix, i
 }
 
 namespace ugpg {
-void launch_bn_bwd_reduce(const float* da, const float* y, int64_t npix, int C, const float* mean,
+void launch_bn_bwd_reduce(const float* da, YRef y, int64_t npix, int C, const float* mean,
                           const float* invstd, const float* scale, const float* shift, float* part,
                           int nslots, hipStream_t st) {
     const int64_t ppb = cdiv(npix, (int64_t)nslots);
@@ -419,12 +434,13 @@ extern "C" size_t ugpg_bn_relu_bwd_partials_workspace(int C) {
 
 // finalize + apply of ugpg_bn_relu_bwd from partials a data gradient wrote (bnb_part)
 extern "C" int ugpg_bn_relu_bwd_partials(const float* part, int nslots, const float* da,
-                                         const float* y, int64_t npix, int C, const float* mean,
-                                         const float* invstd, const float* scale,
-                                         const float* shift, float* dy, float* dgamma,
-                                         float* dbeta, float* dbias, int acc, void* ws,
-                                         size_t ws_bytes, void* stream) {
-    if (!part || nslots <= 0 || !da || !y || !dy || !mean || !invstd || !scale || !shift ||
+                                         const float* y_f32, const void* y_bf16, int64_t npix,
+                                         int C, const float* mean, const float* invstd,
+                                         const float* scale, const float* shift, float* dy,
+                                         float* dgamma, float* dbeta, float* dbias, int acc,
+                                         void* ws, size_t ws_bytes, void* stream) {
+    const YRef y = yref(y_f32, y_bf16);
+    if (!part || nslots <= 0 || !da || (!y.f && !y.h) || !dy || !mean || !invstd || !scale || !shift ||
         C % 4 || C <= 0 || C > 1024 || npix <= 0) {
         set_error("bn_relu_bwd_partials: bad arguments (C=%d nslots=%d)", C, nslots);
         return UGPG_ERR_INVALID;
@@ -446,12 +462,12 @@ extern "C" int ugpg_bn_relu_bwd_partials(const float* part, int nslots, const fl
 }
 
 extern "C" int ugpg_bn_relu_apply(ugpg_src_t src, int64_t npix, float* out, void* stream) {
-    if (!src.data || !out || src.C % 4) {
+    if ((!src.data && !src.data_bf16) || !out || src.C % 4) {
         set_error("bn_relu_apply: bad arguments");
         return UGPG_ERR_INVALID;
     }
     const int64_t n4 = npix * src.C / 4;
     hipLaunchKernelGGL(bn_relu_apply_kernel, dim3(stream_grid(n4)), dim3(256), 0,
-                       as_stream(stream), src.data, src.scale, src.shift, n4, src.C, out);
+                       as_stream(stream), yref(src), src.scale, src.shift, n4, src.C, out);
     return check_launch("bn_relu_apply");
 }

@@ -37,6 +37,30 @@ inline unsigned stream_grid(int64_t work, int block = 256) {
     return (unsigned)g;
 }
 
+// 4 consecutive bf16 (8 bytes) widened to fp32 (exact)
+__device__ __forceinline__ f32x4 ld4_bf16(const __bf16* p) {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    return f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                 __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
+}
+// An NHWC activation stored in fp32 or (the bf16 arithmetic's storage, ugpg_src_t
+// data_bf16) in bf16: exactly one of f / h is set.  The choice is uniform per kernel, so
+// the branch in ld4 costs a scalar test.
+struct YRef {
+    const float* f;
+    const __bf16* h;
+    __device__ __forceinline__ f32x4 ld4(size_t off) const {
+        return f ? *reinterpret_cast<const f32x4*>(f + off) : ld4_bf16(h + off);
+    }
+    __device__ __forceinline__ float ld1(size_t off) const {
+        return f ? f[off] : (float)h[off];
+    }
+};
+inline YRef yref(const void* f32, const void* bf16) {
+    return YRef{static_cast<const float*>(f32), f32 ? nullptr : static_cast<const __bf16*>(bf16)};
+}
+inline YRef yref(const ugpg_src_t& s) { return yref(s.data, s.data_bf16); }
+
 __device__ __forceinline__ float act_apply(float v, const float* sc, const float* sh, int c) {
     return sc ? fmaxf(fmaf(v, sc[c], sh[c]), 0.0f) : v;
 }
@@ -119,7 +143,7 @@ __device__ __forceinline__ void ac_index(int o, int in, int out, int& i0, int& i
 // bn_bwd_reduce_kernel, finalized by ugpg_bn_relu_bwd_partials).  Thread layout of that
 // kernel: C/4 threads per pixel (4 channels each), 256/(C/4) pixel slots per block.
 struct BnbArgs {
-    const float* y;
+    YRef y;
     const float* mean;
     const float* invstd;
     const float* scale;

@@ -792,11 +792,13 @@ extern "C" int ugpg_conv3x3_fwd_ntiles(int B, int H, int W, int Cin, int Cout, i
 }
 
 extern "C" int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream) {
-    if (!p || !p->src[0].data || !p->wpk || !p->out[0]) {
+    if (!p || (!p->src[0].data && !p->src[0].data_bf16) || !p->wpk ||
+        (!p->out[0] && !p->out_bf16)) {
         set_error("conv3x3_fwd: null argument");
         return UGPG_ERR_INVALID;
     }
-    const int C0 = p->src[0].C, C1 = p->src[1].data ? p->src[1].C : 0;
+    const bool has1 = p->src[1].data || p->src[1].data_bf16;
+    const int C0 = p->src[0].C, C1 = has1 ? p->src[1].C : 0;
     const int Cin = C0 + C1;
     if (Cin % 8 || C0 % 8 || p->Cout % 64 || p->B <= 0 || p->H <= 0 || p->W <= 0) {
         set_error("conv3x3_fwd: unsupported shape Cin=%d (C0=%d) Cout=%d", Cin, C0, p->Cout);
@@ -819,8 +821,21 @@ extern "C" int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream) {
         set_error("conv3x3_fwd: split-bf16 path needs 16-channel sources (C0=%d C1=%d)", C0, C1);
         return UGPG_ERR_INVALID;
     }
+    // bf16 activation storage (data / out[0] NULL): the single-piece persistent form reads
+    // and writes it (images >= 32 wide); the image-layer kernel writes it
+    const bool b16_in = !p->src[0].data || (has1 && !p->src[1].data);
+    const bool b16_out = !p->out[0];
+    const bool x6r_np1 = p->wfmt == UGPG_WFMT_BF16 && p->W >= 32;
+    const bool img = p->wfmt == UGPG_WFMT_F32 && img_fwd_eligible(p->W, C0, C1, p->Cout);
+    if ((b16_in && !x6r_np1) || (b16_out && !(x6r_np1 || img)) ||
+        (b16_out && (p->out_split != p->Cout || p->accumulate[0]))) {
+        set_error("conv3x3_fwd: bf16-only activations (src data / out[0] NULL) need the bf16 "
+                  "weight format and an image >= 32 wide (or, for the output, the fp32 image "
+                  "layer), one output and no accumulate");
+        return UGPG_ERR_INVALID;
+    }
     const bool bnb = p->bnb_part != nullptr;
-    if (bnb && (!p->bnb_y || !p->bnb_mean || !p->bnb_invstd || !p->bnb_scale || !p->bnb_shift ||
+    if (bnb && ((!p->bnb_y && !p->bnb_y_bf16) || !p->bnb_mean || !p->bnb_invstd || !p->bnb_scale || !p->bnb_shift ||
                 p->out_split != p->Cout || p->accumulate[0] || p->Cout > 1024)) {
         set_error("conv3x3_fwd: BatchNorm-backward partials need bnb_y/mean/invstd/scale/shift, "
                   "one output and no accumulate");
@@ -846,14 +861,14 @@ extern "C" int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream) {
         }
     }
     ConvFwdArgs a;
-    a.bnb_y = p->bnb_y;
+    a.bnb_y = yref(p->bnb_y, p->bnb_y_bf16);
     a.bnb_mean = p->bnb_mean;
     a.bnb_invstd = p->bnb_invstd;
     a.bnb_scale = p->bnb_scale;
     a.bnb_shift = p->bnb_shift;
     a.bnb_part = p->bnb_part;
     a.src0_16 = static_cast<const __bf16*>(p->src[0].data_bf16);
-    a.src1_16 = p->src[1].data ? static_cast<const __bf16*>(p->src[1].data_bf16) : nullptr;
+    a.src1_16 = has1 ? static_cast<const __bf16*>(p->src[1].data_bf16) : nullptr;
     a.out0_16 = static_cast<__bf16*>(p->out_bf16);
     if (p->out_bf16 && (p->out_split != p->Cout || p->accumulate[0])) {
         set_error("conv3x3_fwd: out_bf16 needs one output without accumulate");
@@ -867,7 +882,7 @@ extern "C" int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream) {
     // forms that do not fuse the partials: the same reduction as a pass after the conv
     auto bnb_pass = [&]() {
         const int nslots = ugpg_conv3x3_fwd_ntiles(p->B, p->H, p->W, Cin, p->Cout, p->wfmt);
-        launch_bn_bwd_reduce(p->out[0], p->bnb_y, (int64_t)p->B * p->H * p->W, p->Cout,
+        launch_bn_bwd_reduce(p->out[0], a.bnb_y, (int64_t)p->B * p->H * p->W, p->Cout,
                              p->bnb_mean, p->bnb_invstd, p->bnb_scale, p->bnb_shift, p->bnb_part,
                              nslots, as_stream(stream));
     };
@@ -913,7 +928,7 @@ extern "C" int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream) {
         a.tiles_y = (int)cdiv(p->H, 8);
         a.ntiles = p->B * a.tiles_x * a.tiles_y;
         if (launch_img_fwd(a, true, st)) return check_launch("conv3x3_img_fwd");  // + out16
-        if (p->stats) {  // ugpg_conv3x3_fwd_ntiles counted the image kernel's slots
+        if (p->stats || b16_out) {  // ugpg_conv3x3_fwd_ntiles counted the image kernel's slots
             set_error("conv3x3_fwd: BatchNorm partials of an 8-channel source need one "
                       "output without accumulate");
             return UGPG_ERR_INVALID;
@@ -1001,12 +1016,27 @@ extern "C" int ugpg_pack_conv3x3_batch(const ugpg_pack_item_t* items, int n, int
     return check_launch("pack_conv3x3_batch");
 }
 
+static int wgrad_c1(const ugpg_wgrad_t* p) {
+    return p->src[1].data || p->src[1].data_bf16 ? p->src[1].C : 0;
+}
+// bf16 activation storage of the sources (data NULL): all sources alike
+static bool wgrad_b16(const ugpg_wgrad_t* p) { return !p->src[0].data; }
+
 static int wgrad_check(const ugpg_wgrad_t* p) {
-    if (!p || !p->src[0].data || !p->dy || !p->dw) {
+    if (!p || (!p->src[0].data && !p->src[0].data_bf16) || !p->dy || !p->dw) {
         set_error("conv3x3_wgrad: null argument");
         return UGPG_ERR_INVALID;
     }
-    const int C0 = p->src[0].C, C1 = p->src[1].data ? p->src[1].C : 0;
+    const int C0 = p->src[0].C, C1 = wgrad_c1(p);
+    if (wgrad_b16(p) != (C1 && !p->src[1].data) && C1) {
+        set_error("conv3x3_wgrad: both sources must be stored alike (fp32 or bf16)");
+        return UGPG_ERR_INVALID;
+    }
+    if (wgrad_b16(p) && (p->math != UGPG_WFMT_BF16 || p->db || C0 % 64 || C1 % 64)) {
+        set_error("conv3x3_wgrad: bf16-stored sources need the bf16 arithmetic, 64-channel "
+                  "sources and no bias gradient");
+        return UGPG_ERR_INVALID;
+    }
     if (p->Cout % 64 || C0 % 4 || (C1 && (C0 % 64 || C1 % 64)) || p->Cin_real > C0 + C1) {
         set_error("conv3x3_wgrad: unsupported shape C0=%d C1=%d Cout=%d", C0, C1, p->Cout);
         return UGPG_ERR_INVALID;
@@ -1050,7 +1080,7 @@ static WgradPlan wgrad_plan_for(const ugpg_wgrad_t* p, WgradKind k, int Cin) {
 
 extern "C" size_t ugpg_conv3x3_wgrad_workspace(const ugpg_wgrad_t* p) {
     if (wgrad_check(p)) return 0;
-    const int C0 = p->src[0].C, C1 = p->src[1].data ? p->src[1].C : 0;
+    const int C0 = p->src[0].C, C1 = wgrad_c1(p);
     const int Cin = C0 + C1;
     WgradPlan w = wgrad_plan_for(p, wgrad_kind(p, C0, C1), Cin);
     return ((size_t)w.nsplit * 9 * p->Cout * Cin + (size_t)w.nsplit * p->Cout) * sizeof(float);
@@ -1059,7 +1089,7 @@ extern "C" size_t ugpg_conv3x3_wgrad_workspace(const ugpg_wgrad_t* p) {
 extern "C" int ugpg_conv3x3_wgrad(const ugpg_wgrad_t* p, void* ws, size_t ws_bytes,
                                   void* stream) {
     if (int e = wgrad_check(p)) return e;
-    const int C0 = p->src[0].C, C1 = p->src[1].data ? p->src[1].C : 0;
+    const int C0 = p->src[0].C, C1 = wgrad_c1(p);
     const int Cin = C0 + C1;
     const WgradKind kind = wgrad_kind(p, C0, C1);
     WgradPlan w = wgrad_plan_for(p, kind, Cin);
@@ -1077,6 +1107,8 @@ extern "C" int ugpg_conv3x3_wgrad(const ugpg_wgrad_t* p, void* ws, size_t ws_byt
     a.sc1 = p->src[1].scale;
     a.sh1 = p->src[1].shift;
     a.C1 = C1;
+    a.src0_16 = static_cast<const __bf16*>(p->src[0].data_bf16);
+    a.src1_16 = static_cast<const __bf16*>(p->src[1].data_bf16);
     a.dy = p->dy;
     a.Cout = p->Cout;
     a.Cin = Cin;

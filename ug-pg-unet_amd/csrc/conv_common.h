@@ -25,14 +25,15 @@ struct ConvFwdArgs {
     int B, H, W, Cin, Cout;
     int tiles_x, tiles_y, ntiles;
     // BatchNorm-backward partials of out0 (ugpg_conv_t.bnb_*; bnb_part == nullptr: off)
-    const float* bnb_y;
+    YRef bnb_y;
     const float* bnb_mean;
     const float* bnb_invstd;
     const float* bnb_scale;
     const float* bnb_shift;
     float* bnb_part;
-    // bf16 copies (ugpg_src_t.data_bf16, ugpg_conv_t.out_bf16): read by / written beside
-    // the single-piece persistent form; nullptr: none
+    // bf16 activations (ugpg_src_t.data_bf16, ugpg_conv_t.out_bf16): read by / written by
+    // the single-piece persistent form; nullptr: none.  out0 == nullptr with out0_16 set:
+    // the output is stored in bf16 only (stats and partials of the rounded values)
     const __bf16* src0_16;
     const __bf16* src1_16;
     __bf16* out0_16;
@@ -163,6 +164,9 @@ struct WgradArgs {
     const float* sh1;
     int C1;
     const float* dy;
+    // bf16 activation storage (src0/src1 == nullptr; the x6w single-piece form only)
+    const __bf16* src0_16;
+    const __bf16* src1_16;
     int Cout, Cin;
     float* part;
     float* dbpart;
@@ -181,7 +185,7 @@ bool img_fwd_eligible(int W, int C0, int C1, int Cout);
 int img_fwd_slots(int B, int H, int W, int nwm);
 bool launch_img_fwd(const ConvFwdArgs& a, bool wf32, hipStream_t st);  // writes out0_16 too
 // bn.hip: the per-slot BatchNorm-backward reduction (partials layout of ugpg_conv_t.bnb_part)
-void launch_bn_bwd_reduce(const float* da, const float* y, int64_t npix, int C, const float* mean,
+void launch_bn_bwd_reduce(const float* da, YRef y, int64_t npix, int C, const float* mean,
                           const float* invstd, const float* scale, const float* shift, float* part,
                           int nslots, hipStream_t st);
 // batched weight packing (ugpg_pack_conv3x3_batch), kernel-argument descriptors

@@ -27,6 +27,7 @@
 // a 16-lane read group touches 16 distinct 16-B bank slots (32-wide tile: one
 // image row; 16-wide tile: permuted rows, see tile_pixel<16, true>, with HS=24).
 #include <algorithm>
+#include <atomic>
 #include <type_traits>
 
 #include "conv_common.h"
@@ -73,22 +74,23 @@ __device__ __forceinline__ void split3(f32x8 v, u32x4& p0, u32x4& p1, u32x4& p2)
     }
 }
 
-// compute units of the stream's device (cached per device)
+// compute units of the stream's device (cached per device; relaxed atomics: entries are
+// written once with the same value, from any host thread)
 static int cu_count(hipStream_t st) {
-    static int cache[64] = {0};
+    static std::atomic<int> cache[64];
     int dev = 0;
     if (hipStreamGetDevice(st, &dev) != hipSuccess || dev < 0 || dev >= 64) {
         (void)hipGetLastError();
         if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
     }
-    if (!cache[dev]) {
-        int n = 0;
+    int n = cache[dev].load(std::memory_order_relaxed);
+    if (!n) {
         if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
             n <= 0)
             n = 256;
-        cache[dev] = n;
+        cache[dev].store(n, std::memory_order_relaxed);
     }
-    return cache[dev];
+    return n;
 }
 
 // identity lazy-activation coefficients (for sources stored already activated)
@@ -335,6 +337,13 @@ __device__ __forceinline__ f32x4 gld16(const void* p) {
     asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p));
     return r;
 }
+typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
+// the same for 8 bytes (4 bf16)
+__device__ __forceinline__ u32x2v gld8(const void* p) {
+    u32x2v r;
+    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(r) : "v"(p));
+    return r;
+}
 // LDS-DMA: 16 bytes per lane from g (per-lane address) to lds_wave + 16*lane (lds_wave
 // wave-uniform), counted by vmcnt like a load; no VGPR destination
 __device__ __forceinline__ void glds16(const void* g, void* lds_wave) {
@@ -396,6 +405,9 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
     const int nl = wn * 32 + (lane & 31);
     const float bv = a.bias ? a.bias[n0 + nl] : 0.f;
     const int lane_off = 4 * h * ostride + ocol0 + nl;
+    // bf16 storage only (out0 == nullptr, one output): the stored -- rounded -- values are
+    // the ones the BatchNorm statistics describe
+    const bool only16 = out == nullptr;
     float psum = 0.f;
     // the stores of m-tiles [m0, m1)
     auto store_rows = [&](auto accumulate, int m0, int m1) {
@@ -405,18 +417,22 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
             if (mt < m0 || mt >= m1) continue;
             const int py = wm * MT + mt;
             if (py >= vh) break;  // uniform
-            float* rowp = out + (size_t)((b * a.H + ty0 + py) * a.W + tx0) * ostride + lane_off;
+            const size_t rowe = (size_t)((b * a.H + ty0 + py) * a.W + tx0) * ostride + lane_off;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int pxc = (r & 3) + 8 * (r >> 2);  // + 4h in lane_off
-                const float v = acc[mt][r] + bv;
+                float v = acc[mt][r] + bv;
+                if (!ACC && only16) v = (float)(__bf16)v;
                 acc[mt][r] = v;
                 if (fullw || pxc + 4 * h < vw) {
-                    float* p = rowp + pxc * ostride;
-                    if constexpr (ACC) *p += v;
-                    else *p = v;
-                    if (!ACC && a.out0_16)  // bf16 copy (one output: ostride == Cout)
-                        a.out0_16[p - a.out0] = (__bf16)v;
+                    const size_t e = rowe + (size_t)pxc * ostride;
+                    if constexpr (ACC) {
+                        out[e] += v;
+                    } else {
+                        if (!only16) out[e] = v;
+                        if (a.out0_16)  // bf16 storage or copy (one output: ostride == Cout)
+                            a.out0_16[e] = (__bf16)v;
+                    }
                     psum += v;
                 }
             }
@@ -436,13 +452,12 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
         for (int mt = 0; mt < MT; ++mt) {
             const int py = wm * MT + mt;
             if (py >= vh) break;  // uniform
-            const float* yrow =
-                a.bnb_y + (size_t)((b * a.H + ty0 + py) * a.W + tx0 + 4 * h) * a.Cout + n;
+            const size_t yrow = (size_t)((b * a.H + ty0 + py) * a.W + tx0 + 4 * h) * a.Cout + n;
             float yv[16];
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int pxc = min((r & 3) + 8 * (r >> 2), vw - 1 - 4 * h);
-                yv[r] = yrow[(size_t)max(pxc, -4 * h) * a.Cout];
+                yv[r] = a.bnb_y.ld1(yrow + (size_t)max(pxc, -4 * h) * a.Cout);
             }
             // this row's output stores issue while its y loads are in flight
             store_rows(std::integral_constant<bool, false>{}, mt, mt + 1);
@@ -603,10 +618,9 @@ __device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a,
             for (int u = 0; u < YB; ++u) {
                 const int mt = m0 + u;
                 const int py = min(wm * WR + prow(mt), vh - 1), px = min(pcol(mt) + l16, vw - 1);
-                const float* yp =
-                    a.bnb_y + (size_t)((b * a.H + ty0 + py) * a.W + tx0 + px) * a.Cout + n0 + c0;
+                const size_t yp = (size_t)((b * a.H + ty0 + py) * a.W + tx0 + px) * a.Cout + n0 + c0;
 #pragma unroll
-                for (int nt = 0; nt < 2; ++nt) yv[u][nt] = *reinterpret_cast<const f32x4*>(yp + 16 * nt);
+                for (int nt = 0; nt < 2; ++nt) yv[u][nt] = a.bnb_y.ld4(yp + 16 * nt);
             }
             store_tiles(std::integral_constant<bool, false>{}, m0, m0 + YB);
 #pragma unroll
@@ -1393,8 +1407,11 @@ template <int NP>
 constexpr int wrec() { return NP == 3 ? WX_REC : 192; }
 
 // (A paired 16x16x32 form, as the forward's, measured 2 % slower: 32x32x16 it is.)
-template <int TH, int TW, int NP>
+// XB16: the activation operand is stored in bf16 (a.src*_16; the bf16 arithmetic's storage,
+// NP = 1): 8-byte loads of 4 channels instead of 16-byte ones, same load count per step
+template <int TH, int TW, int NP, bool XB16 = false>
 __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) {
+    static_assert(!XB16 || NP == 1, "bf16 activation storage: single-piece arithmetic");
     constexpr int REC = wrec<NP>();
     static_assert(TW == 16, "one 16-pixel row per MFMA k-step");
     constexpr int P = TH * TW, HWD = TW + 2, NHALO = (TH + 2) * HWD;
@@ -1446,7 +1463,8 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
     if (loader) {
         // ------------------------------------------------------------ loader waves
         const int lt = tid - 256;
-        f32x4 rdy[DY_PER], rx[X_PER];
+        f32x4 rdy[DY_PER];
+        typename std::conditional<XB16, u32x2v, f32x4>::type rx[X_PER];
         Act4 xa;
         float xlo = 0.f;
         unsigned dvalid = 0, xvalid = 0;
@@ -1485,6 +1503,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
             const int co0 = c.nb * 64, ci0 = c.cb * 64;
             const bool second = ci0 >= a.C0;
             const float* xsrc = second ? a.src1 : a.src0;
+            const __bf16* xsrc16 = second ? a.src1_16 : a.src0_16;
             const float* xsc = second ? a.sc1 : a.sc0;
             const float* xsh = second ? a.sh1 : a.sh0;
             const int Cs = second ? a.C1 : a.C0, cbase = second ? ci0 - a.C0 : ci0;
@@ -1549,11 +1568,14 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
                 }
             }
             const float* dyb = a.dy + ((size_t)(b * a.H + ty0) * a.W + tx0) * a.Cout + co0 + q4;
-            const float* xb = xsrc + ((size_t)(b * a.H + ty0) * a.W + tx0) * Cs + cbase + q4;
+            const size_t xb = ((size_t)(b * a.H + ty0) * a.W + tx0) * Cs + cbase + q4;
 #pragma unroll
             for (int v = 0; v < DY_PER; ++v) rdy[v] = gld16(dyb + dof[v]);
 #pragma unroll
-            for (int v = 0; v < X_PER; ++v) rx[v] = gld16(xb + xof[v]);
+            for (int v = 0; v < X_PER; ++v) {
+                if constexpr (XB16) rx[v] = gld8(xsrc16 + xb + xof[v]);
+                else rx[v] = gld16(xsrc + xb + xof[v]);
+            }
         };
         // record layout: [piece][64 ch] bf16 at byte piece*128 + ch*2
         auto put = [&](char* rec, int q, f32x4 v) {
@@ -1576,7 +1598,13 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
             for (int v = 0; v < X_PER; ++v) {
                 const int idx = lt + v * 256;
                 const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-                const f32x4 val = ((xvalid >> v) & 1u) ? act_floor4(rx[v], xa, xlo) : z;
+                f32x4 raw;
+                if constexpr (XB16)  // 4 bf16 widened (exact)
+                    raw = f32x4{__uint_as_float(rx[v].x << 16), __uint_as_float(rx[v].x & 0xffff0000u),
+                                __uint_as_float(rx[v].y << 16), __uint_as_float(rx[v].y & 0xffff0000u)};
+                else
+                    raw = rx[v];
+                const f32x4 val = ((xvalid >> v) & 1u) ? act_floor4(raw, xa, xlo) : z;
                 put(idx < X_Q ? xs + (idx >> 4) * REC : dummy, idx & 15, val);
             }
         };
@@ -1735,6 +1763,9 @@ void launch_wgrad_x6(const WgradArgs& a, int np, hipStream_t st) {
     if (np == 3)
         hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW, 3>), dim3((unsigned)g),
                            dim3(512), 0, st, a);
+    else if (a.src0 == nullptr)  // bf16 activation storage (the host checked both sources)
+        hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW, 1, true>),
+                           dim3((unsigned)g), dim3(512), 0, st, a);
     else
         hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW, 1>), dim3((unsigned)g),
                            dim3(512), 0, st, a);
@@ -2042,8 +2073,9 @@ __global__ void __launch_bounds__(4096 / PX) conv3x3_img_fwd_kernel(ConvFwdArgs 
         if (a.bias)
 #pragma unroll
             for (int i = 0; i < 4; ++i) bv[i] = a.bias[n0 + 4 * cq + i];
-        float* orow =
-            a.out0 + ((size_t)(b * a.H + ty0 + row) * a.W + tx0 + c0) * a.Cout + n0 + 4 * cq;
+        const size_t orow = ((size_t)(b * a.H + ty0 + row) * a.W + tx0 + c0) * a.Cout + n0 + 4 * cq;
+        // out0 == nullptr: bf16 storage only, the statistics describe the rounded values
+        const bool only16 = a.out0 == nullptr;
         float sj[4] = {0.f, 0.f, 0.f, 0.f};
         float v[PX][4];
 #pragma unroll
@@ -2052,12 +2084,17 @@ __global__ void __launch_bounds__(4096 / PX) conv3x3_img_fwd_kernel(ConvFwdArgs 
             v[p][1] = acc[p][0].y + bv[1];
             v[p][2] = acc[p][1].x + bv[2];
             v[p][3] = acc[p][1].y + bv[3];
+            if (only16)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) v[p][i] = (float)(__bf16)v[p][i];
             if (rok && c0 + p < vw) {
 #ifndef IMG_NOSTORE
-                *reinterpret_cast<f32x4*>(orow + (size_t)p * a.Cout) = f32x4{v[p][0], v[p][1], v[p][2], v[p][3]};
+                if (!only16)
+                    *reinterpret_cast<f32x4*>(a.out0 + orow + (size_t)p * a.Cout) =
+                        f32x4{v[p][0], v[p][1], v[p][2], v[p][3]};
                 if (a.out0_16) {
                     typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
-                    *reinterpret_cast<bf4*>(a.out0_16 + (orow - a.out0) + (size_t)p * a.Cout) =
+                    *reinterpret_cast<bf4*>(a.out0_16 + orow + (size_t)p * a.Cout) =
                         bf4{(__bf16)v[p][0], (__bf16)v[p][1], (__bf16)v[p][2], (__bf16)v[p][3]};
                 }
 #endif

@@ -18,7 +18,7 @@ namespace ugpg {
 // (NT = nontemporal window loads: measured neutral, instantiated off)
 
 template <bool NT>
-__global__ void maxpool2_fwd_kernel(const float* x, const float* sc, const float* sh, int B, int H,
+__global__ void maxpool2_fwd_kernel(YRef x, const float* sc, const float* sh, int B, int H,
                                     int W, int C, float* out, uint8_t* am) {
     const int Ho = H / 2, Wo = W / 2, C4 = C / 4;
     const int64_t total = (int64_t)B * Ho * Wo * C4;
@@ -35,10 +35,11 @@ __global__ void maxpool2_fwd_kernel(const float* x, const float* sc, const float
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int y = 2 * oy + (k >> 1), xx = 2 * ox + (k & 1);
-            const f32x4* src = reinterpret_cast<const f32x4*>(x + ((size_t)(b * H + y) * W + xx) * C + c);
+            const size_t off = ((size_t)(b * H + y) * W + xx) * C + c;
             // NT: the window is read once here; the skip connection re-reads the block's
             // output only several layers later, long after it would have left the caches
-            xv[k] = NT ? __builtin_nontemporal_load(src) : *src;
+            xv[k] = NT && x.f ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(x.f + off))
+                              : x.ld4(off);
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -118,7 +119,7 @@ __global__ void __launch_bounds__(256)
             f32x4* dst = reinterpret_cast<f32x4*>(din + p * C + c);
             if (acc) g += *dst;
             *dst = g;
-            st.add(g, *reinterpret_cast<const f32x4*>(bnb.y + p * C + c));
+            st.add(g, bnb.y.ld4(p * C + c));
         }
     }
     st.write(bnb, C);
@@ -189,17 +190,27 @@ __device__ __forceinline__ void ac_range_tight(int i, int in, int out, int& lo, 
 // indices/weights and the 64-bit image offsets are computed once per thread, and a
 // thread keeps one channel quad (the x-stride is a multiple of C/4), loading the lazy
 // BatchNorm coefficients once.  Same arithmetic, same order as the flat forms.
-__global__ void bilinear_nhwc_fwd_kernel(const float* x, const float* sc, const float* sh, int B,
-                                         int Hi, int Wi, int C, float* out, int Ho, int Wo) {
+__global__ void bilinear_nhwc_fwd_kernel(YRef x, const float* sc, const float* sh, int B,
+                                         int Hi, int Wi, int C, float* out, __bf16* out16,
+                                         int Ho, int Wo) {
     const int C4 = C / 4;
     const int row = blockIdx.y;  // b * Ho + oy
     const int b = row / Ho, oy = row % Ho;
     int y0, y1, x0, x1;
     float ly0, ly1, lx0, lx1;
     ac_index(oy, Hi, Ho, y0, y1, ly0, ly1);
-    const float* r0 = x + ((size_t)b * Hi + y0) * Wi * C;
-    const float* r1 = x + ((size_t)b * Hi + y1) * Wi * C;
-    float* orow = out + (size_t)row * Wo * C;
+    const size_t r0 = ((size_t)b * Hi + y0) * Wi * C;  // element offsets of the two rows
+    const size_t r1 = ((size_t)b * Hi + y1) * Wi * C;
+    const size_t orow = (size_t)row * Wo * C;
+    // out16 (out == nullptr): bf16 storage of the result (the bf16 arithmetic's conv input)
+    auto store = [&](size_t e, f32x4 v) {
+        if (out16) {
+            typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+            *reinterpret_cast<bf4*>(out16 + e) = bf4{(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+        } else {
+            *reinterpret_cast<f32x4*>(out + e) = v;
+        }
+    };
     const int n = Wo * C4, stride = gridDim.x * blockDim.x;
     const bool fixed_c = stride % C4 == 0;  // then a thread keeps its channel quad
     int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -234,10 +245,10 @@ __global__ void bilinear_nhwc_fwd_kernel(const float* x, const float* sc, const 
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 ac_index(ox0 + u * step, Wi, Wo, x0, x1, wx0[u], wx1[u]);
-                a[u][0] = *reinterpret_cast<const f32x4*>(r0 + (size_t)x0 * C + c);
-                a[u][1] = *reinterpret_cast<const f32x4*>(r0 + (size_t)x1 * C + c);
-                a[u][2] = *reinterpret_cast<const f32x4*>(r1 + (size_t)x0 * C + c);
-                a[u][3] = *reinterpret_cast<const f32x4*>(r1 + (size_t)x1 * C + c);
+                a[u][0] = x.ld4(r0 + (size_t)x0 * C + c);
+                a[u][1] = x.ld4(r0 + (size_t)x1 * C + c);
+                a[u][2] = x.ld4(r1 + (size_t)x0 * C + c);
+                a[u][3] = x.ld4(r1 + (size_t)x1 * C + c);
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -245,7 +256,7 @@ __global__ void bilinear_nhwc_fwd_kernel(const float* x, const float* sc, const 
                             a11 = act(a[u][3]);
                 const f32x4 v = ly0 * (wx0[u] * a00 + wx1[u] * a01) +
                                 ly1 * (wx0[u] * a10 + wx1[u] * a11);
-                *reinterpret_cast<f32x4*>(orow + (size_t)(ox0 + u * step) * C + c) = v;
+                store(orow + (size_t)(ox0 + u * step) * C + c, v);
             }
         }
         return;
@@ -257,12 +268,12 @@ __global__ void bilinear_nhwc_fwd_kernel(const float* x, const float* sc, const 
         }
         const int ox = t / C4;
         ac_index(ox, Wi, Wo, x0, x1, lx0, lx1);
-        const f32x4 a00 = act(*reinterpret_cast<const f32x4*>(r0 + (size_t)x0 * C + c));
-        const f32x4 a01 = act(*reinterpret_cast<const f32x4*>(r0 + (size_t)x1 * C + c));
-        const f32x4 a10 = act(*reinterpret_cast<const f32x4*>(r1 + (size_t)x0 * C + c));
-        const f32x4 a11 = act(*reinterpret_cast<const f32x4*>(r1 + (size_t)x1 * C + c));
+        const f32x4 a00 = act(x.ld4(r0 + (size_t)x0 * C + c));
+        const f32x4 a01 = act(x.ld4(r0 + (size_t)x1 * C + c));
+        const f32x4 a10 = act(x.ld4(r1 + (size_t)x0 * C + c));
+        const f32x4 a11 = act(x.ld4(r1 + (size_t)x1 * C + c));
         const f32x4 v = ly0 * (lx0 * a00 + lx1 * a01) + ly1 * (lx0 * a10 + lx1 * a11);
-        *reinterpret_cast<f32x4*>(orow + (size_t)ox * C + c) = v;
+        store(orow + (size_t)ox * C + c, v);
     }
 }
 
@@ -383,7 +394,7 @@ __global__ void __launch_bounds__(256)
         f32x4* dst = reinterpret_cast<f32x4*>(din + o);
         if (acc) s += *dst;
         *dst = s;
-        st.add(s, *reinterpret_cast<const f32x4*>(bnb.y + o));
+        st.add(s, bnb.y.ld4(o));
     }
     st.write(bnb, C);
 }
@@ -492,7 +503,7 @@ __global__ void nhwc_to_nchw_kernel(const float* in, int B, int C, int HW, int C
 // 16 lanes per pixel; lane16 owns channels {4*l16 + 64*j}.
 constexpr int HEAD_NC_MAX = 4, HEAD_CJ_MAX = 4;
 
-__global__ void __launch_bounds__(256) head_fwd_kernel(const float* x, const float* sc,
+__global__ void __launch_bounds__(256) head_fwd_kernel(YRef x, const float* sc,
                                                        const float* sh, int64_t npix, int C,
                                                        const float* w, const float* bias, int nc,
                                                        float* h) {
@@ -502,7 +513,7 @@ __global__ void __launch_bounds__(256) head_fwd_kernel(const float* x, const flo
         float acc[HEAD_NC_MAX] = {0.f, 0.f, 0.f, 0.f};
         for (int j = 0; j < CJ; ++j) {
             const int c = l16 * 4 + 64 * j;
-            const f32x4 v = act_apply4(*reinterpret_cast<const f32x4*>(x + p * C + c), sc, sh, c);
+            const f32x4 v = act_apply4(x.ld4(p * C + c), sc, sh, c);
             for (int k = 0; k < nc; ++k) {
                 const f32x4 wv = *reinterpret_cast<const f32x4*>(w + (size_t)k * C + c);
                 acc[k] += v.x * wv.x + v.y * wv.y + v.z * wv.z + v.w * wv.w;
@@ -522,7 +533,7 @@ __global__ void __launch_bounds__(256) head_fwd_kernel(const float* x, const flo
 // pixels' loads go out before the first is used (the per-pixel form ran at 3.3 TB/s).
 // Arithmetic and reduction order are those of head_fwd_kernel (bit-identical).
 template <int CJ>
-__global__ void __launch_bounds__(256) head_fwd_cj_kernel(const float* x, const float* sc,
+__global__ void __launch_bounds__(256) head_fwd_cj_kernel(YRef x, const float* sc,
                                                           const float* sh, int64_t npix,
                                                           const float* w, const float* bias,
                                                           int nc, float* h) {
@@ -548,7 +559,7 @@ __global__ void __launch_bounds__(256) head_fwd_cj_kernel(const float* x, const 
             const int64_t p = min(p0 + u * G, npix - 1);
 #pragma unroll
             for (int j = 0; j < CJ; ++j)
-                v[u][j] = *reinterpret_cast<const f32x4*>(x + p * C + l16 * 4 + 64 * j);
+                v[u][j] = x.ld4(p * C + l16 * 4 + 64 * j);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -673,7 +684,7 @@ __global__ void __launch_bounds__(256) head_split_bwd_kernel(const float* dl, in
 // (sc, sh) its affine, already loaded here: the fusion costs no memory traffic); same
 // block plan, so nslots = the block count (ugpg_head_bwd_bnb_slots).
 template <int NC, int CJ, bool BNB>
-__global__ void __launch_bounds__(256) head_bwd_kernel(const float* x, const float* sc,
+__global__ void __launch_bounds__(256) head_bwd_kernel(YRef x, const float* sc,
                                                        const float* sh, int64_t npix, int C,
                                                        const float* w, int nc, const float* dh,
                                                        float* da, int acc_da, int64_t ppb,
@@ -729,8 +740,8 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(const float* x, const flo
         }
 #pragma unroll
         for (int j = 0; j < CJ; ++j) {
-            x0[j] = *reinterpret_cast<const f32x4*>(x + p * C + l16 * 4 + 64 * j);
-            x1[j] = *reinterpret_cast<const f32x4*>(x + (p + 16) * C + l16 * 4 + 64 * j);
+            x0[j] = x.ld4(p * C + l16 * 4 + 64 * j);
+            x1[j] = x.ld4((p + 16) * C + l16 * 4 + 64 * j);
         }
         pixel(p, d0, x0);
         pixel(p + 16, d1, x1);
@@ -742,7 +753,7 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(const float* x, const flo
         for (int k = 0; k < NC; ++k) d0[k] = dh[p * NC + k];
 #pragma unroll
         for (int j = 0; j < CJ; ++j)
-            x0[j] = *reinterpret_cast<const f32x4*>(x + p * C + l16 * 4 + 64 * j);
+            x0[j] = x.ld4(p * C + l16 * 4 + 64 * j);
         pixel(p, d0, x0);
     }
     __shared__ f32x4 red[256];
@@ -1207,7 +1218,7 @@ __global__ void rmsprop4_kernel(f32x4* p, const f32x4* g, f32x4* v, int64_t n4, 
 }
 
 // ------------------------------------------------------------- Herlev head
-__global__ void avgpool_fwd_kernel(const float* x, const float* sc, const float* sh, int B, int HW,
+__global__ void avgpool_fwd_kernel(YRef x, const float* sc, const float* sh, int B, int HW,
                                    int C, float* out) {
     const int64_t total = (int64_t)B * C / 4;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
@@ -1215,7 +1226,7 @@ __global__ void avgpool_fwd_kernel(const float* x, const float* sc, const float*
         const int c = (int)(i % (C / 4)) * 4, b = (int)(i / (C / 4));
         f32x4 s = {0.f, 0.f, 0.f, 0.f};
         for (int p = 0; p < HW; ++p)
-            s += act_apply4(*reinterpret_cast<const f32x4*>(x + ((size_t)b * HW + p) * C + c), sc, sh, c);
+            s += act_apply4(x.ld4(((size_t)b * HW + p) * C + c), sc, sh, c);
         *reinterpret_cast<f32x4*>(out + (size_t)b * C + c) = s / (float)HW;
     }
 }
@@ -1329,10 +1340,11 @@ using namespace ugpg;
 
 extern "C" int ugpg_maxpool2_fwd(ugpg_src_t s, int B, int H, int W, float* out, uint8_t* am,
                                  void* stream) {
-    UGPG_REQUIRE(s.data && out && am && s.C % 4 == 0 && H >= 2 && W >= 2, "maxpool2_fwd");
+    UGPG_REQUIRE((s.data || s.data_bf16) && out && am && s.C % 4 == 0 && H >= 2 && W >= 2,
+                 "maxpool2_fwd");
     const int64_t total = (int64_t)B * (H / 2) * (W / 2) * (s.C / 4);
     hipLaunchKernelGGL(maxpool2_fwd_kernel<false>, dim3(stream_grid(total)), dim3(256), 0,
-                       as_stream(stream), s.data, s.scale, s.shift, B, H, W, s.C, out, am);
+                       as_stream(stream), yref(s), s.scale, s.shift, B, H, W, s.C, out, am);
     return check_launch("maxpool2_fwd");
 }
 
@@ -1346,10 +1358,10 @@ extern "C" int ugpg_maxpool2_bwd(const float* dout, const uint8_t* am, int B, in
 }
 
 static bool bnb_args(const ugpg_bnb_t* d, int64_t npix, int C, BnbArgs& b) {
-    if (!d || !d->y || !d->mean || !d->invstd || !d->scale || !d->shift || !d->part ||
+    if (!d || (!d->y && !d->y_bf16) || !d->mean || !d->invstd || !d->scale || !d->shift || !d->part ||
         d->nslots != ugpg_bnb_slots(npix, C) || C % 4 || C > 1024)
         return false;
-    b.y = d->y;
+    b.y = yref(d->y, d->y_bf16);
     b.mean = d->mean;
     b.invstd = d->invstd;
     b.scale = d->scale;
@@ -1373,8 +1385,9 @@ extern "C" int ugpg_maxpool2_bwd_bnb(const float* dout, const uint8_t* am, int B
 }
 
 extern "C" int ugpg_bilinear_nhwc_fwd(ugpg_src_t s, int B, int Hi, int Wi, float* out, int Ho,
-                                      int Wo, void* stream) {
-    UGPG_REQUIRE(s.data && out && s.C % 4 == 0 && Ho > 0 && Wo > 0, "bilinear_nhwc_fwd");
+                                      int Wo, void* out_bf16, void* stream) {
+    UGPG_REQUIRE((s.data || s.data_bf16) && (out || out_bf16) && s.C % 4 == 0 && Ho > 0 && Wo > 0,
+                 "bilinear_nhwc_fwd");
     UGPG_REQUIRE((int64_t)B * Ho < 65536, "bilinear_nhwc_fwd: shape");
     // a quarter of the row's quads in threads when that divides evenly (the kernel's
     // 4-quads-per-thread form), else one quad per thread
@@ -1382,7 +1395,8 @@ extern "C" int ugpg_bilinear_nhwc_fwd(ugpg_src_t s, int B, int Hi, int Wi, float
     const unsigned gx = nq % 1024 == 0 ? (unsigned)std::min<int64_t>(nq / 1024, 64)
                                        : (unsigned)std::min<int64_t>(cdiv(nq, 256), 64);
     hipLaunchKernelGGL(bilinear_nhwc_fwd_kernel, dim3(gx, (unsigned)(B * Ho)), dim3(256), 0,
-                       as_stream(stream), s.data, s.scale, s.shift, B, Hi, Wi, s.C, out, Ho, Wo);
+                       as_stream(stream), yref(s), s.scale, s.shift, B, Hi, Wi, s.C, out,
+                       out ? nullptr : static_cast<__bf16*>(out_bf16), Ho, Wo);
     return check_launch("bilinear_nhwc_fwd");
 }
 
@@ -1403,9 +1417,9 @@ extern "C" int ugpg_bilinear_nhwc_bwd_bnb(const float* dout, int B, int Ho, int 
     // one workgroup (= partial slot) per input row; its threads keep their channels
     UGPG_REQUIRE(dout && din && B > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0 && C % 4 == 0 &&
                      C <= 1024 && 256 % (C / 4) == 0 && bnb && bnb->nslots == B * Hi &&
-                     bnb->y && bnb->mean && bnb->invstd && bnb->scale && bnb->shift && bnb->part,
+                     (bnb->y || bnb->y_bf16) && bnb->mean && bnb->invstd && bnb->scale && bnb->shift && bnb->part,
                  "bilinear_nhwc_bwd_bnb");
-    b.y = bnb->y;
+    b.y = yref(bnb->y, bnb->y_bf16);
     b.mean = bnb->mean;
     b.invstd = bnb->invstd;
     b.scale = bnb->scale;
@@ -1473,22 +1487,22 @@ extern "C" int ugpg_nhwc_to_nchw(const float* in, int B, int C, int H, int W, in
 
 extern "C" int ugpg_head_fwd(ugpg_src_t s, int64_t npix, const float* w, const float* b, int nc,
                              float* h, void* stream) {
-    UGPG_REQUIRE(s.data && w && b && h && s.C % 64 == 0 && s.C <= 64 * HEAD_CJ_MAX && nc >= 1 &&
+    UGPG_REQUIRE((s.data || s.data_bf16) && w && b && h && s.C % 64 == 0 && s.C <= 64 * HEAD_CJ_MAX && nc >= 1 &&
                      nc <= HEAD_NC_MAX,
                  "head_fwd");
     const dim3 grid(stream_grid(cdiv(npix, (int64_t)4) * 16));
     if (s.C == 64)
-        hipLaunchKernelGGL(head_fwd_cj_kernel<1>, grid, dim3(256), 0, as_stream(stream), s.data,
+        hipLaunchKernelGGL(head_fwd_cj_kernel<1>, grid, dim3(256), 0, as_stream(stream), yref(s),
                            s.scale, s.shift, npix, w, b, nc, h);
     else if (s.C == 128)
-        hipLaunchKernelGGL(head_fwd_cj_kernel<2>, grid, dim3(256), 0, as_stream(stream), s.data,
+        hipLaunchKernelGGL(head_fwd_cj_kernel<2>, grid, dim3(256), 0, as_stream(stream), yref(s),
                            s.scale, s.shift, npix, w, b, nc, h);
     else if (s.C == 256)
-        hipLaunchKernelGGL(head_fwd_cj_kernel<4>, grid, dim3(256), 0, as_stream(stream), s.data,
+        hipLaunchKernelGGL(head_fwd_cj_kernel<4>, grid, dim3(256), 0, as_stream(stream), yref(s),
                            s.scale, s.shift, npix, w, b, nc, h);
     else
         hipLaunchKernelGGL(head_fwd_kernel, dim3(stream_grid(npix * 16)), dim3(256), 0,
-                           as_stream(stream), s.data, s.scale, s.shift, npix, s.C, w, b, nc, h);
+                           as_stream(stream), yref(s), s.scale, s.shift, npix, s.C, w, b, nc, h);
     return check_launch("head_fwd");
 }
 
@@ -1543,7 +1557,8 @@ extern "C" int ugpg_head_bwd(ugpg_src_t s, int64_t npix, const float* w, int nc,
 extern "C" int ugpg_head_bwd_bnb(ugpg_src_t s, int64_t npix, const float* w, int nc,
                                  const float* dh, float* dw, float* db, float* da, int acc_da,
                                  void* ws, size_t ws_bytes, const ugpg_bnb_t* bnb, void* stream) {
-    UGPG_REQUIRE(bnb && bnb->y == s.data && s.scale && bnb->nslots == ugpg_head_bwd_bnb_slots(npix),
+    UGPG_REQUIRE(bnb && bnb->y == s.data && bnb->y_bf16 == (s.data ? bnb->y_bf16 : s.data_bf16) &&
+                     s.scale && bnb->nslots == ugpg_head_bwd_bnb_slots(npix),
                  "head_bwd_bnb");
     return head_bwd_common(s, npix, w, nc, dh, dw, db, da, acc_da, ws, ws_bytes, bnb, stream);
 }
@@ -1551,14 +1566,14 @@ extern "C" int ugpg_head_bwd_bnb(ugpg_src_t s, int64_t npix, const float* w, int
 static int head_bwd_common(ugpg_src_t s, int64_t npix, const float* w, int nc, const float* dh,
                            float* dw, float* db, float* da, int acc_da, void* ws,
                            size_t ws_bytes, const ugpg_bnb_t* bnbd, void* stream) {
-    UGPG_REQUIRE(s.data && w && dh && dw && da && s.C % 64 == 0 && s.C <= 64 * HEAD_CJ_MAX &&
+    UGPG_REQUIRE((s.data || s.data_bf16) && w && dh && dw && da && s.C % 64 == 0 && s.C <= 64 * HEAD_CJ_MAX &&
                      nc >= 1 && nc <= HEAD_NC_MAX,
                  "head_bwd");
     BnbArgs bnb{};
     if (bnbd) {
         UGPG_REQUIRE(bnbd->mean && bnbd->invstd && bnbd->scale && bnbd->shift && bnbd->part,
                      "head_bwd_bnb");
-        bnb.y = bnbd->y;
+        bnb.y = yref(bnbd->y, bnbd->y_bf16);
         bnb.mean = bnbd->mean;
         bnb.invstd = bnbd->invstd;
         bnb.scale = bnbd->scale;
@@ -1574,7 +1589,7 @@ static int head_bwd_common(ugpg_src_t s, int64_t npix, const float* w, int nc, c
     int64_t ppb;
     const int nblk = head_nblk(npix, ppb);
     hipStream_t st = as_stream(stream);
-    using K = void (*)(const float*, const float*, const float*, int64_t, int, const float*, int,
+    using K = void (*)(YRef, const float*, const float*, int64_t, int, const float*, int,
                        const float*, float*, int, int64_t, float*, int, BnbArgs);
 #define HB(B_)                                                                              \
     {{head_bwd_kernel<1, 1, B_>, head_bwd_kernel<1, 2, B_>, head_bwd_kernel<1, 3, B_>,     \
@@ -1588,7 +1603,7 @@ static int head_bwd_common(ugpg_src_t s, int64_t npix, const float* w, int nc, c
     static const K table[2][HEAD_NC_MAX][HEAD_CJ_MAX] = {HB(false), HB(true)};
 #undef HB
     hipLaunchKernelGGL(table[bnbd ? 1 : 0][nc - 1][s.C / 64 - 1], dim3(nblk), dim3(256), 0, st,
-                       s.data, s.scale, s.shift, npix, s.C, w, nc, dh, da, acc_da, ppb,
+                       yref(s), s.scale, s.shift, npix, s.C, w, nc, dh, da, acc_da, ppb,
                        static_cast<float*>(ws), nblk, bnb);
     if (int e = check_launch("head_bwd")) return e;
     hipLaunchKernelGGL(head_bwd_finalize_kernel, dim3((unsigned)cdiv(nc * (s.C + 1), 64)), dim3(1024), 0,
@@ -1761,9 +1776,9 @@ extern "C" int ugpg_rmsprop_step(float* p, const float* g, float* v, int64_t n, 
 }
 
 extern "C" int ugpg_avgpool_fwd(ugpg_src_t s, int B, int HW, float* out, void* stream) {
-    UGPG_REQUIRE(s.data && out && s.C % 4 == 0, "avgpool_fwd");
+    UGPG_REQUIRE((s.data || s.data_bf16) && out && s.C % 4 == 0, "avgpool_fwd");
     hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(stream_grid((int64_t)B * s.C / 4)), dim3(256), 0,
-                       as_stream(stream), s.data, s.scale, s.shift, B, HW, s.C, out);
+                       as_stream(stream), yref(s), s.scale, s.shift, B, HW, s.C, out);
     return check_launch("avgpool_fwd");
 }
 

@@ -26,14 +26,14 @@ class ConvDesc(C.Structure):
     _fields_ = [("B", _i), ("H", _i), ("W", _i), ("src", Src * 2), ("wpk", _p), ("bias", _p),
                 ("Cout", _i), ("out", _p * 2), ("out_split", _i), ("accumulate", _i * 2),
                 ("stats", _p), ("stats_slots", _i), ("wfmt", _i), ("bnb_y", _p),
-                ("bnb_mean", _p), ("bnb_invstd", _p), ("bnb_scale", _p), ("bnb_shift", _p),
+                ("bnb_y_bf16", _p), ("bnb_mean", _p), ("bnb_invstd", _p), ("bnb_scale", _p), ("bnb_shift", _p),
                 ("bnb_part", _p), ("bnb_slots", _i), ("out_bf16", _p)]
 
 
 class Bnb(C.Structure):
     """ugpg_bnb_t."""
-    _fields_ = [("y", _p), ("mean", _p), ("invstd", _p), ("scale", _p), ("shift", _p),
-                ("part", _p), ("nslots", _i)]
+    _fields_ = [("y", _p), ("y_bf16", _p), ("mean", _p), ("invstd", _p), ("scale", _p),
+                ("shift", _p), ("part", _p), ("nslots", _i)]
 
 
 class PackItem(C.Structure):
@@ -61,16 +61,17 @@ SIGNATURES = {
     "ugpg_bn_finalize": (_i, [_p, _i, _i, _p, _p, _p, _p, _p, _f, _f, _p, _p, _p, _p, _p]),
     "ugpg_bn_eval_params": (_i, [_p, _p, _p, _p, _f, _i, _p, _p, _p]),
     "ugpg_bn_relu_bwd_workspace": (_sz, [_i64, _i]),
-    "ugpg_bn_relu_bwd": (_i, [_p, _p, _i64, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i, _p, _sz, _p]),
+    "ugpg_bn_relu_bwd": (_i, [_p, _p, _p, _i64, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i, _p, _sz,
+                              _p]),
     "ugpg_bn_relu_bwd_partials_workspace": (_sz, [_i]),
-    "ugpg_bn_relu_bwd_partials": (_i, [_p, _i, _p, _p, _i64, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i,
-                                       _p, _sz, _p]),
+    "ugpg_bn_relu_bwd_partials": (_i, [_p, _i, _p, _p, _p, _i64, _i, _p, _p, _p, _p, _p, _p, _p,
+                                       _p, _i, _p, _sz, _p]),
     "ugpg_bn_relu_apply": (_i, [Src, _i64, _p, _p]),
     "ugpg_maxpool2_fwd": (_i, [Src, _i, _i, _i, _p, _p, _p]),
     "ugpg_maxpool2_bwd": (_i, [_p, _p, _i, _i, _i, _i, _p, _i, _p]),
     "ugpg_maxpool2_bwd_bnb": (_i, [_p, _p, _i, _i, _i, _i, _p, _i, C.POINTER(Bnb), _p]),
     "ugpg_bnb_slots": (_i, [_i64, _i]),
-    "ugpg_bilinear_nhwc_fwd": (_i, [Src, _i, _i, _i, _p, _i, _i, _p]),
+    "ugpg_bilinear_nhwc_fwd": (_i, [Src, _i, _i, _i, _p, _i, _i, _p, _p]),
     "ugpg_bilinear_nhwc_bwd": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _i, _p]),
     "ugpg_bilinear_nhwc_bwd_bnb": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _i, C.POINTER(Bnb), _p]),
     "ugpg_cast_f32_bf16": (_i, [_p, _p, _i64, _p]),

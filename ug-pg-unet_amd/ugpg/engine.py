@@ -24,11 +24,16 @@ from .ops import Act
 # A/B switch: BN1's backward reduction fused into the data gradient of conv2
 _FUSE_BN_BWD = os.environ.get("UGPG_FUSE_BN_BWD", "1") != "0"
 _FUSE_BN_BWD_MIN_K = int(os.environ.get("UGPG_FUSE_BN_BWD_MIN_K", "64"))
-# bf16 copies of the conv outputs under the bf16 arithmetic (config 3), read by the next
-# convs' loaders: off by default -- measured 2.5 % slower (the single-piece form is not
-# bound by its halo bytes, and the copy's stores lengthen the epilogue); the oracle's
-# bf16 model follows oracle.ref_cpu.BF16_STORE
-_BF16_STORE = os.environ.get("UGPG_BF16_STORE", "0") == "1"
+
+
+def _store16(W: int) -> bool:
+    """bf16 storage of activations of an image this wide: under the bf16 arithmetic
+    (config 3) every conv output, and the upsampled input of an Up conv, of an image
+    >= 32 wide is kept in bf16 only (torch.autocast keeps bf16 conv outputs): its readers
+    -- the next conv, max-pool, bilinear x2, the heads, BatchNorm backward, the weight
+    gradient -- read half the bytes.  BatchNorm's statistics describe the stored (rounded)
+    values; the oracle models it as oracle.ref_cpu.BF16_STORE."""
+    return ops.conv_math() == "bf16" and W >= 32
 
 
 def ceil_to(v: int, m: int) -> int:
@@ -61,6 +66,11 @@ class BlockCtx:
     part2: torch.Tensor = None  # BN2-backward partials written by the last producer of da2
 
 
+def _grad_like(y):
+    """An fp32 gradient buffer shaped like activation y (whatever y's storage)."""
+    return torch.empty(y.shape, dtype=torch.float32, device=y.device)
+
+
 def _conv_bn(seq):
     return (seq[0], seq[1]), (seq[3], seq[4])
 
@@ -80,7 +90,10 @@ def double_conv_forward(mod, srcs, ctx: BlockCtx, save: bool):
         if w.shape[1] > cin:
             raise ValueError(f"conv expects {w.shape[1]} input channels, got {cin}")
         wpk = ops.pack_conv3x3(w.detach(), ops.conv_pack_k(cin), 0)
-        y = ops.empty(B, H, W, cout, like=srcs[0].y)
+        # bf16 storage: the single-piece form writes it, and the image layer's fp32 kernel
+        store16 = _store16(W) and (wpk.ugpg_fmt == ops.WFMT_BF16 or (cin == 8 and cout in (64, 128)))
+        y = ops.empty(B, H, W, cout, like=srcs[0].y,
+                      dtype=torch.bfloat16 if store16 else torch.float32)
         train = _bn_mode(bn)
         stats = None
         ntiles = 0
@@ -88,13 +101,8 @@ def double_conv_forward(mod, srcs, ctx: BlockCtx, save: bool):
             ntiles = ops.conv_ntiles(B, H, W, cin, cout, wpk)
             stats = ops.empty(3 * cout * ntiles, like=y)
         bias = conv.bias.detach() if conv.bias is not None else None
-        # bf16 arithmetic: a bf16 copy of y for the next convs' loaders (the persistent
-        # single-piece form, images >= 32 wide), written beside y by the same epilogue
-        y16 = None
-        if _BF16_STORE and W >= 32 and ops.conv_math() == "bf16":
-            y16 = ops.empty(B, H, W, cout, like=y, dtype=torch.bfloat16)
         ops.conv3x3_fwd(cur, wpk, bias, cout, [y], stats=stats,
-                        flops=2.0 * B * H * W * cout * 9 * w.shape[1], out16=y16)
+                        flops=2.0 * B * H * W * cout * 9 * w.shape[1])
         if train:
             if bn.momentum is None:
                 raise NotImplementedError("BatchNorm2d(momentum=None) is not supported")
@@ -114,7 +122,7 @@ def double_conv_forward(mod, srcs, ctx: BlockCtx, save: bool):
                 ctx.y1, ctx.st1 = y, st
             else:
                 ctx.y2, ctx.st2 = y, st
-        cur = [Act(y, scale, shift, y16)]
+        cur = [Act(y, scale, shift)]
         cin = cout
     return cur[0]
 
@@ -206,6 +214,15 @@ class UNetGraph:
                     specs.append((w1, w1.shape[1], 1))
         return specs
 
+    def prepare_eval_bn(self):
+        """Eval-mode BatchNorm coefficients of every block, cached on the modules (the same
+        call double_conv_forward makes), computed on the current stream."""
+        for blk in self.blocks:
+            for _, bn in _conv_bn(blk.mod.conv_op):
+                if not _bn_mode(bn):
+                    ops.bn_eval_params(bn.weight.detach(), bn.bias.detach(), bn.running_mean,
+                                       bn.running_var, float(bn.eps), owner=bn)
+
     # -------------------------------------------------------------- forward
     def forward(self, x, save: bool):
         if x.dim() != 4:
@@ -235,7 +252,7 @@ class UNetGraph:
             elif blk.kind == "up":
                 skip, low = outs[blk.inputs[0]], outs[blk.inputs[1]]
                 _, h, w, _ = low.shape
-                u = ops.bilinear_nhwc_fwd(low, 2 * h, 2 * w)
+                u = ops.bilinear_nhwc_fwd(low, 2 * h, 2 * w, bf16=_store16(2 * w))
                 if u.shape[1:3] != skip.shape[1:3]:
                     raise ValueError("Up: upsampled size does not match the skip connection")
                 ctx.extra["low_hw"] = (h, w)
@@ -296,7 +313,7 @@ class UNetGraph:
                 a = outs[hd.block]
                 acc = da[hd.block] is not None
                 if not acc:
-                    da[hd.block] = torch.empty_like(a.y)
+                    da[hd.block] = _grad_like(a.y)
                 dw = grads.get(conv.weight)
                 dw_flat = dw.view(w.shape) if dw is not None else torch.empty_like(w)
                 db = grads.get(conv.bias)
@@ -326,12 +343,12 @@ class UNetGraph:
                     double_conv_backward(blk.mod, ctx, g, [None], [0], grads)
             elif blk.kind == "down":
                 src = blk.inputs[0]
-                dp = torch.empty_like(ctx.srcs[0].y)
+                dp = _grad_like(ctx.srcs[0].y)
                 double_conv_backward(blk.mod, ctx, g, [dp], [0], grads)
                 H, W = ctx.extra["in_hw"]
                 acc = da[src] is not None
                 if not acc:
-                    da[src] = torch.empty_like(outs[src].y)
+                    da[src] = _grad_like(outs[src].y)
                 st = bn2_state(src, bi)
                 part = ops.maxpool2_bwd(dp, ctx.extra["argmax"], H, W, da[src], acc, bnb=st)
                 if part is not None:
@@ -340,13 +357,13 @@ class UNetGraph:
                 skip, low = blk.inputs
                 acc_s = da[skip] is not None
                 if not acc_s:
-                    da[skip] = torch.empty_like(outs[skip].y)
-                du = torch.empty_like(ctx.srcs[1].y)
+                    da[skip] = _grad_like(outs[skip].y)
+                du = _grad_like(ctx.srcs[1].y)
                 double_conv_backward(blk.mod, ctx, g, [da[skip], du], [acc_s, 0], grads)
                 h, w = ctx.extra["low_hw"]
                 acc_l = da[low] is not None
                 if not acc_l:
-                    da[low] = torch.empty_like(outs[low].y)
+                    da[low] = _grad_like(outs[low].y)
                 part = ops.bilinear_nhwc_bwd(du, h, w, da[low], acc_l, bnb=bn2_state(low, bi))
                 if part is not None:
                     ctxs[low].part2 = part

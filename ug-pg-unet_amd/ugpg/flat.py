@@ -41,9 +41,14 @@ def ensure_flat(module: torch.nn.Module) -> None:
     total = sum(p.numel() for p in params)
     flat = torch.empty(total, dtype=torch.float32, device=dev)
     off = 0
+    cur = torch.cuda.current_stream(dev)
     with torch.no_grad():
         for p in params:
             n = p.numel()
             flat[off:off + n].copy_(p.data.reshape(-1))
+            # the old storage dies here while the copy may still be pending on the current
+            # stream: if it was allocated on another stream, its block must not go back to
+            # that stream's pool before the copy has read it
+            p.data.record_stream(cur)
             p.data = flat[off:off + n].view_as(p)
             off += n

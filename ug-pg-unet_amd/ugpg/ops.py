@@ -41,6 +41,11 @@ def empty(*shape, like=None, device=None, dtype=F32):
     return torch.empty(*shape, dtype=dtype, device=dev)
 
 
+def _yargs(y):
+    """(fp32 pointer, bf16 pointer) of a BatchNorm input stored in either precision."""
+    return (None, ptr(y)) if y.dtype == torch.bfloat16 else (ptr(y), None)
+
+
 def workspace(nbytes: int, device) -> torch.Tensor:
     return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
 
@@ -49,13 +54,13 @@ class Act:
     """A lazily-activated NHWC tensor: value = relu(scale*y + shift) when scale is set.
 
     BatchNorm + ReLU of a DoubleConv (UG_unet_parts.py:11-12) is folded into the
-    consumer's load, so the normalised activation is never written to HBM.
-    y16: optional bf16 copy of y, read by the bf16-arithmetic conv loaders.
-    """
-    __slots__ = ("y", "scale", "shift", "y16")
+    consumer's load, so the normalised activation is never written to HBM.  y is fp32,
+    or bf16 under the bf16 arithmetic (the storage of conv outputs of images >= 32 wide:
+    ugpg_src_t.data_bf16)."""
+    __slots__ = ("y", "scale", "shift")
 
-    def __init__(self, y, scale=None, shift=None, y16=None):
-        self.y, self.scale, self.shift, self.y16 = y, scale, shift, y16
+    def __init__(self, y, scale=None, shift=None):
+        self.y, self.scale, self.shift = y, scale, shift
 
     @property
     def shape(self):
@@ -66,12 +71,13 @@ class Act:
         return self.y.shape[-1]
 
     def src(self) -> Src:
-        return Src(ptr(self.y), ptr(self.scale), ptr(self.shift), self.C, ptr(self.y16))
+        y, y16 = _yargs(self.y)
+        return Src(y, ptr(self.scale), ptr(self.shift), self.C, y16)
 
     def materialize(self) -> torch.Tensor:
-        if self.scale is None:
+        if self.scale is None and self.y.dtype == F32:
             return self.y
-        out = torch.empty_like(self.y)
+        out = torch.empty(self.y.shape, dtype=F32, device=self.y.device)
         check(lib.ugpg_bn_relu_apply(self.src(), self.y.numel() // self.C, ptr(out), stream()),
               "bn_relu_apply")
         return out
@@ -257,20 +263,23 @@ def _timed(name, flops, fn):
 
 
 def conv3x3_fwd(srcs, wpk, bias, cout, outs, split=None, accumulate=(0, 0), stats=None,
-                flops=None, bnb=None, out16=None):
-    """srcs: 1-2 Act; outs: 1-2 NHWC tensors (channel split at `split`).
+                flops=None, bnb=None):
+    """srcs: 1-2 Act; outs: 1-2 NHWC tensors (channel split at `split`); a bf16 outs[0]
+    (one output) stores the result in bf16 only (the bf16 arithmetic's storage).
     flops: algorithmic FLOPs of this call (for the optional KernelTimer).
     bnb: (y, mean, invstd, scale, shift, part) -- also write the BatchNorm-backward
     partials of outs[0] = dL/d(relu(bn(y))) into `part` (3*cout*conv_ntiles floats) for
-    bn_relu_bwd(..., part=part).  out16: a bf16 tensor shaped like outs[0] that also
-    receives the output (the bf16 arithmetic's activation copy)."""
+    bn_relu_bwd(..., part=part)."""
     B, H, W, _ = srcs[0].shape
     d = ConvDesc()
     d.B, d.H, d.W = B, H, W
     d.src[0] = srcs[0].src()
     d.src[1] = srcs[1].src() if len(srcs) > 1 else NULL_SRC
     d.wpk, d.bias, d.Cout = ptr(wpk), ptr(bias), cout
-    d.out[0] = ptr(outs[0])
+    if outs[0].dtype == torch.bfloat16:
+        d.out[0], d.out_bf16 = None, ptr(outs[0])
+    else:
+        d.out[0] = ptr(outs[0])
     d.out[1] = ptr(outs[1]) if len(outs) > 1 else None
     d.out_split = cout if split is None else split
     d.accumulate[0], d.accumulate[1] = int(accumulate[0]), int(accumulate[1])
@@ -279,11 +288,9 @@ def conv3x3_fwd(srcs, wpk, bias, cout, outs, split=None, accumulate=(0, 0), stat
         d.stats_slots = stats.numel() // (3 * cout)
     d.wfmt = wpk.ugpg_fmt
     if bnb is not None:
-        (d.bnb_y, d.bnb_mean, d.bnb_invstd, d.bnb_scale, d.bnb_shift,
-         d.bnb_part) = (ptr(t) for t in bnb)
+        d.bnb_y, d.bnb_y_bf16 = _yargs(bnb[0])
+        d.bnb_mean, d.bnb_invstd, d.bnb_scale, d.bnb_shift, d.bnb_part = (ptr(t) for t in bnb[1:])
         d.bnb_slots = bnb[5].numel() // (3 * cout)
-    if out16 is not None:
-        d.out_bf16 = ptr(out16)
     _timed("conv3x3_fwd", flops,
            lambda: check(lib.ugpg_conv3x3_fwd(C.byref(d), stream()), "conv3x3_fwd"))
 
@@ -351,12 +358,12 @@ def bn_relu_bwd(da, y, mean, invstd, scale, shift, dy, dgamma, dbeta, dconv_bias
     if part is not None:
         ws = workspace(lib.ugpg_bn_relu_bwd_partials_workspace(c), y.device)
         check(lib.ugpg_bn_relu_bwd_partials(
-            ptr(part), part.numel() // (3 * c), ptr(da), ptr(y), npix, c, ptr(mean), ptr(invstd),
+            ptr(part), part.numel() // (3 * c), ptr(da), *_yargs(y), npix, c, ptr(mean), ptr(invstd),
             ptr(scale), ptr(shift), ptr(dy), ptr(dgamma), ptr(dbeta), ptr(dconv_bias),
             int(accumulate), ptr(ws), ws.numel(), stream()), "bn_relu_bwd_partials")
         return
     ws = workspace(lib.ugpg_bn_relu_bwd_workspace(npix, c), y.device)
-    check(lib.ugpg_bn_relu_bwd(ptr(da), ptr(y), npix, c, ptr(mean), ptr(invstd), ptr(scale),
+    check(lib.ugpg_bn_relu_bwd(ptr(da), *_yargs(y), npix, c, ptr(mean), ptr(invstd), ptr(scale),
                                ptr(shift), ptr(dy), ptr(dgamma), ptr(dbeta), ptr(dconv_bias),
                                int(accumulate), ptr(ws), ws.numel(), stream()), "bn_relu_bwd")
 
@@ -379,7 +386,8 @@ def bnb_desc(bn_state, npix, c, like, nslots=None):
         raise ValueError(f"no BatchNorm-backward partials for C={c}")
     part = empty(3 * c * n, like=like)
     d = Bnb()
-    d.y, d.mean, d.invstd, d.scale, d.shift = (ptr(t) for t in bn_state)
+    d.y, d.y_bf16 = _yargs(bn_state[0])
+    d.mean, d.invstd, d.scale, d.shift = (ptr(t) for t in bn_state[1:])
     d.part, d.nslots = ptr(part), n
     return d, part
 
@@ -398,10 +406,13 @@ def maxpool2_bwd(dout, am, H, W, din, accumulate, bnb=None):
     return None
 
 
-def bilinear_nhwc_fwd(a: Act, Ho, Wo):
+def bilinear_nhwc_fwd(a: Act, Ho, Wo, bf16=False):
+    """bf16: store the result in bf16 (an Up conv's input under the bf16 arithmetic, which
+    that conv and its weight gradient round to bf16 anyway)."""
     B, Hi, Wi, c = a.shape
-    out = empty(B, Ho, Wo, c, like=a.y)
-    check(lib.ugpg_bilinear_nhwc_fwd(a.src(), B, Hi, Wi, ptr(out), Ho, Wo, stream()),
+    out = empty(B, Ho, Wo, c, like=a.y, dtype=torch.bfloat16 if bf16 else F32)
+    o32, o16 = _yargs(out)
+    check(lib.ugpg_bilinear_nhwc_fwd(a.src(), B, Hi, Wi, o32, Ho, Wo, o16, stream()),
           "bilinear_nhwc_fwd")
     return out
 
@@ -508,7 +519,8 @@ def head_bwd(a: Act, w, dh, dw, db, da, accumulate, bnb=None):
         n = lib.ugpg_head_bwd_bnb_slots(npix)
         part = empty(3 * c * n, like=da)
         d = Bnb()
-        d.y, d.mean, d.invstd, d.scale, d.shift = (ptr(t) for t in (a.y, *bnb, a.scale, a.shift))
+        d.y, d.y_bf16 = _yargs(a.y)
+        d.mean, d.invstd, d.scale, d.shift = (ptr(t) for t in (*bnb, a.scale, a.shift))
         d.part, d.nslots = ptr(part), n
         check(lib.ugpg_head_bwd_bnb(a.src(), npix, _f32(w), nc, ptr(dh), ptr(dw), ptr(db),
                                     ptr(da), int(accumulate), ptr(ws), ws.numel(), C.byref(d),

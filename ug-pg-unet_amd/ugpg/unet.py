@@ -76,6 +76,19 @@ class _PGUNetBase(nn.Module):
         ensure_flat(self)
         return Fn.run_logits(self.graph(), x, list(self.parameters()))
 
+    def prepare_eval(self):
+        """Build this model's persistent device state for an eval forward -- the flat
+        parameter buffer, the forward weight packs and the eval-mode BatchNorm
+        coefficients (all cached on the parameters / modules) -- on the current stream.
+        A forward issued afterwards on another stream then only reads that state: the
+        trainer runs the previous stage's U-map forward on a second stream, and state
+        first created there would be allocated from, and on replacement freed to, that
+        stream's pool while the other stream may still read it."""
+        ensure_flat(self)
+        g = self.graph()
+        ops.prepack(g._pack_specs(8, False))
+        g.prepare_eval_bn()
+
 
 class PGUNet1(_PGUNetBase):
     """Stage 1 (32x32): inc -> down4 -> up1 -> outc (UG_unet.py:178-193)."""

@@ -14,7 +14,7 @@ import torch.nn as nn
 
 from . import functional as Fn
 from . import ops
-from .engine import Block, UNetGraph
+from .engine import Block, UNetGraph, _grad_like
 
 
 def _conv_bn_relu_layers(cin: int, cout: int):
@@ -127,7 +127,7 @@ class _StandaloneDown(torch.autograd.Function):
         views = _grad_views(ctx.params, need[2:])
         grads = {p: v for p, v in zip(ctx.params, views) if v is not None}
         da = ops.nchw_to_nhwc(dout.contiguous(), dout.shape[1])
-        dp = torch.empty_like(ctx.bctx.srcs[0].y)
+        dp = _grad_like(ctx.bctx.srcs[0].y)
         double_conv_backward(ctx.mod.double_conv, ctx.bctx, da, [dp], [0], grads)
         dx = None
         if need[1]:
@@ -161,8 +161,8 @@ class _StandaloneUp(torch.autograd.Function):
         views = _grad_views(ctx.params, need[3:])
         grads = {p: v for p, v in zip(ctx.params, views) if v is not None}
         da = ops.nchw_to_nhwc(dout.contiguous(), dout.shape[1])
-        dskip = torch.empty_like(ctx.bctx.srcs[0].y)
-        du = torch.empty_like(ctx.bctx.srcs[1].y)
+        dskip = _grad_like(ctx.bctx.srcs[0].y)
+        du = _grad_like(ctx.bctx.srcs[1].y)
         double_conv_backward(ctx.mod.double_conv, ctx.bctx, da, [dskip, du], [0, 0], grads)
         dx1 = dx2 = None
         if need[1]:
@@ -191,7 +191,7 @@ class _StandaloneHead(torch.autograd.Function):
         dh = ops.nchw_to_nhwc(dout.contiguous(), dout.shape[1])
         dw = torch.empty_like(ctx.w2)
         db = torch.empty(w.shape[0], dtype=torch.float32, device=dout.device)
-        da = torch.empty_like(ctx.a.y)
+        da = _grad_like(ctx.a.y)
         ops.head_bwd(ctx.a, ctx.w2, dh, dw, db, da, 0)
         dx = ops.nhwc_to_nchw(da, da.shape[-1]) if ctx.needs_input_grad[1] else None
         return None, dx, dw.view_as(w), db
