@@ -143,7 +143,12 @@ def test_config3_bf16_bs16_step(dev):
     for k in param_keys(state):
         floor, scale = fc[f"floor16/{k}"]
         err = (grads[k].double() - g16[k].double()).abs().max().item()
-        bound = 1e-5 if is_prebn_bias(k) else 3.0 * floor + 1e-6 * scale
+        bound = 3.0 * floor + 1e-6 * scale
+        if is_prebn_bias(k):
+            # true value 0 (train-mode BN removes it): pure rounding noise, allowed the fp32
+            # test's absolute 1e-5 or the bf16 oracle's own spread, whichever is larger
+            # (the image layer's bf16-stored output: spread 2.5e-5, oracle value 2.1e-5)
+            bound = max(1e-5, bound)
         ratios.append((err / bound, k))
         if err > bound:
             bad.append(f"{k}: {err:.3e} > {bound:.3e}")
