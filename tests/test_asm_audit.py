@@ -17,9 +17,10 @@ ROOT = Path(__file__).resolve().parent.parent
 CSRC = ROOT / "ug-pg-unet_amd" / "csrc"
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 KERNELS = [
-    "_ZN4ugpg22conv3x3_fwd_x6r_kernelILi3ELb1ELi32ELi8EEEvNS_11ConvFwdArgsE",
-    "_ZN4ugpg22conv3x3_fwd_x6r_kernelILi3ELb1ELi16ELi8EEEvNS_11ConvFwdArgsE",
-    "_ZN4ugpg22conv3x3_fwd_x6r_kernelILi1ELb0ELi32ELi8EEEvNS_11ConvFwdArgsE",
+    "_ZN4ugpg22conv3x3_fwd_x6r_kernelILi3ELb1ELi32ELi8ELb0EEEvNS_11ConvFwdArgsE",
+    "_ZN4ugpg22conv3x3_fwd_x6r_kernelILi3ELb1ELi16ELi8ELb0EEEvNS_11ConvFwdArgsE",
+    "_ZN4ugpg22conv3x3_fwd_x6r_kernelILi1ELb0ELi32ELi8ELb0EEEvNS_11ConvFwdArgsE",
+    "_ZN4ugpg22conv3x3_fwd_x6r_kernelILi1ELb0ELi32ELi8ELb1EEEvNS_11ConvFwdArgsE",
     "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi3ELb0EEEvNS_9WgradArgsE",
     "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi1ELb0EEEvNS_9WgradArgsE",
     "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi1ELb1EEEvNS_9WgradArgsE",

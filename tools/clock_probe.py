@@ -26,6 +26,7 @@ from ugpg._C import lib  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--layers", default="inc.3,down1.3,down2.3,up4.0")
+    ap.add_argument("--out16", action="store_true", help="bf16 output storage (math bf16)")
     ap.add_argument("--seconds", type=float, default=2.0)
     ap.add_argument("--stamps", action="store_true")
     ap.add_argument("--wgrad", action="store_true", help="time the weight gradient instead")
@@ -38,12 +39,14 @@ def main():
     for name, H, C0, C1, Cout in LAYERS:
         if name not in a.layers.split(","):
             continue
-        srcs = [ops.Act(torch.randn(B, H, H, C0, device=dev),
+        dt16 = torch.bfloat16 if a.out16 and a.math == "bf16" and H >= 32 and C0 >= 16 else torch.float32
+        srcs = [ops.Act(torch.randn(B, H, H, C0, device=dev).to(dt16),
                         torch.rand(C0, device=dev) + 0.5, torch.randn(C0, device=dev) * 0.1)]
         if C1:
-            srcs.append(ops.Act(torch.randn(B, H, H, C1, device=dev)))
+            srcs.append(ops.Act(torch.randn(B, H, H, C1, device=dev).to(dt16)))
         w = torch.randn(Cout, C0 + C1, 3, 3, device=dev) * 0.05
-        out = torch.empty(B, H, H, Cout, device=dev)
+        out = torch.empty(B, H, H, Cout, device=dev,
+                          dtype=torch.bfloat16 if a.out16 and a.math == "bf16" and H >= 32 else torch.float32)
         wpk = ops.pack_conv3x3(w, C0 + C1, 0)
         st = torch.empty(3 * Cout * ops.conv_ntiles(B, H, H, C0 + C1, Cout, wpk), device=dev)
         flops = 2.0 * B * H * H * Cout * 9 * (C0 + C1)
@@ -61,15 +64,16 @@ def main():
                 torch.cuda.synchronize()
                 n += 20
             dt = (time.perf_counter() - t0) / n
-            v = (ctypes.c_double * 6)()
+            v = (ctypes.c_double * 9)()
             nwg = fn(v)
             if not a.stamps:
                 what = f"clock {v[0]:.0f} MHz"
             elif a.wgrad:
                 what = f"loader vm_wait {v[0]:.1%} barrier {v[3]:.1%}"
             else:
-                what = "loader vm_wait/barrier per phase " + " ".join(
-                    f"p{q}:{v[q]:.1%}/{v[3 + q]:.1%}" for q in range(3))
+                what = ("loader vm_wait/barrier per phase " + " ".join(
+                    f"p{q}:{v[q]:.1%}/{v[3 + q]:.1%}" for q in range(3)) +
+                    f" | compute barrier {v[6]:.1%} epilogue {v[7]:.1%}, {v[8]:.0f} cyc/step")
             print(f"{name}: {dt*1e3:.3f} ms/launch {flops/dt/1e12:.0f} TF  {what} "
                   f"(median of {nwg} workgroups)", flush=True)
 

@@ -18,7 +18,10 @@ for s in "$@"; do
   case $s in
     bisect) step bisect 300 python tools/stream_bisect.py --reps 4 --main fwdbwd ;;
     probe) step probe 300 python tools/umap_stream_probe.py --steps 4 --reps 2 ;;
-    tprobe) step tprobe 300 python tools/umap_trainer_probe.py --steps 4 --reps 3 ;;
+    stamps) step stamps 300 env UGPG_LIB=exp/lib_stamp.so python tools/clock_probe.py --stamps --seconds 1 --layers inc.3,down1.3,down2.3,down3.3,up4.0 &&
+            step stamps16 300 env UGPG_LIB=exp/lib_stamp.so python tools/clock_probe.py --stamps --seconds 1 --math bf16 --out16 --layers inc.3,down1.3,down2.3,down3.3,up4.0 ;;
+    stamp:*) IFS=: read -r _ lib math <<< "$s"
+            step stamp_${lib}_${math} 300 env UGPG_LIB=exp/$lib.so python tools/clock_probe.py --stamps --seconds 1 --math $math --out16 --layers inc.3,down1.3,down2.3,down3.3,up4.0 ;;
     tests:*) f=${s#tests:}; n=$(basename "${f%% *}" .py); step t_${n%%::*} 900 python -u -m pytest $f -q -rf -x --timeout 400 --timeout-method thread -p no:cacheprovider ;;
     alltests) step alltests 1100 python -u -m pytest tests -m gpu -q -rf --timeout 500 --timeout-method thread -p no:cacheprovider ;;
     bench) step bench 600 python bench.py ;;

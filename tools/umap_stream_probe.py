@@ -1,9 +1,12 @@
 """Run-to-run determinism of the trainer's U map on a second HIP stream (diagnostic).
 
 Variants, each repeated from the same weights and inputs:
-  one      -- the one-stream order (trainer.umap_side_stream = False);
-  side     -- the trainer's side stream (ugpg/trainer.py:_umap_on_side), concurrent with
-              the current stage's forward;
+  one      -- the one-stream order (the trainer's);
+  side     -- the previous stage's U-map forward on a side stream, concurrent with the
+              current stage's forward: its persistent state built first on the current
+              stream (prepare_eval), side waits for current, data.record_stream(side),
+              current waits for side before the loss, U.record_stream(current) (the
+              round-3 experiment, removed from the trainer: DESIGN.md §6a);
   noprep   -- the same ordering rules, but the previous stage's persistent state (flat
               parameters, packs, eval BatchNorm coefficients) is first built ON the side
               stream (no prepare_eval on the current stream);
@@ -32,9 +35,13 @@ def patched_forward(mode):
         cur = torch.cuda.current_stream()
         side = self.__dict__.get("_side") or torch.cuda.Stream()
         self._side = side
+        if mode == "side":
+            prev = self.models[stage - 1]
+            prev.eval()
+            prev.prepare_eval()
         if mode != "naive":
             side.wait_stream(cur)
-        # (no prepare_eval: the previous stage's packs etc. are first built on `side`)
+        # (noprep / serial / naive: the previous stage's packs etc. are first built on `side`)
         with torch.cuda.stream(side):
             umap = self.uncertainty_loss.generate_uncertainty_map(
                 data, self.models[stage - 1], self.stage_configs[stage - 1]["resolution"],
@@ -63,8 +70,7 @@ def run(variant, steps, B, res=256):
     tr.models[4].load_state_dict(det_state(4, 3, 1, seed=0))
     tr.current_stage, tr.current_model = 4, tr.models[4]
     tr.setup_optimizer(4)
-    tr.umap_side_stream = variant == "side"
-    if variant in ("noprep", "serial", "naive"):
+    if variant != "one":
         tr._forward_device = patched_forward(variant).__get__(tr)
     x = G.randn(5, (B, 3, res, res), "x").to(dev)
     t = G.bernoulli(6, (B, 1, res, res), 0.5, "t").to(dev)

@@ -382,9 +382,39 @@ __device__ __forceinline__ void lds_barrier() {
 // row (TW == 32): lane (h, c) holds pixels (r&3) + 8(r>>2) + 4h of row wm*MT + mt,
 // channel c, so addresses are one row base + a per-lane offset + a constant per r;
 // the accumulate and bounds decisions are uniform per item.
+//
+// bf16-only storage (the forward under bf16 arithmetic): the lane layout above holds one
+// channel of 16 pixels, so direct stores are 2 bytes per lane (64-byte segments, 16
+// store instructions per m-tile -- measured: half of the K = 64 layers' loop time in
+// the epilogue).  Instead each m-tile goes through the wave's LDS staging area `stg`
+// (32 pixels x 40 floats: the two pixel halves h land on opposite bank halves) and
+// leaves as 16-byte stores of 8 channels (2 per lane per m-tile).
+constexpr int X6_STG_PITCH = 40;
+constexpr int X6_STG_WAVE = 2048;  // floats: 32 x 40 fp32, or the bf16 y tile of 4 m-tiles
+// BatchNorm-backward partials with bf16 y: the item's y tile (MT m-tiles x 32 pixels x the
+// wave's 32 channels) DMA'd into the wave's staging area as [mt][pixel][channel] bf16
+// (2 KiB per m-tile; 16 bytes per lane: pixel (lane>>2) + 16j, channels 8(lane&3)..)
+template <int TH, int TW, int MT>
+__device__ __forceinline__ void x6_dma_bnb_y(const ConvFwdArgs& a, int b, int ty0, int tx0, int n0,
+                                             int wm, int wn, float* stg) {
+    const int lane = threadIdx.x & 63;
+    const int vh = min(TH, a.H - ty0), vw = min(TW, a.W - tx0);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        const int py = min(wm * MT + mt, vh - 1);  // rows past the image: never read back
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int px = min((lane >> 2) + 16 * j, vw - 1), k = lane & 3;
+            const __bf16* g = a.bnb_y.h + ((size_t)(b * a.H + ty0 + py) * a.W + tx0 + px) * a.Cout +
+                              n0 + wn * 32 + 8 * k;
+            glds16(g, reinterpret_cast<char*>(stg) + (mt * 2 + j) * 1024);
+        }
+    }
+}
 template <int TH, int TW, int MT>
 __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&acc)[MT], int tile,
-                                                 int b, int ty0, int tx0, int n0, int wm, int wn) {
+                                                 int b, int ty0, int tx0, int n0, int wm, int wn,
+                                                 float* stg) {
     static_assert(TW == 32, "one image row per 32-pixel MFMA tile");
     const int lane = threadIdx.x & 63, h = lane >> 5;
     const int vh = min(TH, a.H - ty0), vw = min(TW, a.W - tx0);
@@ -438,8 +468,48 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
             }
         }
     };
+    // bf16-only storage through the staging area (no accumulate, no bnb: the host allows
+    // bf16-only outputs on forwards only)
+    auto store16_rows = [&]() {
+        const int l32 = lane & 31;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+            const int py = wm * MT + mt;
+            if (py >= vh) break;  // uniform
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) {
+                float v0, v1;
+                pk_bf16(acc[mt][r] + bv, acc[mt][r + 1] + bv, v0, v1);
+                acc[mt][r] = v0;
+                acc[mt][r + 1] = v1;
+                const int p0 = (r & 3) + 8 * (r >> 2) + 4 * h;  // r + 1: pixel p0 + 1
+                if (fullw || p0 < vw) psum += v0;
+                if (fullw || p0 + 1 < vw) psum += v1;
+                stg[p0 * X6_STG_PITCH + l32] = v0;
+                stg[(p0 + 1) * X6_STG_PITCH + l32] = v1;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            const size_t rowb = (size_t)((b * a.H + ty0 + py) * a.W + tx0) * ostride + ocol0 + wn * 32;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int p = (lane >> 2) + 16 * j, k = lane & 3;
+                const f32x4 lo = *reinterpret_cast<const f32x4*>(stg + p * X6_STG_PITCH + 8 * k);
+                const f32x4 hi = *reinterpret_cast<const f32x4*>(stg + p * X6_STG_PITCH + 8 * k + 4);
+                // exact bf16 values: the packed words are bit selections
+                auto pk = [](float x, float y) {
+                    return (__builtin_bit_cast(unsigned, x) >> 16) |
+                           (__builtin_bit_cast(unsigned, y) & 0xffff0000u);
+                };
+                const u32x4 w = {pk(lo.x, lo.y), pk(lo.z, lo.w), pk(hi.x, hi.y), pk(hi.z, hi.w)};
+                if (fullw || p < vw)
+                    *reinterpret_cast<u32x4*>(a.out0_16 + rowb + (size_t)p * ostride + 8 * k) = w;
+            }
+            asm volatile("" ::: "memory");  // the next m-tile's staging writes after these reads
+        }
+    };
     const bool bnb = a.bnb_part != nullptr && !oacc;  // (the host refuses bnb + accumulate)
     if (oacc) store_rows(std::integral_constant<bool, true>{}, 0, MT);
+    else if (only16 && !bnb) store16_rows();
     else if (!bnb) store_rows(std::integral_constant<bool, false>{}, 0, MT);
     if (bnb) {
         // BatchNorm-backward partials of the stored output (as x6q_epilogue_wave): this
@@ -448,29 +518,43 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
         const float mu = a.bnb_mean[n], is = a.bnb_invstd[n], sc = a.bnb_scale[n],
                     sh = a.bnb_shift[n];
         float sg = 0.f, sgx = 0.f, sx = 0.f;
+        if (a.bnb_y.h) vm_wait<0>();  // the staged y tile has landed
+        auto part = [&](int mt, int r, float y) {
+            const int pxc = (r & 3) + 8 * (r >> 2);
+            if (fullw || pxc + 4 * h < vw) {
+                const float gv = fmaf(y, sc, sh) > 0.f ? acc[mt][r] : 0.f;
+                const float xh = (y - mu) * is;
+                sg += gv;
+                sgx = fmaf(gv, xh, sgx);
+                sx += xh;
+            }
+        };
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
             const int py = wm * MT + mt;
             if (py >= vh) break;  // uniform
-            const size_t yrow = (size_t)((b * a.H + ty0 + py) * a.W + tx0 + 4 * h) * a.Cout + n;
-            float yv[16];
+            if (a.bnb_y.h) {
+                // bf16 y: the item's tile was DMA'd into the staging area during its last
+                // step (conv3x3_fwd_x6r_kernel, x6_dma_bnb_y); lane (h, c) reads channel c
+                // of its pixels (2-byte gathers from HBM ran the data gradient at half the
+                // forward's speed)
+                store_rows(std::integral_constant<bool, false>{}, mt, mt + 1);
+                const __bf16* t16 = reinterpret_cast<const __bf16*>(stg) + mt * 1024 + (lane & 31);
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int pxc = min((r & 3) + 8 * (r >> 2), vw - 1 - 4 * h);
-                yv[r] = a.bnb_y.ld1(yrow + (size_t)max(pxc, -4 * h) * a.Cout);
-            }
-            // this row's output stores issue while its y loads are in flight
-            store_rows(std::integral_constant<bool, false>{}, mt, mt + 1);
+                for (int r = 0; r < 16; ++r)
+                    part(mt, r, (float)t16[((r & 3) + 8 * (r >> 2) + 4 * h) * 32]);
+            } else {
+                float yv[16];
+                const size_t yrow = (size_t)((b * a.H + ty0 + py) * a.W + tx0 + 4 * h) * a.Cout + n;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int pxc = (r & 3) + 8 * (r >> 2);
-                if (fullw || pxc + 4 * h < vw) {
-                    const float gv = fmaf(yv[r], sc, sh) > 0.f ? acc[mt][r] : 0.f;
-                    const float xh = (yv[r] - mu) * is;
-                    sg += gv;
-                    sgx = fmaf(gv, xh, sgx);
-                    sx += xh;
+                for (int r = 0; r < 16; ++r) {
+                    const int pxc = min((r & 3) + 8 * (r >> 2), vw - 1 - 4 * h);
+                    yv[r] = a.bnb_y.f[yrow + (size_t)max(pxc, -4 * h) * a.Cout];
                 }
+                // this row's output stores issue while its y loads are in flight
+                store_rows(std::integral_constant<bool, false>{}, mt, mt + 1);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) part(mt, r, yv[r]);
             }
         }
         sg += __shfl_xor(sg, 32, 64);
@@ -729,19 +813,25 @@ __device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a,
 __device__ unsigned long long g_clk[8192];
 #endif
 #if defined(X6R_STAMP) || defined(X6W_STAMP)
-// diagnostic build only: median over workgroups of the loader waves' fraction of the
-// main loop spent in vm_wait (out[0..2], per phase) and at barriers (out[3..5])
+// diagnostic build only: median over workgroups (16-slot records) of the loader waves'
+// fraction of the main loop spent in vm_wait (out[0..2], per phase) and at barriers
+// (out[3..5]); the first compute wave's fraction at barriers (out[6]) and in the
+// per-item epilogue (out[7]); loop cycles per step of the compute wave (out[8])
 extern "C" int ugpg_debug_stamps(double* out) {
     static unsigned long long h[8192];
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_clk), sizeof(h)) != hipSuccess) return -1;
-    static double f[6][1024];
+    static double f[9][512];
     int n = 0;
-    for (int i = 0; i < 1024; ++i)
-        if (h[8 * i] > 0) {
-            for (int q = 0; q < 6; ++q) f[q][n] = (double)h[8 * i + 1 + q] / h[8 * i];
+    for (int i = 0; i < 512; ++i)
+        if (h[16 * i] > 0) {
+            const unsigned long long* r = h + 16 * i;
+            for (int q = 0; q < 6; ++q) f[q][n] = (double)r[1 + q] / r[0];
+            f[6][n] = r[8] ? (double)r[9] / r[8] : 0.0;
+            f[7][n] = r[8] ? (double)r[10] / r[8] : 0.0;
+            f[8][n] = r[11] ? (double)r[8] / r[11] : 0.0;
             ++n;
         }
-    for (int q = 0; q < 6; ++q) {
+    for (int q = 0; q < 9; ++q) {
         std::sort(f[q], f[q] + n);
         out[q] = n ? f[q][n / 2] : 0.0;
     }
@@ -767,10 +857,13 @@ extern "C" int ugpg_debug_clock(double* mhz) {
 // at bs16 (64 images' worth of 16 x 16 tiles x 8 column blocks = 128 items).  (Measured
 // and dropped: two compute waves per SIMD, 512-pixel single-piece items, column-block-major
 // item order.)
-template <int NP, bool M16, int TWT = 32, int THT = 256 / TWT>
+template <int NP, bool M16, int TWT = 32, int THT = 256 / TWT, bool XB16 = false>
 __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) {
     constexpr int NCW = 4;  // compute waves (one per SIMD) + 4 loader waves
     static_assert(!M16 || NP == 3, "the 16x16x32 form pairs the split-bf16 products");
+    // XB16: every source is stored in bf16 only (single-piece form): one 16-byte halo load
+    // per (pixel, 8 channels) instead of two
+    static_assert(!XB16 || NP == 1, "bf16 sources only in the single-piece form");
     static_assert(TWT == 32 || (M16 && TWT == 16), "16-wide tiles only in the 16x16x32 form");
     static_assert(THT * TWT == 256 || (M16 && THT * TWT == 128),
                   "256-pixel items; 128 in the 16x16x32 form");
@@ -813,6 +906,9 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
     constexpr bool CTAB = NP == 1;
     constexpr int CTAB_N = CTAB ? X6R_CTAB_MAX : 4;
     __shared__ __attribute__((aligned(16))) float ctab[2][CTAB_N];
+    // the 32x32-form epilogue's per-wave staging of bf16-only outputs (x6_epilogue_wave)
+    constexpr int OSTG_N = M16 ? 4 : NCW * X6_STG_WAVE;
+    __shared__ __attribute__((aligned(16))) float ostg[OSTG_N];
     u32x4* const Bring = smem + 2 * A_VECS;
     u32x4* const dummy = smem + 2 * A_VECS + NSLOT * R_STR;  // writes of idle lanes
 
@@ -854,36 +950,14 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
         const int lt = tid - NCW * 64;
         const int hhl = (lt >> 4) & 1;  // channel half of this lane (same for all its items)
         auto item_px = [](int idx) { return (idx >> 5) * 16 + (idx & 15); };
-        f32x4 ra[2][A_PER][2];
+        constexpr int LPV = XB16 ? 1 : 2;  // global loads per halo vector
+        f32x4 ra[2][A_PER][LPV];
         unsigned avalid[2] = {0u, 0u};
         Act4 r0[2], r1[2];
         float lo[2] = {0.f, 0.f};
         bool b16[2] = {false, false};
         // cursor over loader steps (clamped to the last one): chunk, item, column block
         // and tile position, advanced without divisions except at item changes
-        struct Cur {
-            int s, c, itm, nb;
-            Pos p;
-        };
-        auto cur_at = [&](int s) {
-            Cur q;
-            q.s = min(s, last);
-            q.c = q.s % nchunk;
-            q.itm = item0 + (q.s / nchunk) * nslots;
-            q.nb = q.itm % NB;
-            q.p = pos_of(q.itm);
-            return q;
-        };
-        auto advance = [&](Cur& q) {
-            if (q.s >= last) return;
-            ++q.s;
-            if (++q.c == nchunk) {
-                q.c = 0;
-                q.itm += nslots;
-                q.nb = q.itm % NB;
-                q.p = pos_of(q.itm);
-            }
-        };
         // per-lane halo pixel offsets (row, column within the halo) of the A_PER vectors
         int hy[A_PER], hx[A_PER];
 #pragma unroll
@@ -892,18 +966,58 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
             hy[v] = hp < NHALO ? hp / HWD : -(1 << 20);  // never inside the image
             hx[v] = hp % HWD;
         }
+        // the halo cursor also carries, per item, each vector's (clamped) image pixel
+        // index and whether it lies inside the image: a step then addresses its loads
+        // with one multiply-add per vector
+        struct Cur {
+            int s, c, itm, nb;
+            Pos p;
+            int pix[A_PER];
+            unsigned pok;
+        };
+        auto locate = [&](Cur& q) {
+            unsigned ok = 0;
+#pragma unroll
+            for (int v = 0; v < A_PER; ++v) {
+                const int gy = q.p.ty0 - 1 + hy[v], gx = q.p.tx0 - 1 + hx[v];
+                ok |= (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W ? 1u : 0u) << v;
+                const int cy = min(max(gy, 0), a.H - 1), cx = min(max(gx, 0), a.W - 1);
+                q.pix[v] = (q.p.b * a.H + cy) * a.W + cx;
+            }
+            q.pok = ok;
+        };
+        auto cur_at = [&](int s, bool halo) {
+            Cur q;
+            q.s = min(s, last);
+            q.c = q.s % nchunk;
+            q.itm = item0 + (q.s / nchunk) * nslots;
+            q.nb = q.itm % NB;
+            q.p = pos_of(q.itm);
+            if (halo) locate(q);
+            return q;
+        };
+        auto advance = [&](Cur& q, bool halo) {
+            if (q.s >= last) return;
+            ++q.s;
+            if (++q.c == nchunk) {
+                q.c = 0;
+                q.itm += nslots;
+                q.nb = q.itm % NB;
+                q.p = pos_of(q.itm);
+                if (halo) locate(q);
+            }
+        };
         auto load_halo = [&](const Cur& q, auto S, auto TABC) {
             constexpr int st = decltype(S)::value;
             constexpr bool TAB = decltype(TABC)::value;
             const int c = q.c;
-            const Pos& p = q.p;
             const int cb0 = c * BKC;
             const bool second = cb0 >= a.C0;
             const float* src = second ? a.src1 : a.src0;
             // single-piece form: a source's bf16 copy is read instead (half the bytes; the
             // second load repeats the first address, so the load count stays fixed)
             const __bf16* s16 = NP == 1 ? (second ? a.src1_16 : a.src0_16) : nullptr;
-            b16[st] = s16 != nullptr;
+            b16[st] = XB16 || s16 != nullptr;
             const float* sc = second ? a.sc1 : a.sc0;
             const float* sh = second ? a.sh1 : a.sh0;
             const int Cs = second ? a.C1 : a.C0;
@@ -927,30 +1041,29 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
                 r1[st].s = gld16(scp + cc + 4);
                 r1[st].h = gld16(shp + cc + 4);
             }
-            unsigned av = 0;
 #pragma unroll
             for (int v = 0; v < A_PER; ++v) {
-                const int gy = p.ty0 - 1 + hy[v], gx = p.tx0 - 1 + hx[v];
-                const bool ok = cok && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
-                const int cy = min(max(gy, 0), a.H - 1), cx = min(max(gx, 0), a.W - 1);
-                const size_t off = ((size_t)(p.b * a.H + cy) * a.W + cx) * Cs + cc;
-                const void* g0 = s16 ? static_cast<const void*>(s16 + off)
-                                     : static_cast<const void*>(src + off);
-                const void* g1 = s16 ? g0 : static_cast<const void*>(src + off + 4);
-                ra[st][v][0] = gld16(g0);
-                ra[st][v][1] = gld16(g1);
-                av |= (ok ? 1u : 0u) << v;
+                const size_t off = (size_t)q.pix[v] * Cs + cc;
+                if constexpr (XB16) {
+                    ra[st][v][0] = gld16(s16 + off);
+                } else {
+                    const void* g0 = s16 ? static_cast<const void*>(s16 + off)
+                                         : static_cast<const void*>(src + off);
+                    const void* g1 = s16 ? g0 : static_cast<const void*>(src + off + 4);
+                    ra[st][v][0] = gld16(g0);
+                    ra[st][v][LPV - 1] = gld16(g1);
+                }
             }
-            avalid[st] = av;
+            avalid[st] = cok ? q.pok : 0u;
         };
-        constexpr int HALO_LOADS = (CTAB ? 0 : 4) + 2 * A_PER;  // global loads per loop halo
+        constexpr int HALO_LOADS = (CTAB ? 0 : 4) + LPV * A_PER;  // global loads per loop halo
         auto store_halo = [&](int k, auto S, int v0, int v1) {
             constexpr int st = decltype(S)::value;
             u32x4* As = smem + (k & 1) * A_VECS;
 #pragma unroll
             for (int v = v0; v < v1; ++v) {
                 const int hp = item_px(lt + v * 256), hh = hhl;
-                f32x4 raw0 = ra[st][v][0], raw1 = ra[st][v][1];
+                f32x4 raw0 = ra[st][v][0], raw1 = ra[st][v][LPV - 1];
                 if (NP == 1 && b16[st]) {  // 8 bf16 in the first load: widen (exact)
                     const u32x4 w = __builtin_bit_cast(u32x4, raw0);
 #pragma unroll
@@ -964,11 +1077,19 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
                 const f32x4 lo4 = act_floor4(raw0, r0[st], lo[st]),
                             hi4 = act_floor4(raw1, r1[st], lo[st]);
                 const bool ok = (avalid[st] >> v) & 1u;
-                const f32x8 x = {ok ? lo4.x : 0.f, ok ? lo4.y : 0.f, ok ? lo4.z : 0.f,
-                                 ok ? lo4.w : 0.f, ok ? hi4.x : 0.f, ok ? hi4.y : 0.f,
-                                 ok ? hi4.z : 0.f, ok ? hi4.w : 0.f};
                 u32x4 pc[NP];
-                split_n<NP>(x, pc);
+                if constexpr (NP == 1) {
+                    // one piece: zero the four packed words instead of the eight floats
+                    const f32x8 x = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
+                    split_n<NP>(x, pc);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) pc[0][i] = ok ? pc[0][i] : 0u;
+                } else {
+                    const f32x8 x = {ok ? lo4.x : 0.f, ok ? lo4.y : 0.f, ok ? lo4.z : 0.f,
+                                     ok ? lo4.w : 0.f, ok ? hi4.x : 0.f, ok ? hi4.y : 0.f,
+                                     ok ? hi4.z : 0.f, ok ? hi4.w : 0.f};
+                    split_n<NP>(x, pc);
+                }
                 const int hl = hp < NHALO ? (hp / HWD) * HS + hp % HWD : NHALO;
 #pragma unroll
                 for (int q = 0; q < NP; ++q) As[(q * 2 + hh) * NHP + hl] = pc[q];
@@ -1009,7 +1130,7 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
             }
         }
         {
-            const Cur q0 = cur_at(0);
+            const Cur q0 = cur_at(0, true);
             load_halo(q0, Set0{}, TabOff{});
             vm_wait<0>();
             store_halo(0, Set0{}, 0, A_PER);
@@ -1017,17 +1138,17 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
             dma_row(q0, 1, 1);
             dma_row(q0, 2, 2);
             if constexpr (LA == 6) {
-                const Cur q1 = cur_at(1);
+                const Cur q1 = cur_at(1, false);
                 dma_row(q1, 0, 3);
                 dma_row(q1, 1, 4);
                 dma_row(q1, 2, 5);
             }
-            load_halo(cur_at(1), Set1{}, TabOff{});
-            load_halo(cur_at(2), Set0{}, TabOff{});
+            load_halo(cur_at(1, true), Set1{}, TabOff{});
+            load_halo(cur_at(2, true), Set0{}, TabOff{});
             vm_wait<0>();
         }
         lds_barrier();
-        Cur cw = cur_at(LA / 3), ch = cur_at(3);  // weight rows of step k+LA/3, halo of step k+3
+        Cur cw = cur_at(LA / 3, false), ch = cur_at(3, true);  // weight rows of step k+LA/3, halo of step k+3
         int sl = LA % NSLOT;                      // ring slot of row 3k+LA
         // Phase ph of step k DMAs row j = 3(k+1)+ph into the slot of row j-4 (read in
         // the phase before, whose MFMAs consumed it before that phase's barrier) and
@@ -1091,8 +1212,8 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
             // phase 2
             dma_row(cw, 2, (sl + 2) % NSLOT);
             load_halo(ch, S, TabOn{});
-            advance(cw);
-            advance(ch);
+            advance(cw, false);
+            advance(ch, true);
             sl = (sl + 3) % NSLOT;
             if constexpr (LA == 3) {
                 ST_WAIT(st_vm[2], vm_wait<R + H>());  // row j+1
@@ -1112,16 +1233,37 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
         vm_wait<0>();  // no load outlives the workgroup (nothing may run before this wait:
                        // the last loads' destination registers are dead to the compiler)
 #ifdef X6R_STAMP
-        if (tid == NCW * 64 && blockIdx.x < 1024) {
-            g_clk[8 * blockIdx.x] = __builtin_amdgcn_s_memtime() - st_t0;
+        if (tid == NCW * 64 && blockIdx.x < 512) {
+            g_clk[16 * blockIdx.x] = __builtin_amdgcn_s_memtime() - st_t0;
             for (int q = 0; q < 3; ++q) {
-                g_clk[8 * blockIdx.x + 1 + q] = st_vm[q];
-                g_clk[8 * blockIdx.x + 4 + q] = st_bar[q];
+                g_clk[16 * blockIdx.x + 1 + q] = st_vm[q];
+                g_clk[16 * blockIdx.x + 4 + q] = st_bar[q];
             }
         }
 #endif
         return;
     }
+#ifdef X6R_STAMP
+    // diagnostic build: the compute waves' cycles at barriers and in the epilogue
+    unsigned long long cs_bar = 0, cs_epi = 0;
+    const unsigned long long cs_t0 = __builtin_amdgcn_s_memtime();
+#define CS_WAIT(acc, stmt)                                          \
+    {                                                               \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+        stmt;                                                       \
+        acc += __builtin_amdgcn_s_memtime() - t_;                   \
+    }
+#define CS_STORE()                                                          \
+    if (tid == 0 && blockIdx.x < 512) {                                     \
+        g_clk[16 * blockIdx.x + 8] = __builtin_amdgcn_s_memtime() - cs_t0; \
+        g_clk[16 * blockIdx.x + 9] = cs_bar;                                \
+        g_clk[16 * blockIdx.x + 10] = cs_epi;                               \
+        g_clk[16 * blockIdx.x + 11] = total;                                \
+    }
+#else
+#define CS_WAIT(acc, stmt) stmt
+#define CS_STORE()
+#endif
 
     // ---------------------------------------------------------------- compute waves
     const int wm = wave >> 1, wn = wave & 1;
@@ -1218,11 +1360,11 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 }
-                if (t % 3 == 2) read_barrier();
+                if (t % 3 == 2) CS_WAIT(cs_bar, read_barrier());
             }
             if (++cc == nchunk) {
-                x6q_epilogue_wave<TH, TW, NWM>(a, acc, cp.tile, cp.b, cp.ty0, cp.tx0, cp.nb * BN, wm,
-                                               wn);
+                CS_WAIT(cs_epi, (x6q_epilogue_wave<TH, TW, NWM>(a, acc, cp.tile, cp.b, cp.ty0, cp.tx0,
+                                                                cp.nb * BN, wm, wn)));
                 cc = 0;
                 item += nslots;
                 if (item < iend) cp = pos_of(item);
@@ -1238,6 +1380,7 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
             g_clk[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - clk_r0;
         }
 #endif
+        CS_STORE();
         return;
     } else {
     f32x16 acc[MT];
@@ -1281,6 +1424,11 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
     for (int k = 0; k < total; ++k) {
         const u32x4* Ac = smem + (k & 1) * A_VECS;
         if constexpr (NP == 1) {
+            // the item's last step: its BatchNorm-backward y tile (bf16) goes to the staging
+            // area now, so the epilogue finds it landed
+            if (cc == nchunk - 1 && a.bnb_part && a.bnb_y.h)
+                x6_dma_bnb_y<TH, TW, MT>(a, cp.b, cp.ty0, cp.tx0, cp.nb * BN, wm, wn,
+                                         ostg + wave * X6_STG_WAVE);
             // single piece: 4 MFMAs per tap cannot cover the next tap's fragment reads, so
             // the reads run two taps ahead, across the step boundary (the next step's first
             // two taps are read in phase 2: halo(k+1) and row 3k+3 are visible from there)
@@ -1300,7 +1448,7 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
                     }
                 }
                 __builtin_amdgcn_sched_barrier(0);
-                if (t % 3 == 2) read_barrier();
+                if (t % 3 == 2) CS_WAIT(cs_bar, read_barrier());
             }
         } else {
         u32x4 fa[2][MT][NP], fb[2][NP];
@@ -1326,11 +1474,13 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
                 }
             }
             __builtin_amdgcn_sched_barrier(0);  // taps do not mix
-            if (t % 3 == 2) read_barrier();
+            if (t % 3 == 2) CS_WAIT(cs_bar, read_barrier());
         }
         }
         if (++cc == nchunk) {
-            x6_epilogue_wave<TH, TW, MT>(a, acc, cp.tile, cp.b, cp.ty0, cp.tx0, cp.nb * BN, wm, wn);
+            CS_WAIT(cs_epi, (x6_epilogue_wave<TH, TW, MT>(a, acc, cp.tile, cp.b, cp.ty0, cp.tx0,
+                                                          cp.nb * BN, wm, wn,
+                                                          ostg + wave * X6_STG_WAVE)));
             cc = 0;
             item += nslots;
             if (item < iend) cp = pos_of(item);
@@ -1346,7 +1496,10 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
         g_clk[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - clk_r0;
     }
 #endif
+    CS_STORE();
     }
+#undef CS_WAIT
+#undef CS_STORE
 }
 // ---------------------------------------------------------------------------
 // Split-bf16 weight gradient: dW[co][ci][t] = sum_p dy[p][co] * act(x)[p+t][ci].
@@ -1643,10 +1796,10 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
         vm_wait<0>();  // no load outlives the workgroup (nothing may run before this wait:
                        // the last loads' destination registers are dead to the compiler)
 #ifdef X6W_STAMP
-        if (tid == 256 && blockIdx.x < 1024) {
-            g_clk[8 * blockIdx.x] = __builtin_amdgcn_s_memtime() - st_t0;
-            g_clk[8 * blockIdx.x + 1] = st_vm;
-            g_clk[8 * blockIdx.x + 4] = st_bar;
+        if (tid == 256 && blockIdx.x < 512) {
+            g_clk[16 * blockIdx.x] = __builtin_amdgcn_s_memtime() - st_t0;
+            g_clk[16 * blockIdx.x + 1] = st_vm;
+            g_clk[16 * blockIdx.x + 4] = st_bar;
         }
 #endif
         return;
@@ -2205,6 +2358,9 @@ int launch_fwd_x6(const ConvFwdArgs& a, int np, hipStream_t st) {
         else if (np == 3)
             hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<3, true>), dim3((unsigned)g), dim3(512), 0,
                                st, a);
+        else if (!a.src0 && a.src0_16 && (a.C1 == 0 || (!a.src1 && a.src1_16)))
+            hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 8, true>), dim3((unsigned)g),
+                               dim3(512), 0, st, a);
         else
             hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false>), dim3((unsigned)g), dim3(512), 0,
                                st, a);

@@ -11,7 +11,6 @@ host once per batch instead of the reference's six ``.item()``/``.cpu()`` calls.
 from __future__ import annotations
 
 import json
-import os
 import time
 from pathlib import Path
 
@@ -133,56 +132,15 @@ class UncertaintyGuidedProgressiveTrainer:
         print(f"Weight transfer completed for stage {new_stage}")
 
     # ------------------------------------------------------------ hot path
-    # Run the previous stage's U-map forward on a second HIP stream, concurrently with the
-    # current stage's forward (the two are independent until the loss).  Results are
-    # bit-identical to the one-stream order (tests/test_gpu_models.py); see _umap_on_side.
-    umap_side_stream = os.environ.get("UGPG_UMAP_STREAM", "1") != "0"
-
-    def _umap_on_side(self, data, stage):
-        """Enqueue the U map on the side stream.  Ordering and allocator rules (each one a
-        way to get a U map that silently differs between runs):
-          1. side waits for the current stream: `data` (resized / copied on the current
-             stream) is complete before the previous-stage model reads it;
-          2. data.record_stream(side): its block is not handed to a new current-stream
-             allocation while the side stream may still read it;
-          3. the caller makes the current stream wait for side before the loss reads U,
-             and U.record_stream(current): U's block (side-stream pool) is not recycled
-             by a later side-stream allocation while its current-stream readers (loss
-             forward/backward, metrics) are pending.
-        Every intermediate of the previous-stage forward is allocated, used and freed on
-        the side stream only; its persistent state (flat parameters, weight packs, eval
-        BatchNorm coefficients) is built on the current stream first (prepare_eval), so
-        nothing long-lived is allocated from the side stream's pool."""
-        cur = torch.cuda.current_stream(data.device)
-        prev = self.models[stage - 1]
-        prev.eval()
-        prev.prepare_eval()
-        side = self.__dict__.get("_side")
-        if side is None or side.device != data.device:
-            side = self._side = torch.cuda.Stream(device=data.device)
-        side.wait_stream(cur)
-        with torch.cuda.stream(side):
-            umap = self.uncertainty_loss.generate_uncertainty_map(
-                data, self.models[stage - 1], self.stage_configs[stage - 1]["resolution"],
-                self.stage_configs[stage]["resolution"])
-        data.record_stream(side)
-        return umap, cur, side
-
     def _forward_device(self, data, target, stage, mbuf):
         """Forward + uncertainty map + weighted loss; results stay on the device.
         mbuf: 8-float device buffer [final, base, dice, acc, wrong, u_mean, u_std, 0]."""
         umap = None
-        if stage > 1 and self.umap_side_stream and data.is_cuda:
-            umap, cur, side = self._umap_on_side(data, stage)
-            output = self.current_model(data)
-            cur.wait_stream(side)
-            umap.record_stream(cur)
-        else:
-            output = self.current_model(data)
-            if stage > 1:
-                umap = self.uncertainty_loss.generate_uncertainty_map(
-                    data, self.models[stage - 1], self.stage_configs[stage - 1]["resolution"],
-                    self.stage_configs[stage]["resolution"])
+        output = self.current_model(data)
+        if stage > 1:
+            umap = self.uncertainty_loss.generate_uncertainty_map(
+                data, self.models[stage - 1], self.stage_configs[stage - 1]["resolution"],
+                self.stage_configs[stage]["resolution"])
         final, base = weighted_loss_tensors(self.base_criterion, output, target, umap,
                                             self.uncertainty_alpha,
                                             out=mbuf[0:2] if mbuf is not None else None)
