@@ -151,7 +151,9 @@ int ugpg_pack_conv3x3_batch(const ugpg_pack_item_t* items, int n, int wfmt, void
 typedef struct {
     int B, H, W;
     ugpg_src_t src[2];
-    const float* dy;       /* NHWC [B][H][W][Cout] */
+    const float* dy;       /* NHWC [B][H][W][Cout] ... */
+    const void* dy_bf16;   /* ... or stored in bf16 (dy == NULL: math UGPG_WFMT_BF16 with
+                              64-channel sources and no db; what the bf16 arithmetic reads) */
     int Cout;
     float* dw;
     int Cin_real;
@@ -203,22 +205,28 @@ typedef struct {
 } ugpg_bnb_t;
 int ugpg_bnb_slots(int64_t npix, int C);
 /* (y: the BN input in fp32, or y == NULL and y_bf16 its bf16 storage) */
+/* dy: fp32, or dy == NULL and dy_bf16 receives it rounded to bf16 (nearest even) -- under
+ * the bf16 arithmetic exactly the operand its data and weight gradients read (one of the
+ * two, never both) */
 int ugpg_bn_relu_bwd_partials(const float* part, int nslots, const float* da, const float* y,
                               const void* y_bf16, int64_t npix, int C, const float* mean,
                               const float* invstd, const float* scale, const float* shift,
-                              float* dy, float* dgamma, float* dbeta, float* dconv_bias,
-                              int accumulate_params, void* ws, size_t ws_bytes, void* stream);
+                              float* dy, void* dy_bf16, float* dgamma, float* dbeta,
+                              float* dconv_bias, int accumulate_params, void* ws, size_t ws_bytes,
+                              void* stream);
 int ugpg_bn_relu_bwd(const float* da, const float* y, const void* y_bf16, int64_t npix, int C,
                      const float* mean, const float* invstd, const float* scale,
-                     const float* shift, float* dy, float* dgamma, float* dbeta,
+                     const float* shift, float* dy, void* dy_bf16, float* dgamma, float* dbeta,
                      float* dconv_bias, int accumulate_params, void* ws, size_t ws_bytes,
                      void* stream);
 /* Materialise relu(scale*y+shift) (used only for the standalone block API). */
 int ugpg_bn_relu_apply(ugpg_src_t src, int64_t npix, float* out, void* stream);
 
 /* ---- MaxPool2d(2) (UG_unet_parts.py:49, K8) on an activated source -------- */
-int ugpg_maxpool2_fwd(ugpg_src_t src, int B, int H, int W, float* out, uint8_t* argmax,
-                      void* stream);
+/* out: fp32, or out == NULL and out_bf16 receives it rounded to bf16 (nearest even): the
+ * next conv's bf16 operand exactly (the bf16 arithmetic's storage) */
+int ugpg_maxpool2_fwd(ugpg_src_t src, int B, int H, int W, float* out, void* out_bf16,
+                      uint8_t* argmax, void* stream);
 int ugpg_maxpool2_bwd(const float* dout, const uint8_t* argmax, int B, int H, int W, int C,
                       float* din, int accumulate, void* stream);
 /* The same, also writing the BatchNorm-backward partials of din (see ugpg_bnb_t). */

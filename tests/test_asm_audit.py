@@ -21,9 +21,11 @@ KERNELS = [
     "_ZN4ugpg22conv3x3_fwd_x6r_kernelILi3ELb1ELi16ELi8ELb0EEEvNS_11ConvFwdArgsE",
     "_ZN4ugpg22conv3x3_fwd_x6r_kernelILi1ELb0ELi32ELi8ELb0EEEvNS_11ConvFwdArgsE",
     "_ZN4ugpg22conv3x3_fwd_x6r_kernelILi1ELb0ELi32ELi8ELb1EEEvNS_11ConvFwdArgsE",
-    "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi3ELb0EEEvNS_9WgradArgsE",
-    "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi1ELb0EEEvNS_9WgradArgsE",
-    "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi1ELb1EEEvNS_9WgradArgsE",
+    "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi3ELi0EEEvNS_9WgradArgsE",
+    "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi1ELi0EEEvNS_9WgradArgsE",
+    "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi1ELi1EEEvNS_9WgradArgsE",
+    "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi1ELi2EEEvNS_9WgradArgsE",
+    "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi1ELi3EEEvNS_9WgradArgsE",
 ]
 
 

@@ -530,6 +530,35 @@ def test_bf16_stored_bn_input(dev, math):
                     ops.conv3x3_wgrad(srcs, dyw, dw, None, C * (2 if two else 1))
                     ws_.append(dw)
                 eq(ws_[0], ws_[1], f"bf16 wgrad of bf16-stored sources (two={two})")
+            # dy stored in bf16 by the BatchNorm backward (standalone and from partials):
+            # the round-to-nearest-even of the fp32 dy; the weight gradient (fp32 or bf16
+            # sources) and the data gradient reading it give exactly the fp32-dy results
+            dy32 = torch.empty(B, H, W, C, device=dev)
+            ops.bn_relu_bwd(parts[0][0], y16, *st, dy32, *(torch.empty(C, device=dev)
+                                                           for _ in range(3)))
+            for use_part in (False, True):
+                dy16 = torch.empty(B, H, W, C, device=dev, dtype=torch.bfloat16)
+                ops.bn_relu_bwd(parts[0][0], y16, *st, dy16,
+                                *(torch.empty(C, device=dev) for _ in range(3)),
+                                part=parts[0][1] if use_part else None)
+                eq(dy16, dy32.to(torch.bfloat16), f"bf16 dy (partials={use_part})")
+            for t in (y, y16):
+                w2 = []
+                for d in (dy32, dy16):
+                    dw = torch.empty(C, C, 3, 3, device=dev)
+                    ops.conv3x3_wgrad([ops.Act(t, sc, sh)], d, dw, None, C)
+                    w2.append(dw)
+                eq(w2[0], w2[1], f"bf16 wgrad of a bf16-stored dy (x {t.dtype})")
+            d2 = []
+            for d in (dy32, dy16):
+                da = torch.empty(B, H, W, C, device=dev)
+                ops.conv3x3_fwd([ops.Act(d)], wpk, None, C, [da])
+                d2.append(da)
+            eq(d2[0], d2[1], "bf16 dgrad of a bf16-stored dy")
+            # max-pool output stored in bf16: the rounded fp32 output, same argmax
+            p16b, am16b = ops.maxpool2_fwd(ops.Act(y16, sc, sh), bf16=True)
+            eq(p16b, p32.to(torch.bfloat16), "maxpool fwd bf16 output")
+            eq(am16b, am32, "maxpool argmax (bf16 output)")
         # avgpool (Herlev)
         eq(ops.avgpool_fwd(ops.Act(y, sc, sh)), ops.avgpool_fwd(ops.Act(y16, sc, sh)), "avgpool")
     finally:

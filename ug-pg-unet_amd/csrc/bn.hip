@@ -232,12 +232,14 @@ __global__ void bn_bwd_finalize_kernel(const float* part, int nblk, int C, int64
 // keeps one 4-channel group: its per-channel coefficients are loaded once, and four
 // float4 pairs are in flight per thread.
 // TY: the storage of y (float, or __bf16 under the bf16 arithmetic)
-template <bool NT, typename TY>
+// TO: the storage of dy (float, or __bf16 = RNE of the same fp32 value: under the bf16
+// arithmetic exactly what the data and weight gradients read)
+template <bool NT, typename TY, typename TO>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const float* da, const TY* __restrict__ y,
                                                            int64_t npix, int C, const float* mean,
                                                            const float* invstd, const float* scale,
                                                            const float* shift, const float* coef,
-                                                           float* dy) {
+                                                           TO* dy) {
     const int64_t n4 = npix * C / 4;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -257,7 +259,17 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const float* da, cons
         return o;
     };
     const f32x4* D = reinterpret_cast<const f32x4*>(da);
-    f32x4* O = reinterpret_cast<f32x4*>(dy);
+    auto store = [&](int64_t k, f32x4 o) {
+        if constexpr (std::is_same<TO, float>::value) {
+            reinterpret_cast<f32x4*>(dy)[k] = o;
+        } else {
+            typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+            typedef float f32x2_t __attribute__((ext_vector_type(2)));
+            const unsigned lo = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2_t{o.x, o.y}, bf16x2_t));
+            const unsigned hi = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2_t{o.z, o.w}, bf16x2_t));
+            reinterpret_cast<uint2*>(dy)[k] = uint2{lo, hi};
+        }
+    };
     auto Y = [&](int64_t k) {  // 4 values of y (a 16- or 8-byte vector)
         if constexpr (std::is_same<TY, float>::value) {
             const f32x4* q = reinterpret_cast<const f32x4*>(y) + k;
@@ -281,9 +293,9 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const float* da, cons
             v[u] = Y(i + u * stride);
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) O[i + u * stride] = one(d[u], v[u]);
+        for (int u = 0; u < 4; ++u) store(i + u * stride, one(d[u], v[u]));
     }
-    for (; i < n4; i += stride) O[i] = one(D[i], Y(i));
+    for (; i < n4; i += stride) store(i, one(D[i], Y(i)));
 }
 
 __global__ void bn_relu_apply_kernel(YRef x, const float* sc, const float* sh,
@@ -310,13 +322,19 @@ static unsigned apply_grid(int64_t n4) {
 // read next by the data and weight gradients, stays in the caches (step -0.55 %)
 void launch_bn_apply(unsigned ga, hipStream_t st, const float* da, YRef y, int64_t npix,
                      int C, const float* mean, const float* invstd, const float* scale,
-                     const float* shift, const float* coef, float* dy) {
-    if (y.f)
-        hipLaunchKernelGGL((bn_bwd_apply_kernel<true, float>), dim3(ga), dim3(256), 0, st, da, y.f,
-                           npix, C, mean, invstd, scale, shift, coef, dy);
+                     const float* shift, const float* coef, float* dy, __bf16* dy16) {
+    if (y.f && dy)
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<true, float, float>), dim3(ga), dim3(256), 0, st,
+                           da, y.f, npix, C, mean, invstd, scale, shift, coef, dy);
+    else if (y.f)
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<true, float, __bf16>), dim3(ga), dim3(256), 0, st,
+                           da, y.f, npix, C, mean, invstd, scale, shift, coef, dy16);
+    else if (dy)
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<true, __bf16, float>), dim3(ga), dim3(256), 0, st,
+                           da, y.h, npix, C, mean, invstd, scale, shift, coef, dy);
     else
-        hipLaunchKernelGGL((bn_bwd_apply_kernel<true, __bf16>), dim3(ga), dim3(256), 0, st, da,
-                           y.h, npix, C, mean, invstd, scale, shift, coef, dy);
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<true, __bf16, __bf16>), dim3(ga), dim3(256), 0, st,
+                           da, y.h, npix, C, mean, invstd, scale, shift, coef, dy16);
 }
 constexpr int64_t kBwdBlocks = 2048, kBwdPpt = 8;
 namespace {
@@ -381,12 +399,12 @@ extern "C" size_t ugpg_bn_relu_bwd_workspace(int64_t npix, int C) {
 
 extern "C" int ugpg_bn_relu_bwd(const float* da, const float* y_f32, const void* y_bf16,
                                 int64_t npix, int C, const float* mean, const float* invstd,
-                                const float* scale, const float* shift, float* dy, float* dgamma,
-                                float* dbeta, float* dbias, int acc, void* ws, size_t ws_bytes,
-                                void* stream) {
+                                const float* scale, const float* shift, float* dy, void* dy_bf16,
+                                float* dgamma, float* dbeta, float* dbias, int acc, void* ws,
+                                size_t ws_bytes, void* stream) {
     const YRef y = yref(y_f32, y_bf16);
-    if (!da || (!y.f && !y.h) || !dy || !mean || !invstd || !scale || !shift || C % 4 || C > 1024 ||
-        npix <= 0) {
+    if (!da || (!y.f && !y.h) || !dy == !dy_bf16 || !mean || !invstd || !scale || !shift ||
+        C % 4 || C > 1024 || npix <= 0) {
         set_error("bn_relu_bwd: bad arguments (C=%d)", C);
         return UGPG_ERR_INVALID;
     }
@@ -408,7 +426,8 @@ extern "C" int ugpg_bn_relu_bwd(const float* da, const float* y_f32, const void*
     // the apply kernel keeps one channel group per thread: grid * 1024 must be a multiple of C
     const unsigned q = (unsigned)(C / std::gcd(1024, C));
     const unsigned ga = (apply_grid(npix * C / 4) + q - 1) / q * q;
-    launch_bn_apply(ga, st, da, y, npix, C, mean, invstd, scale, shift, coef, dy);
+    launch_bn_apply(ga, st, da, y, npix, C, mean, invstd, scale, shift, coef, dy,
+                    static_cast<__bf16*>(dy_bf16));
     return check_launch("bn_bwd_apply");
 }
 
@@ -437,11 +456,11 @@ extern "C" int ugpg_bn_relu_bwd_partials(const float* part, int nslots, const fl
                                          const float* y_f32, const void* y_bf16, int64_t npix,
                                          int C, const float* mean, const float* invstd,
                                          const float* scale, const float* shift, float* dy,
-                                         float* dgamma, float* dbeta, float* dbias, int acc,
-                                         void* ws, size_t ws_bytes, void* stream) {
+                                         void* dy_bf16, float* dgamma, float* dbeta, float* dbias,
+                                         int acc, void* ws, size_t ws_bytes, void* stream) {
     const YRef y = yref(y_f32, y_bf16);
-    if (!part || nslots <= 0 || !da || (!y.f && !y.h) || !dy || !mean || !invstd || !scale || !shift ||
-        C % 4 || C <= 0 || C > 1024 || npix <= 0) {
+    if (!part || nslots <= 0 || !da || (!y.f && !y.h) || !dy == !dy_bf16 || !mean || !invstd ||
+        !scale || !shift || C % 4 || C <= 0 || C > 1024 || npix <= 0) {
         set_error("bn_relu_bwd_partials: bad arguments (C=%d nslots=%d)", C, nslots);
         return UGPG_ERR_INVALID;
     }
@@ -457,7 +476,8 @@ extern "C" int ugpg_bn_relu_bwd_partials(const float* part, int nslots, const fl
     if (int e = check_launch("bn_bwd_finalize")) return e;
     const unsigned q = (unsigned)(C / std::gcd(1024, C));
     const unsigned ga = (apply_grid(npix * C / 4) + q - 1) / q * q;
-    launch_bn_apply(ga, st, da, y, npix, C, mean, invstd, scale, shift, coef, dy);
+    launch_bn_apply(ga, st, da, y, npix, C, mean, invstd, scale, shift, coef, dy,
+                    static_cast<__bf16*>(dy_bf16));
     return check_launch("bn_bwd_apply");
 }
 

@@ -1023,11 +1023,16 @@ static int wgrad_c1(const ugpg_wgrad_t* p) {
 static bool wgrad_b16(const ugpg_wgrad_t* p) { return !p->src[0].data; }
 
 static int wgrad_check(const ugpg_wgrad_t* p) {
-    if (!p || (!p->src[0].data && !p->src[0].data_bf16) || !p->dy || !p->dw) {
+    if (!p || (!p->src[0].data && !p->src[0].data_bf16) || (!p->dy && !p->dy_bf16) || !p->dw) {
         set_error("conv3x3_wgrad: null argument");
         return UGPG_ERR_INVALID;
     }
     const int C0 = p->src[0].C, C1 = wgrad_c1(p);
+    if (!p->dy && (p->math != UGPG_WFMT_BF16 || p->db || C0 % 64 || C1 % 64)) {
+        set_error("conv3x3_wgrad: a bf16-stored dy needs the bf16 arithmetic, 64-channel "
+                  "sources and no bias gradient");
+        return UGPG_ERR_INVALID;
+    }
     if (wgrad_b16(p) != (C1 && !p->src[1].data) && C1) {
         set_error("conv3x3_wgrad: both sources must be stored alike (fp32 or bf16)");
         return UGPG_ERR_INVALID;
@@ -1110,6 +1115,7 @@ extern "C" int ugpg_conv3x3_wgrad(const ugpg_wgrad_t* p, void* ws, size_t ws_byt
     a.src0_16 = static_cast<const __bf16*>(p->src[0].data_bf16);
     a.src1_16 = static_cast<const __bf16*>(p->src[1].data_bf16);
     a.dy = p->dy;
+    a.dy16 = p->dy ? nullptr : static_cast<const __bf16*>(p->dy_bf16);
     a.Cout = p->Cout;
     a.Cin = Cin;
     a.part = static_cast<float*>(ws);

@@ -167,6 +167,8 @@ struct WgradArgs {
     // bf16 activation storage (src0/src1 == nullptr; the x6w single-piece form only)
     const __bf16* src0_16;
     const __bf16* src1_16;
+    // dy stored in bf16 (dy == nullptr; the x6w single-piece form only)
+    const __bf16* dy16;
     int Cout, Cin;
     float* part;
     float* dbpart;

@@ -389,6 +389,20 @@ __device__ __forceinline__ void lds_barrier() {
 // the epilogue).  Instead each m-tile goes through the wave's LDS staging area `stg`
 // (32 pixels x 40 floats: the two pixel halves h land on opposite bank halves) and
 // leaves as 16-byte stores of 8 channels (2 per lane per m-tile).
+#ifdef X6R_STAMP
+// diagnostic build: cycles of the last epilogue of each workgroup's first compute wave in
+// its store phase and its statistics phase
+__device__ unsigned long long g_epi[512 * 4];
+#define EPI_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define EPI_REC(t0, t1)                                                       \
+    if (threadIdx.x == 0 && blockIdx.x < 512) {                               \
+        g_epi[4 * blockIdx.x] = t1 - t0;                                      \
+        g_epi[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memtime() - t1;        \
+    }
+#else
+#define EPI_T(v)
+#define EPI_REC(t0, t1)
+#endif
 constexpr int X6_STG_PITCH = 40;
 constexpr int X6_STG_WAVE = 2048;  // floats: 32 x 40 fp32, or the bf16 y tile of 4 m-tiles
 // BatchNorm-backward partials with bf16 y: the item's y tile (MT m-tiles x 32 pixels x the
@@ -508,9 +522,11 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
         }
     };
     const bool bnb = a.bnb_part != nullptr && !oacc;  // (the host refuses bnb + accumulate)
+    EPI_T(et0);
     if (oacc) store_rows(std::integral_constant<bool, true>{}, 0, MT);
     else if (only16 && !bnb) store16_rows();
     else if (!bnb) store_rows(std::integral_constant<bool, false>{}, 0, MT);
+    EPI_T(et1);
     if (bnb) {
         // BatchNorm-backward partials of the stored output (as x6q_epilogue_wave): this
         // lane's channel over its pixels, the two pixel halves (h) combined by a shuffle
@@ -594,6 +610,7 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
         a.stats[(1 * (size_t)a.Cout + n) * S + slot] = s;
         a.stats[(2 * (size_t)a.Cout + n) * S + slot] = q;
     }
+    EPI_REC(et0, et1);
 }
 
 // Epilogue of the 16x16x32 form: acc[mt][nt] is D[oc][px] of m-tile mt (16 pixels:
@@ -676,8 +693,10 @@ __device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a,
         }
     };
     const bool bnb = a.bnb_part != nullptr && !oacc;  // (the host refuses bnb + accumulate)
+    EPI_T(et0);
     if (oacc) store_tiles(std::integral_constant<bool, true>{}, 0, MTW);
     else if (!bnb) store_tiles(std::integral_constant<bool, false>{}, 0, MTW);
+    EPI_T(et1);
     if (bnb) {
         // BatchNorm-backward partials of the stored output da (the reduction of
         // ugpg_bn_relu_bwd, bn.hip bn_bwd_reduce_kernel, on the tile still in registers):
@@ -807,6 +826,7 @@ __device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a,
         a.stats[(1 * (size_t)a.Cout + n) * S + slot] = sv;
         a.stats[(2 * (size_t)a.Cout + n) * S + slot] = qv;
     }
+    EPI_REC(et0, et1);
 }
 
 #if defined(X6R_CLOCK) || defined(X6R_STAMP) || defined(X6W_STAMP)
@@ -816,11 +836,16 @@ __device__ unsigned long long g_clk[8192];
 // diagnostic build only: median over workgroups (16-slot records) of the loader waves'
 // fraction of the main loop spent in vm_wait (out[0..2], per phase) and at barriers
 // (out[3..5]); the first compute wave's fraction at barriers (out[6]) and in the
-// per-item epilogue (out[7]); loop cycles per step of the compute wave (out[8])
+// per-item epilogue (out[7]); loop cycles per step of the compute wave (out[8]); cycles of
+// the last epilogue's store phase (out[9]) and statistics phase (out[10])
 extern "C" int ugpg_debug_stamps(double* out) {
     static unsigned long long h[8192];
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_clk), sizeof(h)) != hipSuccess) return -1;
-    static double f[9][512];
+#ifdef X6R_STAMP
+    static unsigned long long he[512 * 4];
+    if (hipMemcpyFromSymbol(he, HIP_SYMBOL(g_epi), sizeof(he)) != hipSuccess) return -1;
+#endif
+    static double f[11][512];
     int n = 0;
     for (int i = 0; i < 512; ++i)
         if (h[16 * i] > 0) {
@@ -829,9 +854,15 @@ extern "C" int ugpg_debug_stamps(double* out) {
             f[6][n] = r[8] ? (double)r[9] / r[8] : 0.0;
             f[7][n] = r[8] ? (double)r[10] / r[8] : 0.0;
             f[8][n] = r[11] ? (double)r[8] / r[11] : 0.0;
+#ifdef X6R_STAMP
+            f[9][n] = (double)he[4 * i];
+            f[10][n] = (double)he[4 * i + 1];
+#else
+            f[9][n] = f[10][n] = 0.0;
+#endif
             ++n;
         }
-    for (int q = 0; q < 9; ++q) {
+    for (int q = 0; q < 11; ++q) {
         std::sort(f[q], f[q] + n);
         out[q] = n ? f[q][n / 2] : 0.0;
     }
@@ -1560,11 +1591,13 @@ template <int NP>
 constexpr int wrec() { return NP == 3 ? WX_REC : 192; }
 
 // (A paired 16x16x32 form, as the forward's, measured 2 % slower: 32x32x16 it is.)
-// XB16: the activation operand is stored in bf16 (a.src*_16; the bf16 arithmetic's storage,
-// NP = 1): 8-byte loads of 4 channels instead of 16-byte ones, same load count per step
-template <int TH, int TW, int NP, bool XB16 = false>
+// XB bit 1: the activation operand is stored in bf16 (a.src*_16), bit 2: dy is (a.dy16) --
+// the bf16 arithmetic's storage, NP = 1: 8-byte loads of 4 channels instead of 16-byte
+// ones, same load count per step
+template <int TH, int TW, int NP, int XB = 0>
 __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) {
-    static_assert(!XB16 || NP == 1, "bf16 activation storage: single-piece arithmetic");
+    constexpr bool XB16 = (XB & 1) != 0, DB16 = (XB & 2) != 0;
+    static_assert(XB == 0 || NP == 1, "bf16 storage: single-piece arithmetic");
     constexpr int REC = wrec<NP>();
     static_assert(TW == 16, "one 16-pixel row per MFMA k-step");
     constexpr int P = TH * TW, HWD = TW + 2, NHALO = (TH + 2) * HWD;
@@ -1616,7 +1649,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
     if (loader) {
         // ------------------------------------------------------------ loader waves
         const int lt = tid - 256;
-        f32x4 rdy[DY_PER];
+        typename std::conditional<DB16, u32x2v, f32x4>::type rdy[DY_PER];
         typename std::conditional<XB16, u32x2v, f32x4>::type rx[X_PER];
         Act4 xa;
         float xlo = 0.f;
@@ -1720,10 +1753,13 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
                     xvalid |= (ok ? 1u : 0u) << v;
                 }
             }
-            const float* dyb = a.dy + ((size_t)(b * a.H + ty0) * a.W + tx0) * a.Cout + co0 + q4;
+            const size_t dyo0 = ((size_t)(b * a.H + ty0) * a.W + tx0) * a.Cout + co0 + q4;
             const size_t xb = ((size_t)(b * a.H + ty0) * a.W + tx0) * Cs + cbase + q4;
 #pragma unroll
-            for (int v = 0; v < DY_PER; ++v) rdy[v] = gld16(dyb + dof[v]);
+            for (int v = 0; v < DY_PER; ++v) {
+                if constexpr (DB16) rdy[v] = gld8(a.dy16 + dyo0 + dof[v]);
+                else rdy[v] = gld16(a.dy + dyo0 + dof[v]);
+            }
 #pragma unroll
             for (int v = 0; v < X_PER; ++v) {
                 if constexpr (XB16) rx[v] = gld8(xsrc16 + xb + xof[v]);
@@ -1745,7 +1781,13 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
             for (int v = 0; v < DY_PER; ++v) {
                 const int idx = lt + v * 256;
                 const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-                put(dys + (idx >> 4) * REC, idx & 15, ((dvalid >> v) & 1u) ? rdy[v] : z);
+                f32x4 d;
+                if constexpr (DB16)  // 4 bf16 widened (exact)
+                    d = f32x4{__uint_as_float(rdy[v].x << 16), __uint_as_float(rdy[v].x & 0xffff0000u),
+                              __uint_as_float(rdy[v].y << 16), __uint_as_float(rdy[v].y & 0xffff0000u)};
+                else
+                    d = rdy[v];
+                put(dys + (idx >> 4) * REC, idx & 15, ((dvalid >> v) & 1u) ? d : z);
             }
 #pragma unroll
             for (int v = 0; v < X_PER; ++v) {
@@ -1916,8 +1958,15 @@ void launch_wgrad_x6(const WgradArgs& a, int np, hipStream_t st) {
     if (np == 3)
         hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW, 3>), dim3((unsigned)g),
                            dim3(512), 0, st, a);
-    else if (a.src0 == nullptr)  // bf16 activation storage (the host checked both sources)
-        hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW, 1, true>),
+    // bf16 storage of the activations (the host checked both sources alike) and of dy
+    else if (a.src0 == nullptr && a.dy == nullptr)
+        hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW, 1, 3>),
+                           dim3((unsigned)g), dim3(512), 0, st, a);
+    else if (a.dy == nullptr)
+        hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW, 1, 2>),
+                           dim3((unsigned)g), dim3(512), 0, st, a);
+    else if (a.src0 == nullptr)
+        hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW, 1, 1>),
                            dim3((unsigned)g), dim3(512), 0, st, a);
     else
         hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW, 1>), dim3((unsigned)g),

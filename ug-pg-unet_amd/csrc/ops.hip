@@ -19,7 +19,7 @@ namespace ugpg {
 
 template <bool NT>
 __global__ void maxpool2_fwd_kernel(YRef x, const float* sc, const float* sh, int B, int H,
-                                    int W, int C, float* out, uint8_t* am) {
+                                    int W, int C, float* out, __bf16* out16, uint8_t* am) {
     const int Ho = H / 2, Wo = W / 2, C4 = C / 4;
     const int64_t total = (int64_t)B * Ho * Wo * C4;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
@@ -55,7 +55,15 @@ __global__ void maxpool2_fwd_kernel(YRef x, const float* sc, const float* sh, in
                     }
             }
         }
-        *reinterpret_cast<f32x4*>(out + i * 4) = best;
+        if (out) {
+            *reinterpret_cast<f32x4*>(out + i * 4) = best;
+        } else {  // bf16 storage (RNE): the next conv's bf16 operand, exactly
+            typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+            typedef float f32x2_t __attribute__((ext_vector_type(2)));
+            const unsigned lo = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2_t{best.x, best.y}, bf16x2_t));
+            const unsigned hi = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2_t{best.z, best.w}, bf16x2_t));
+            *reinterpret_cast<uint2*>(out16 + i * 4) = uint2{lo, hi};
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) am[i * 4 + j] = idx[j];
     }
@@ -1338,13 +1346,15 @@ using namespace ugpg;
         }                                                \
     } while (0)
 
-extern "C" int ugpg_maxpool2_fwd(ugpg_src_t s, int B, int H, int W, float* out, uint8_t* am,
-                                 void* stream) {
-    UGPG_REQUIRE((s.data || s.data_bf16) && out && am && s.C % 4 == 0 && H >= 2 && W >= 2,
+extern "C" int ugpg_maxpool2_fwd(ugpg_src_t s, int B, int H, int W, float* out, void* out_bf16,
+                                 uint8_t* am, void* stream) {
+    UGPG_REQUIRE((s.data || s.data_bf16) && (out || out_bf16) && am && s.C % 4 == 0 && H >= 2 &&
+                     W >= 2,
                  "maxpool2_fwd");
     const int64_t total = (int64_t)B * (H / 2) * (W / 2) * (s.C / 4);
     hipLaunchKernelGGL(maxpool2_fwd_kernel<false>, dim3(stream_grid(total)), dim3(256), 0,
-                       as_stream(stream), yref(s), s.scale, s.shift, B, H, W, s.C, out, am);
+                       as_stream(stream), yref(s), s.scale, s.shift, B, H, W, s.C, out,
+                       static_cast<__bf16*>(out_bf16), am);
     return check_launch("maxpool2_fwd");
 }
 

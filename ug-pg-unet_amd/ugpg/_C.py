@@ -43,8 +43,8 @@ class PackItem(C.Structure):
 
 class WgradDesc(C.Structure):
     """ugpg_wgrad_t."""
-    _fields_ = [("B", _i), ("H", _i), ("W", _i), ("src", Src * 2), ("dy", _p), ("Cout", _i),
-                ("dw", _p), ("Cin_real", _i), ("db", _p), ("accumulate", _i), ("math", _i)]
+    _fields_ = [("B", _i), ("H", _i), ("W", _i), ("src", Src * 2), ("dy", _p), ("dy_bf16", _p),
+                ("Cout", _i), ("dw", _p), ("Cin_real", _i), ("db", _p), ("accumulate", _i), ("math", _i)]
 
 
 # name -> (restype, argtypes); must match include/ugpg.h exactly
@@ -61,13 +61,13 @@ SIGNATURES = {
     "ugpg_bn_finalize": (_i, [_p, _i, _i, _p, _p, _p, _p, _p, _f, _f, _p, _p, _p, _p, _p]),
     "ugpg_bn_eval_params": (_i, [_p, _p, _p, _p, _f, _i, _p, _p, _p]),
     "ugpg_bn_relu_bwd_workspace": (_sz, [_i64, _i]),
-    "ugpg_bn_relu_bwd": (_i, [_p, _p, _p, _i64, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i, _p, _sz,
-                              _p]),
+    "ugpg_bn_relu_bwd": (_i, [_p, _p, _p, _i64, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _p,
+                              _sz, _p]),
     "ugpg_bn_relu_bwd_partials_workspace": (_sz, [_i]),
     "ugpg_bn_relu_bwd_partials": (_i, [_p, _i, _p, _p, _p, _i64, _i, _p, _p, _p, _p, _p, _p, _p,
-                                       _p, _i, _p, _sz, _p]),
+                                       _p, _p, _i, _p, _sz, _p]),
     "ugpg_bn_relu_apply": (_i, [Src, _i64, _p, _p]),
-    "ugpg_maxpool2_fwd": (_i, [Src, _i, _i, _i, _p, _p, _p]),
+    "ugpg_maxpool2_fwd": (_i, [Src, _i, _i, _i, _p, _p, _p, _p]),
     "ugpg_maxpool2_bwd": (_i, [_p, _p, _i, _i, _i, _i, _p, _i, _p]),
     "ugpg_maxpool2_bwd_bnb": (_i, [_p, _p, _i, _i, _i, _i, _p, _i, C.POINTER(Bnb), _p]),
     "ugpg_bnb_slots": (_i, [_i64, _i]),

@@ -127,20 +127,26 @@ def double_conv_forward(mod, srcs, ctx: BlockCtx, save: bool):
     return cur[0]
 
 
-def _bn_relu_wgrad(conv, bn, y, st, in_srcs, dy, grads, part=None):
-    """In place: dy <- dL/d(conv output) from dL/d(relu(bn(y))); then dW, db.
-    part: BatchNorm-backward partials written by the data gradient that produced dy."""
+def _bn_relu_wgrad(conv, bn, y, st, in_srcs, da, grads, part=None):
+    """dy = dL/d(conv output) from da = dL/d(relu(bn(y))) -- in place, or, where the bf16
+    arithmetic stores the activations in bf16 (y is bf16), into a bf16 tensor: exactly the
+    operand its weight and data gradients read -- then dW, db.  Returns dy.
+    part: BatchNorm-backward partials written by the data gradient that produced da."""
     mean, invstd, scale, shift = st
     if mean is None:
         raise RuntimeError("backward through an eval-mode BatchNorm is not supported")
     # the conv bias gradient (sum of dy) comes out of the BN-backward reduction
     db = grads.get(conv.bias) if conv.bias is not None else None
-    ops.bn_relu_bwd(dy, y, mean, invstd, scale, shift, dy, grads.get(bn.weight),
+    dy = da
+    if y.dtype == torch.bfloat16 and all(s.C % 64 == 0 for s in in_srcs):
+        dy = ops.empty(*da.shape, like=da, dtype=torch.bfloat16)
+    ops.bn_relu_bwd(da, y, mean, invstd, scale, shift, dy, grads.get(bn.weight),
                     grads.get(bn.bias), db, part=part)
     dw = grads.get(conv.weight)
     if dw is not None:
         co, ci = conv.weight.shape[0], conv.weight.shape[1]
         ops.conv3x3_wgrad(in_srcs, dy, dw, None, ci, flops=2.0 * dy.numel() / co * co * 9 * ci)
+    return dy
 
 
 def double_conv_backward(mod, ctx: BlockCtx, da2, targets, acc_flags, grads, pad_out=None):
@@ -153,7 +159,7 @@ def double_conv_backward(mod, ctx: BlockCtx, da2, targets, acc_flags, grads, pad
     B, H, W, cout = ctx.y2.shape
     a1 = Act(ctx.y1, ctx.st1[2], ctx.st1[3])
     # stage 2: BN2/ReLU backward, wgrad(conv2), dgrad(conv2) -> dL/d(a1)
-    _bn_relu_wgrad(c2, b2, ctx.y2, ctx.st2, [a1], da2, grads, part=ctx.part2)
+    dy2 = _bn_relu_wgrad(c2, b2, ctx.y2, ctx.st2, [a1], da2, grads, part=ctx.part2)
     cmid = c2.weight.shape[1]
     da1 = ops.empty(B, H, W, cmid, like=da2)
     npix = B * H * W
@@ -167,25 +173,25 @@ def double_conv_backward(mod, ctx: BlockCtx, da2, targets, acc_flags, grads, pad
     if ctx.st1[0] is not None and _FUSE_BN_BWD and cout >= _FUSE_BN_BWD_MIN_K:
         part = ops.empty(3 * cmid * ops.conv_ntiles(B, H, W, cout, cmid, wpk2), like=da2)
         bnb = (ctx.y1, *ctx.st1, part)
-    ops.conv3x3_fwd([Act(da2)], wpk2, None, cmid, [da1], flops=2.0 * npix * cmid * 9 * cout,
+    ops.conv3x3_fwd([Act(dy2)], wpk2, None, cmid, [da1], flops=2.0 * npix * cmid * 9 * cout,
                     bnb=bnb)
     # stage 1: BN1/ReLU backward, wgrad(conv1), dgrad(conv1) -> source targets
-    _bn_relu_wgrad(c1, b1, ctx.y1, ctx.st1, ctx.srcs, da1, grads, part=part)
+    dy1 = _bn_relu_wgrad(c1, b1, ctx.y1, ctx.st1, ctx.srcs, da1, grads, part=part)
     if not any(t is not None for t in targets):
         return
     cin = c1.weight.shape[1]
     fl = 2.0 * npix * cin * 9 * cmid
     if pad_out is not None:
         wpk = ops.pack_conv3x3(c1.weight.detach(), pad_out, 1)
-        ops.conv3x3_fwd([Act(da1)], wpk, None, pad_out, [targets[0]], accumulate=(acc_flags[0], 0),
+        ops.conv3x3_fwd([Act(dy1)], wpk, None, pad_out, [targets[0]], accumulate=(acc_flags[0], 0),
                         flops=fl)
         return
     wpk = ops.pack_conv3x3(c1.weight.detach(), cin, 1)
     if len(targets) == 1:
-        ops.conv3x3_fwd([Act(da1)], wpk, None, cin, [targets[0]], accumulate=(acc_flags[0], 0),
+        ops.conv3x3_fwd([Act(dy1)], wpk, None, cin, [targets[0]], accumulate=(acc_flags[0], 0),
                         flops=fl)
     else:
-        ops.conv3x3_fwd([Act(da1)], wpk, None, cin, [targets[0], targets[1]],
+        ops.conv3x3_fwd([Act(dy1)], wpk, None, cin, [targets[0], targets[1]],
                         split=ctx.srcs[0].C, accumulate=(acc_flags[0], acc_flags[1]), flops=fl)
 
 
@@ -245,7 +251,7 @@ class UNetGraph:
                 srcs = [Act(x0)]
             elif blk.kind == "down":
                 a = outs[blk.inputs[0]]
-                p, am = ops.maxpool2_fwd(a)
+                p, am = ops.maxpool2_fwd(a, bf16=_store16(a.shape[2] // 2))
                 ctx.extra["argmax"] = am
                 ctx.extra["in_hw"] = a.shape[1:3]
                 srcs = [Act(p)]

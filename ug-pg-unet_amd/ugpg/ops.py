@@ -301,7 +301,8 @@ def conv3x3_wgrad(srcs, dy, dw, db, cin_real, accumulate=0, flops=None):
     d.B, d.H, d.W = B, H, W
     d.src[0] = srcs[0].src()
     d.src[1] = srcs[1].src() if len(srcs) > 1 else NULL_SRC
-    d.dy, d.Cout = ptr(dy), dy.shape[-1]
+    d.dy, d.dy_bf16 = _yargs(dy)  # dy fp32, or bf16 (the bf16 arithmetic's storage)
+    d.Cout = dy.shape[-1]
     d.dw, d.Cin_real, d.db, d.accumulate = ptr(dw), cin_real, ptr(db), int(accumulate)
     d.math = _MATH_FMT[_conv_math]
     nbytes = lib.ugpg_conv3x3_wgrad_workspace(C.byref(d))
@@ -352,28 +353,31 @@ def bn_eval_params(gamma, beta, rm, rv, eps, owner=None):
 def bn_relu_bwd(da, y, mean, invstd, scale, shift, dy, dgamma, dbeta, dconv_bias=None,
                 accumulate=0, part=None):
     """part: partials the data gradient producing `da` wrote (conv3x3_fwd(bnb=...)):
-    only the finalize and apply passes run."""
+    only the finalize and apply passes run.  dy: fp32, or a bf16 tensor receiving dy
+    rounded to bf16 (what the bf16 arithmetic's data and weight gradients read)."""
     c = y.shape[-1]
     npix = y.numel() // c
     if part is not None:
         ws = workspace(lib.ugpg_bn_relu_bwd_partials_workspace(c), y.device)
         check(lib.ugpg_bn_relu_bwd_partials(
             ptr(part), part.numel() // (3 * c), ptr(da), *_yargs(y), npix, c, ptr(mean), ptr(invstd),
-            ptr(scale), ptr(shift), ptr(dy), ptr(dgamma), ptr(dbeta), ptr(dconv_bias),
+            ptr(scale), ptr(shift), *_yargs(dy), ptr(dgamma), ptr(dbeta), ptr(dconv_bias),
             int(accumulate), ptr(ws), ws.numel(), stream()), "bn_relu_bwd_partials")
         return
     ws = workspace(lib.ugpg_bn_relu_bwd_workspace(npix, c), y.device)
     check(lib.ugpg_bn_relu_bwd(ptr(da), *_yargs(y), npix, c, ptr(mean), ptr(invstd), ptr(scale),
-                               ptr(shift), ptr(dy), ptr(dgamma), ptr(dbeta), ptr(dconv_bias),
+                               ptr(shift), *_yargs(dy), ptr(dgamma), ptr(dbeta), ptr(dconv_bias),
                                int(accumulate), ptr(ws), ws.numel(), stream()), "bn_relu_bwd")
 
 
 # ------------------------------------------------------------------ pool / resize
-def maxpool2_fwd(a: Act):
+def maxpool2_fwd(a: Act, bf16=False):
+    """bf16: the output stored in bf16 (RNE) only -- the next conv's operand under the bf16
+    arithmetic, exactly."""
     B, H, W, c = a.shape
-    out = empty(B, H // 2, W // 2, c, like=a.y)
+    out = empty(B, H // 2, W // 2, c, like=a.y, dtype=torch.bfloat16 if bf16 else F32)
     am = empty(B, H // 2, W // 2, c, like=a.y, dtype=torch.uint8)
-    check(lib.ugpg_maxpool2_fwd(a.src(), B, H, W, ptr(out), ptr(am), stream()), "maxpool2_fwd")
+    check(lib.ugpg_maxpool2_fwd(a.src(), B, H, W, *_yargs(out), ptr(am), stream()), "maxpool2_fwd")
     return out, am
 
 
