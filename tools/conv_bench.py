@@ -80,6 +80,10 @@ def main():
             srcs.append(ops.Act(torch.randn(B, H, H, C1, device=dev)))
         w = torch.randn(Cout, real_cin, 3, 3, device=dev) * 0.05
         out = torch.empty(B, H, H, Cout, device=dev)
+        # the bf16 arithmetic stores conv outputs of images >= 32 wide in bf16 only, and its
+        # sources (activations, dy) likewise
+        out16 = torch.empty(B, H, H, Cout, device=dev, dtype=torch.bfloat16)
+        srcs16 = [ops.Act(s.y.to(torch.bfloat16), s.scale, s.shift) for s in srcs]
         bias = torch.zeros(Cout, device=dev)
         flops = 2.0 * B * H * H * Cout * 9 * real_cin
         fns = {}
@@ -90,18 +94,23 @@ def main():
             nt = ops.conv_ntiles(B, H, H, cin, Cout, wpk)
             st = torch.empty(3 * Cout * nt, device=dev)
 
-            def f(m=m, wpk=wpk, st=st):
+            st16 = m == "bf16" and H >= 32 and cin >= 16
+
+            def f(m=m, wpk=wpk, st=st, st16=st16):
                 ops.set_conv_math(m)
-                ops.conv3x3_fwd(srcs, wpk, bias, Cout, [out], stats=None if a.nostats else st)
+                ops.conv3x3_fwd(srcs16 if st16 else srcs, wpk, bias, Cout, [out16 if st16 else out],
+                                stats=None if a.nostats else st)
             fns[f"fwd_{m}"] = f
             if wpk1 is not None:
                 dy = torch.randn(B, H, H, Cout, device=dev)
                 d0 = torch.empty(B, H, H, C0, device=dev)
                 d1 = torch.empty(B, H, H, C1, device=dev) if C1 else None
 
-                def g(m=m, wpk1=wpk1, dy=dy, d0=d0, d1=d1):
+                dy16 = dy.to(torch.bfloat16)
+
+                def g(m=m, wpk1=wpk1, dy=dy, d0=d0, d1=d1, dy16=dy16, st16=st16):
                     ops.set_conv_math(m)
-                    ops.conv3x3_fwd([ops.Act(dy)], wpk1, None, real_cin,
+                    ops.conv3x3_fwd([ops.Act(dy16 if st16 else dy)], wpk1, None, real_cin,
                                     [d0, d1] if C1 else [d0], split=C0 if C1 else None)
                 fns[f"dgrad_{m}"] = g
         ops.set_conv_math("x6")
