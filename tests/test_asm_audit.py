@@ -78,3 +78,46 @@ def test_no_packed_f32_valu(asm, kernel):
     start = text.index(kernel + ":")
     body = text[start:text.index(".Lfunc_end", start)]
     assert not re.findall(r"\bv_pk_(add|mul|fma)_f32", body)
+
+
+@pytest.fixture(scope="module")
+def all_asm(tmp_path_factory):
+    """Device assembly of every libugpg source, built with the library's flags."""
+    if not Path(HIPCC).exists():
+        pytest.skip("hipcc not available")
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("ugpg_build", ROOT / "ug-pg-unet_amd" / "build.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    d = tmp_path_factory.mktemp("all_asm")
+    out = {}
+    for src in sorted(CSRC.glob("*.hip")):
+        s = d / (src.stem + ".s")
+        r = subprocess.run([HIPCC, *mod.FLAGS, *mod.PER_FILE.get(src.name, []), f"-I{CSRC}",
+                            f"-I{ROOT / 'include'}", "-S", "--offload-device-only", str(src), "-o",
+                            str(s)], capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out[src.name] = s
+    return out
+
+
+def test_no_packed_fp32_valu_anywhere(all_asm):
+    """No v_pk_{add,mul,fma}_f32 in any kernel of the library: a packed-FP32 write to a VGPR
+    that a just-issued global load reads as its address corrupted the last 16 lanes of the
+    load under concurrent GPU load (build.py NO_PK)."""
+    import re
+    bad = {}
+    for name, s in all_asm.items():
+        n = len(re.findall(r"\bv_pk_(?:add|mul|fma)_f32\b", s.read_text()))
+        if n:
+            bad[name] = n
+    assert not bad, bad
+
+
+def test_no_vmem_operand_overwritten_by_packed_valu(all_asm):
+    """The hazard pattern itself (tools/vmem_war_scan.py): no packed-FP32 VALU writes a VGPR
+    that one of the preceding vector-memory instructions reads."""
+    sys.path.insert(0, str(ROOT / "tools"))
+    from vmem_war_scan import scan
+    hits = {name: len(scan(s)) for name, s in all_asm.items()}
+    assert not any(hits.values()), hits

@@ -44,10 +44,14 @@ def run(bs, tag, poison=False, stage=2, epochs=3):
 
     class Probe(ugpg.UncertaintyGuidedProgressiveTrainer):
         def _forward_device(self, data, target, stage, mbuf):
+            m = self.models[stage]
+            psum = sum(float(p.detach().double().sum()) for p in m.parameters())
             out = super()._forward_device(data, target, stage, mbuf)
+            with torch.no_grad():  # the same forward again (train-mode BN, no autograd)
+                again = float(m(data).double().sum())
             self._probe = (float(out[0].detach().double().sum()),
                            float(out[1].double().sum()) if out[1] is not None else 0.0,
-                           float(data.double().sum()))
+                           float(data.double().sum()), psum, again)
             return out
 
         def train_step(self, data, target, stage):
@@ -58,7 +62,8 @@ def run(bs, tag, poison=False, stage=2, epochs=3):
         def _reduce_metrics(self, mbuf, umap):
             v = mbuf.tolist()
             print(f"{tag} local {' '.join(f'{x:.9g}' for x in v[:7])} | logits {self._probe[0]:.9g} "
-                  f"U {self._probe[1]:.9g} data {self._probe[2]:.9g}", flush=True)
+                  f"U {self._probe[1]:.9g} data {self._probe[2]:.9g} params {self._probe[3]:.12g} "
+                  f"again {self._probe[4]:.9g}", flush=True)
             super()._reduce_metrics(mbuf, umap)
 
     dev = torch.device("cuda:0")

@@ -19,6 +19,10 @@ for s in "$@"; do
     bisect) step bisect 300 python tools/stream_bisect.py --reps 4 --main fwdbwd ;;
     bisect:*) m=${s#bisect:}; step bisect_$m 300 python tools/stream_bisect.py --reps 6 --main $m ;;
     dpsingle) step dpsingle 300 python tools/dp_probe.py single ;;
+    xproc:*) IFS=: read -r _ st bs np it <<< "$s"
+            step xproc_${st}_${bs}_${np} 300 python tools/xproc_bisect.py --stage $st --batch $bs --procs $np --iters ${it:-60} ;;
+    micro:*) IFS=: read -r _ st bs it lib <<< "$s"
+            step micro_${st}_${bs}_${lib:-tree} 300 env ${lib:+UGPG_LIB=exp/$lib.so} python tools/xproc_bisect.py --micro --stage $st --batch $bs --procs 2 --iters ${it:-60} ;;
     poison) step poison 400 python tools/dp_probe.py poison ;;
     dp) step dp 300 python tools/dp_probe.py dp ;;
     dpser) step dpser 300 env AMD_SERIALIZE_KERNEL=3 python tools/dp_probe.py dp ;;

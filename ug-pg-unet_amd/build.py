@@ -22,8 +22,15 @@ INCLUDE = HERE.parent / "include"
 BUILD = HERE / "build"
 LIB = HERE / "ugpg" / "libugpg.so"
 ARCH = os.environ.get("UGPG_ARCH", "gfx950")
+# Device code without packed-FP32 VALU (v_pk_add/mul/fma_f32): a packed-FP32 write to a
+# VGPR that a just-issued global load still reads as its address corrupted the last 16
+# lanes of that load under concurrent GPU load (another stream or process) -- measured on
+# the logits combine, 10-717 of 3000 launches wrong with them, 0 of 6000 without
+# (tools/xproc_bisect.py --micro).  The host compile ignores the feature
+# (ignored there, with a warning).
+NO_PK = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
-         "-Wno-unused-variable", "-Wno-unused-but-set-variable"]
+         "-Wno-unused-variable", "-Wno-unused-but-set-variable", *NO_PK]
 
 
 def _hipcc() -> str:
@@ -67,6 +74,10 @@ def build(force: bool = False, verbose: bool = True, defines=(), out: Path | Non
     lib = Path(out) if out else LIB
     bdir = BUILD if not defines else BUILD / ("v_" + "_".join(d.replace("=", "") for d in defines))
     bdir.mkdir(parents=True, exist_ok=True)
+    # objects built with other flags are stale
+    stamp, flags = bdir / "flags.txt", repr((FLAGS, PER_FILE))
+    if not stamp.exists() or stamp.read_text() != flags:
+        force = True
     srcs = _sources()
     jobs = min(len(srcs), int(os.environ.get("MAX_JOBS", "8")))
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
@@ -81,6 +92,7 @@ def build(force: bool = False, verbose: bool = True, defines=(), out: Path | Non
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr}")
         os.replace(tmp, LIB_)
+    stamp.write_text(flags)
     if verbose:
         print(f"built {LIB_} ({LIB_.stat().st_size / 1e6:.1f} MB)")
     return LIB_

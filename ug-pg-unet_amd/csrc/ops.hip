@@ -606,6 +606,54 @@ struct HeadSet {
     int n;
 };
 
+// Four consecutive outputs of one row per thread (one 16-byte store), the row's vertical
+// indices / weights computed once per head, 32-bit offsets within a head; the same
+// arithmetic and head order as before (per output: ly0*(lx0*a + lx1*b) + ly1*(...), summed
+// over heads in order), so the logits are bit-identical to the one-output-per-thread form.
+#ifndef HEADS_COMBINE_V1
+__global__ void __launch_bounds__(256) heads_combine_kernel(HeadSet hs, int B, int H, int W, int nc,
+                                                            float* logits) {
+    const int W4 = W >> 2;
+    const int64_t total4 = (int64_t)B * nc * H * W4;
+    for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < total4;
+         q += (int64_t)gridDim.x * blockDim.x) {
+        const int x0o = (int)(q % W4) * 4;
+        const int64_t r = q / W4;  // (b, k, y) row
+        const int y = (int)(r % H);
+        const int k = (int)((r / H) % nc), b = (int)(r / ((int64_t)H * nc));
+        f32x4 s = {0.f, 0.f, 0.f, 0.f};
+        // constant head indices: every kernel argument is read once, at the kernel start
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (j >= hs.n) break;
+            const int R = hs.res[j];
+            const float* hp = hs.h[j] + (size_t)b * R * R * nc + k;
+            f32x4 v;
+            if (R == H) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[u] = hp[(y * W + x0o + u) * nc];
+            } else {
+                int y0, y1;
+                float ly0, ly1;
+                ac_index(y, R, H, y0, y1, ly0, ly1);
+                const float* r0 = hp + y0 * R * nc;
+                const float* r1 = hp + y1 * R * nc;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    int x0, x1;
+                    float lx0, lx1;
+                    ac_index(x0o + u, R, W, x0, x1, lx0, lx1);
+                    v[u] = ly0 * (lx0 * r0[x0 * nc] + lx1 * r0[x1 * nc]) +
+                           ly1 * (lx0 * r1[x0 * nc] + lx1 * r1[x1 * nc]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) s[u] = (j == 0) ? v[u] : s[u] + v[u];
+        }
+        *reinterpret_cast<f32x4*>(logits + r * W + x0o) = s;
+    }
+}
+#else
 __global__ void heads_combine_kernel(HeadSet hs, int B, int H, int W, int nc, float* logits) {
     const int64_t total = (int64_t)B * nc * H * W;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
@@ -635,6 +683,7 @@ __global__ void heads_combine_kernel(HeadSet hs, int B, int H, int W, int nc, fl
         logits[i] = s;
     }
 }
+#endif
 
 // dh (NHWC, R x R, nc) from NCHW dlogits (H x W): the transpose of the align-corners
 // upsample R -> H.  One block per (b, iy); for R < 256 the threads split the output
@@ -1525,7 +1574,12 @@ extern "C" int ugpg_heads_combine(const float* const* h, const int* hres, int n,
         hs.h[i] = i < n ? h[i] : nullptr;
         hs.res[i] = i < n ? hres[i] : 0;
     }
+#ifndef HEADS_COMBINE_V1
+    UGPG_REQUIRE(W % 4 == 0, "heads_combine: width");
+    const int64_t total = (int64_t)B * nc * H * W / 4;
+#else
     const int64_t total = (int64_t)B * nc * H * W;
+#endif
     hipLaunchKernelGGL(heads_combine_kernel, dim3(stream_grid(total)), dim3(256), 0,
                        as_stream(stream), hs, B, H, W, nc, logits);
     return check_launch("heads_combine");
