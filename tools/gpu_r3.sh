@@ -36,6 +36,8 @@ for s in "$@"; do
     alltests) step alltests 1100 python -u -m pytest tests -m gpu -q -rf --timeout 500 --timeout-method thread -p no:cacheprovider ;;
     ab:*) IFS=: read -r _ libs layers <<< "$s"
             step ab 400 python tools/conv_bench.py --rounds ${ROUNDS:-4} --maths ${MATHS:-x6,bf16} --layers ${layers:-inc.3,down1.0,down2.3,up4.0,up4.3} --libs $libs ${EXTRA:-} ;;
+    abstep:*) IFS=: read -r _ sa sb <<< "$s"
+            step abstep 400 python tools/ab_step.py --a "$sa" --b "$sb" ${EXTRA:-} ;;
     bench) step bench 600 python bench.py ;;
     bench_bf16) step bench_bf16 300 python bench.py --conv-math bf16 --no-cpu-baseline --secondary-steps 0 ;;
     herlev256) step herlev256 600 python bench.py --workload herlev --res 256 ;;
