@@ -69,6 +69,104 @@ __global__ void maxpool2_fwd_kernel(YRef x, const float* sc, const float* sh, in
     }
 }
 
+// bf16 storage in and out (the bf16 arithmetic): 8 channels per thread, one 16-byte load per
+// window pixel and one 16-byte store (the 4-channel form moved 8 bytes per access and ran at
+// 2.4-3.5 TB/s).  Per element the same arithmetic, max rule and argmax as the fp32 form.
+__device__ __forceinline__ void ld8_bf16(const __bf16* p, f32x4& lo, f32x4& hi) {
+    const uint4 w = *reinterpret_cast<const uint4*>(p);
+    lo = f32x4{__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u),
+               __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u)};
+    hi = f32x4{__uint_as_float(w.z << 16), __uint_as_float(w.z & 0xffff0000u),
+               __uint_as_float(w.w << 16), __uint_as_float(w.w & 0xffff0000u)};
+}
+__device__ __forceinline__ unsigned pk2_bf16(float a, float b) {  // round to nearest even
+    typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+    typedef float f32x2_t __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2_t{a, b}, bf16x2_t));
+}
+__device__ __forceinline__ void st8_bf16(__bf16* p, const f32x4& lo, const f32x4& hi) {
+    *reinterpret_cast<uint4*>(p) =
+        uint4{pk2_bf16(lo.x, lo.y), pk2_bf16(lo.z, lo.w), pk2_bf16(hi.x, hi.y), pk2_bf16(hi.z, hi.w)};
+}
+
+__device__ __forceinline__ f32x4 act4c(f32x4 v, const f32x4& s, const f32x4& h, bool on) {
+    if (on) {
+        v.x = fmaxf(fmaf(v.x, s.x, h.x), 0.0f);
+        v.y = fmaxf(fmaf(v.y, s.y, h.y), 0.0f);
+        v.z = fmaxf(fmaf(v.z, s.z, h.z), 0.0f);
+        v.w = fmaxf(fmaf(v.w, s.w, h.w), 0.0f);
+    }
+    return v;
+}
+
+// A thread keeps its 8 channels (the grid stride, a multiple of 256, is a multiple of C/8),
+// so the activation coefficients are loaded once; U units' window loads go out before the
+// first is used.
+__global__ void __launch_bounds__(256) maxpool2_fwd16_kernel(const __bf16* x, const float* sc,
+                                                             const float* sh, int B, int H, int W,
+                                                             int C, __bf16* out16, uint8_t* am) {
+    constexpr int U = 4;
+    const int Ho = H / 2, Wo = W / 2, C8 = C / 8;
+    const int64_t total = (int64_t)B * Ho * Wo * C8, G = (int64_t)gridDim.x * blockDim.x;
+    int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i0 >= total) return;
+    const int c = (int)(i0 % C8) * 8;
+    const bool on = sc != nullptr;
+    f32x4 s4[2], h4[2];
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+        s4[hf] = on ? *reinterpret_cast<const f32x4*>(sc + c + 4 * hf) : f32x4{1.f, 1.f, 1.f, 1.f};
+        h4[hf] = on ? *reinterpret_cast<const f32x4*>(sh + c + 4 * hf) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    for (; i0 < total; i0 += U * G) {
+        f32x4 xv[U][4][2];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = min(i0 + u * G, total - 1);
+            int64_t r = i / C8;
+            const int ox = (int)(r % Wo);
+            r /= Wo;
+            const int oy = (int)(r % Ho), b = (int)(r / Ho);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int y = 2 * oy + (k >> 1), xx = 2 * ox + (k & 1);
+                ld8_bf16(x + ((size_t)(b * H + y) * W + xx) * C + c, xv[u][k][0], xv[u][k][1]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = i0 + u * G;
+            if (i >= total) break;
+            f32x4 best[2];
+            uint8_t idx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int hf = 0; hf < 2; ++hf) {
+                    const f32x4 v = act4c(xv[u][k][hf], s4[hf], h4[hf], on);
+                    if (k == 0) {
+                        best[hf] = v;
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            if (v[j] > best[hf][j] || isnan(v[j])) {
+                                best[hf][j] = v[j];
+                                idx[4 * hf + j] = (uint8_t)k;
+                            }
+                    }
+                }
+            st8_bf16(out16 + i * 8, best[0], best[1]);
+            unsigned lo = 0, hi = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                lo |= (unsigned)idx[j] << (8 * j);
+                hi |= (unsigned)idx[4 + j] << (8 * j);
+            }
+            *reinterpret_cast<uint2*>(am + i * 8) = uint2{lo, hi};
+        }
+    }
+}
+
 __global__ void maxpool2_bwd_kernel(const float* dout, const uint8_t* am, int B, int H, int W,
                                     int C, float* din, int acc) {
     const int Ho = H / 2, Wo = W / 2, C4 = C / 4;
@@ -282,6 +380,66 @@ __global__ void bilinear_nhwc_fwd_kernel(YRef x, const float* sc, const float* s
         const f32x4 a11 = act(x.ld4(r1 + (size_t)x1 * C + c));
         const f32x4 v = ly0 * (lx0 * a00 + lx1 * a01) + ly1 * (lx0 * a10 + lx1 * a11);
         store(orow + (size_t)ox * C + c, v);
+    }
+}
+
+// bf16 in and out, 8 channels per thread (see maxpool2_fwd16_kernel), one block per output
+// row, U units' loads issued before the first is used; per element the same arithmetic and
+// order as bilinear_nhwc_fwd_kernel.
+__global__ void __launch_bounds__(256) bilinear_nhwc_fwd16_kernel(const __bf16* x, const float* sc,
+                                                                  const float* sh, int B, int Hi,
+                                                                  int Wi, int C, __bf16* out16,
+                                                                  int Ho, int Wo) {
+    constexpr int U = 4;
+    const int C8 = C / 8;
+    const int row = blockIdx.y;  // b * Ho + oy
+    const int b = row / Ho, oy = row % Ho;
+    int y0, y1;
+    float ly0, ly1;
+    ac_index(oy, Hi, Ho, y0, y1, ly0, ly1);
+    const size_t r0 = ((size_t)b * Hi + y0) * Wi * C, r1 = ((size_t)b * Hi + y1) * Wi * C;
+    const size_t orow = (size_t)row * Wo * C;
+    const int n = Wo * C8, G = gridDim.x * blockDim.x;
+    int t0 = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t0 >= n) return;
+    const int c = (t0 % C8) * 8;  // fixed: G is a multiple of 256, hence of C8
+    const bool on = sc != nullptr;
+    f32x4 s4[2], h4[2];
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+        s4[hf] = on ? *reinterpret_cast<const f32x4*>(sc + c + 4 * hf) : f32x4{1.f, 1.f, 1.f, 1.f};
+        h4[hf] = on ? *reinterpret_cast<const f32x4*>(sh + c + 4 * hf) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    for (; t0 < n; t0 += U * G) {
+        f32x4 a[U][4][2];
+        float wx0[U], wx1[U];
+        int oxs[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int t = min(t0 + u * G, n - 1);
+            const int ox = t / C8;
+            int x0, x1;
+            ac_index(ox, Wi, Wo, x0, x1, wx0[u], wx1[u]);
+            oxs[u] = ox;
+            ld8_bf16(x + r0 + (size_t)x0 * C + c, a[u][0][0], a[u][0][1]);
+            ld8_bf16(x + r0 + (size_t)x1 * C + c, a[u][1][0], a[u][1][1]);
+            ld8_bf16(x + r1 + (size_t)x0 * C + c, a[u][2][0], a[u][2][1]);
+            ld8_bf16(x + r1 + (size_t)x1 * C + c, a[u][3][0], a[u][3][1]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (t0 + u * G >= n) break;
+            f32x4 v[2];
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+                const f32x4 a00 = act4c(a[u][0][hf], s4[hf], h4[hf], on),
+                            a01 = act4c(a[u][1][hf], s4[hf], h4[hf], on),
+                            a10 = act4c(a[u][2][hf], s4[hf], h4[hf], on),
+                            a11 = act4c(a[u][3][hf], s4[hf], h4[hf], on);
+                v[hf] = ly0 * (wx0[u] * a00 + wx1[u] * a01) + ly1 * (wx0[u] * a10 + wx1[u] * a11);
+            }
+            st8_bf16(out16 + orow + (size_t)oxs[u] * C + c, v[0], v[1]);
+        }
     }
 }
 
@@ -1400,6 +1558,13 @@ extern "C" int ugpg_maxpool2_fwd(ugpg_src_t s, int B, int H, int W, float* out, 
     UGPG_REQUIRE((s.data || s.data_bf16) && (out || out_bf16) && am && s.C % 4 == 0 && H >= 2 &&
                      W >= 2,
                  "maxpool2_fwd");
+    if (!s.data && !out && s.C % 8 == 0 && 256 % (s.C / 8) == 0) {  // bf16 in and out: 16-byte accesses
+        const int64_t total8 = (int64_t)B * (H / 2) * (W / 2) * (s.C / 8);
+        hipLaunchKernelGGL(maxpool2_fwd16_kernel, dim3(stream_grid(cdiv(total8, (int64_t)4))), dim3(256), 0,
+                           as_stream(stream), static_cast<const __bf16*>(s.data_bf16), s.scale,
+                           s.shift, B, H, W, s.C, static_cast<__bf16*>(out_bf16), am);
+        return check_launch("maxpool2_fwd");
+    }
     const int64_t total = (int64_t)B * (H / 2) * (W / 2) * (s.C / 4);
     hipLaunchKernelGGL(maxpool2_fwd_kernel<false>, dim3(stream_grid(total)), dim3(256), 0,
                        as_stream(stream), yref(s), s.scale, s.shift, B, H, W, s.C, out,
@@ -1450,6 +1615,14 @@ extern "C" int ugpg_bilinear_nhwc_fwd(ugpg_src_t s, int B, int Hi, int Wi, float
     UGPG_REQUIRE((int64_t)B * Ho < 65536, "bilinear_nhwc_fwd: shape");
     // a quarter of the row's quads in threads when that divides evenly (the kernel's
     // 4-quads-per-thread form), else one quad per thread
+    if (!s.data && !out && s.C % 8 == 0 && 256 % (s.C / 8) == 0) {  // bf16 in and out: 16-byte accesses
+        // one block per output row (its 2048-unit rows: 8 units per thread), more for wider rows
+        const unsigned g8 = (unsigned)std::min<int64_t>(cdiv((int64_t)Wo * (s.C / 8), 2048), 64);
+        hipLaunchKernelGGL(bilinear_nhwc_fwd16_kernel, dim3(g8, (unsigned)(B * Ho)), dim3(256), 0,
+                           as_stream(stream), static_cast<const __bf16*>(s.data_bf16), s.scale,
+                           s.shift, B, Hi, Wi, s.C, static_cast<__bf16*>(out_bf16), Ho, Wo);
+        return check_launch("bilinear_nhwc_fwd");
+    }
     const int64_t nq = (int64_t)Wo * (s.C / 4);
     const unsigned gx = nq % 1024 == 0 ? (unsigned)std::min<int64_t>(nq / 1024, 64)
                                        : (unsigned)std::min<int64_t>(cdiv(nq, 256), 64);
