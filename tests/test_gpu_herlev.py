@@ -266,3 +266,56 @@ def test_config4_bs16_parity(dev, res):
             bad.append(f"{k}: {err:.3e} > {bound:.3e}")
     print(f"herlev {res}: gradient headroom (err/bound) worst 3 {sorted(ratios, reverse=True)[:3]}")
     assert not bad, "\n".join(bad)
+
+
+def _oracle_ug(state4, state3, x, y, cw, dtype=torch.float64):
+    """The full UG step of the oracle: prev = the Stage-3 classifier in eval mode on the
+    input resized to 128 (train_herlev.py:216-296, oracle.ref_cpu.herlev_train_step)."""
+    P3 = {k: (v.clone().to(dtype) if v.is_floating_point() else v.clone()) for k, v in state3.items()}
+    with torch.no_grad():
+        prev = O.herlev_forward(3, P3, O.resize_bilinear(x.to(dtype), 128), training=False)
+    return oracle(state4, x, y, prev, cw, dtype)
+
+
+@pytest.mark.parametrize("res", [224])
+def test_config4_bs16_full_ug_step(dev, res):
+    """BASELINE config 4 as the trainer runs it (the bs16 test above feeds random
+    `prev` logits): HerlevTrainer.uncertainty_guided_forward_pass at bs16 -- the Stage-3
+    classifier's eval prediction on the input resized to 128, the uncertainty-weighted CE
+    with class weights, backward -- against the oracle's same step (prev from its own
+    Stage-3 forward), dropout off: loss, U statistics and every gradient (§8d rule)."""
+    B = 16
+    cw = [0.5, 0.75, 1.0, 1.25, 1.5, 1.75, 2.0]
+    tr = _reference_trainer(dev, K, cw, 1.0, res)
+    s4, s3 = herlev_state(4, seed=94), herlev_state(3, seed=95)
+    tr.models[4].load_state_dict(s4)
+    tr.models[3].load_state_dict(s3)
+    tr.models[4].train()
+    for mod in tr.models[4].modules():
+        if isinstance(mod, nn.Dropout):
+            mod.p = 0.0
+    x = G.randn(96, (B, 3, res, res), "x")
+    y = G.randint(97, (B,), K, "y")
+    final, met = tr.uncertainty_guided_forward_pass(x.to(dev), y.to(dev), 4)
+    final.backward()
+    cwt = torch.tensor(cw)
+    o32, f32, b32, w32, g32 = _oracle_ug(s4, s3, x, y, cwt, torch.float32)
+    _, f64, b64, w64, g64 = _oracle_ug(s4, s3, x, y, cwt, torch.float64)
+    assert (met["output"].detach().cpu() - o32).abs().max().item() <= 1e-3
+    assert abs(met["final_loss"] - f64.item()) <= 1e-5 * abs(f64.item())
+    assert abs(met["base_loss"] - b64.item()) <= 1e-5 * abs(b64.item())
+    assert abs(met["uncertainty_weight_mean"] - w64.mean().item()) <= 1e-5
+    floor = {k: (g32[k].double() - g64[k]).abs().max().item() for k in g32}
+    for sd, rel in ((7, 1e-7), (10, 1e-6), (12, 5e-6)):
+        _, _, _, _, gp = _oracle_ug(perturbed_state(s4, sd, rel), s3, x, y, cwt, torch.float32)
+        for k in floor:
+            floor[k] = max(floor[k], (gp[k].double() - g64[k]).abs().max().item())
+    named = dict(tr.models[4].named_parameters())
+    bad, ratios = [], []
+    for k in g32:
+        ok, err, bound = grad_check(k, named[k].grad, g32[k], g64[k], floor[k])
+        ratios.append((err / bound, k))
+        if not ok:
+            bad.append(f"{k}: {err:.3e} > {bound:.3e}")
+    print(f"herlev UG {res}: gradient headroom (err/bound) worst 3 {sorted(ratios, reverse=True)[:3]}")
+    assert not bad, "\n".join(bad)
