@@ -50,7 +50,7 @@ def main():
         wpk = ops.pack_conv3x3(w, C0 + C1, 0)
         st = torch.empty(3 * Cout * ops.conv_ntiles(B, H, H, C0 + C1, Cout, wpk), device=dev)
         flops = 2.0 * B * H * H * Cout * 9 * (C0 + C1)
-        dy = torch.randn(B, H, H, Cout, device=dev)
+        dy = torch.randn(B, H, H, Cout, device=dev).to(dt16)  # bf16 dy under --out16 (the step's form)
         dw = torch.empty_like(w)
         for pipe in ("default",):
             n, t0 = 0, time.perf_counter()

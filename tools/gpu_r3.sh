@@ -30,13 +30,15 @@ for s in "$@"; do
     probe) step probe 300 python tools/umap_stream_probe.py --steps 4 --reps 2 ;;
     stamps) step stamps 300 env UGPG_LIB=exp/lib_stamp.so python tools/clock_probe.py --stamps --seconds 1 --layers inc.3,down1.3,down2.3,down3.3,up4.0 &&
             step stamps16 300 env UGPG_LIB=exp/lib_stamp.so python tools/clock_probe.py --stamps --seconds 1 --math bf16 --out16 --layers inc.3,down1.3,down2.3,down3.3,up4.0 ;;
+    wstamp:*) IFS=: read -r _ lib math <<< "$s"
+            step wstamp_${lib}_${math} 300 env UGPG_LIB=exp/$lib.so python tools/clock_probe.py --stamps --wgrad --seconds 1 --math $math --out16 --layers inc.3,down1.3,down2.3,down3.3,up4.0 ;;
     stamp:*) IFS=: read -r _ lib math <<< "$s"
             step stamp_${lib}_${math} 300 env UGPG_LIB=exp/$lib.so python tools/clock_probe.py --stamps --seconds 1 --math $math --out16 --layers inc.3,down1.3,down2.3,down3.3,up4.0 ;;
     tests:*) f=${s#tests:}; n=$(basename "${f%% *}" .py); step t_${n%%::*} 900 python -u -m pytest $f -q -rf -x --timeout 400 --timeout-method thread -p no:cacheprovider ;;
     alltests) step alltests 1100 python -u -m pytest tests -m gpu -q -rf --timeout 500 --timeout-method thread -p no:cacheprovider ;;
     ab:*) IFS=: read -r _ libs layers <<< "$s"
             step ab 400 python tools/conv_bench.py --rounds ${ROUNDS:-4} --maths ${MATHS:-x6,bf16} --layers ${layers:-inc.3,down1.0,down2.3,up4.0,up4.3} --libs $libs ${EXTRA:-} ;;
-    abstep:*) IFS=: read -r _ sa sb <<< "$s"
+    abstep:*) IFS=@ read -r sa sb <<< "${s#abstep:}"
             step abstep 400 python tools/ab_step.py --a "$sa" --b "$sb" ${EXTRA:-} ;;
     bench) step bench 600 python bench.py ;;
     bench_bf16) step bench_bf16 300 python bench.py --conv-math bf16 --no-cpu-baseline --secondary-steps 0 ;;

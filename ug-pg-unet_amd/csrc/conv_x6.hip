@@ -1649,11 +1649,15 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
     if (loader) {
         // ------------------------------------------------------------ loader waves
         const int lt = tid - 256;
-        typename std::conditional<DB16, u32x2v, f32x4>::type rdy[DY_PER];
-        typename std::conditional<XB16, u32x2v, f32x4>::type rx[X_PER];
-        Act4 xa;
-        float xlo = 0.f;
-        unsigned dvalid = 0, xvalid = 0;
+        // NSET register sets: the single-piece form (NP = 1) keeps two steps' loads in
+        // flight (its steps are a third as long, and one step of flight left the loaders
+        // waiting 11-22 % of the loop in vmcnt: tools/clock_probe.py --stamps --wgrad)
+        constexpr int NSET = NP == 1 ? 2 : 1;
+        typename std::conditional<DB16, u32x2v, f32x4>::type rdy[NSET][DY_PER];
+        typename std::conditional<XB16, u32x2v, f32x4>::type rx[NSET][X_PER];
+        Act4 xa[NSET];
+        float xlo[NSET];
+        unsigned dvalid[NSET], xvalid[NSET];
         // the loader's cursor also carries the item's co / ci blocks and the tile's
         // image position, updated without divisions inside an item
         struct LCur {
@@ -1685,7 +1689,8 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
                 lderive(l);
             }
         };
-        auto gload = [&](const LCur& c) {
+        auto gload = [&](const LCur& c, auto S) {
+            constexpr int st = decltype(S)::value;
             const int co0 = c.nb * 64, ci0 = c.cb * 64;
             const bool second = ci0 >= a.C0;
             const float* xsrc = second ? a.src1 : a.src0;
@@ -1694,10 +1699,10 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
             const float* xsh = second ? a.sh1 : a.sh0;
             const int Cs = second ? a.C1 : a.C0, cbase = second ? ci0 - a.C0 : ci0;
             const bool xon = xsc != nullptr;
-            xlo = xon ? 0.f : -INFINITY;
+            xlo[st] = xon ? 0.f : -INFINITY;
             const int cq = cbase + (lt & 15) * 4;  // q = idx & 15 = lt & 15
-            xa.s = gld16((xon ? xsc : g_act_ones) + cq);
-            xa.h = gld16((xon ? xsh : g_act_zeros) + cq);
+            xa[st].s = gld16((xon ? xsc : g_act_ones) + cq);
+            xa[st].h = gld16((xon ? xsh : g_act_zeros) + cq);
             const int b = c.b, ty0 = c.ty0, tx0 = c.tx0;
             const int q4 = (lt & 15) * 4;
             // per-lane pixel positions inside the tile (compile-time divisors): dy
@@ -1729,10 +1734,10 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
 #pragma unroll
                 for (int v = 0; v < X_PER; ++v)
                     xof[v] = ((xin >> v) & 1u) ? (xpy[v] * a.W + xpx[v]) * Cs : 0;
-                dvalid = (1u << DY_PER) - 1;
-                xvalid = xin;
+                dvalid[st] = (1u << DY_PER) - 1;
+                xvalid[st] = xin;
             } else {
-                dvalid = 0;
+                dvalid[st] = 0;
 #pragma unroll
                 for (int v = 0; v < DY_PER; ++v) {
                     const int p = (lt + v * 256) >> 4;
@@ -1740,9 +1745,9 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
                     const bool ok = gy < a.H && gx < a.W;
                     const int cy = min(gy, a.H - 1), cx = min(gx, a.W - 1);
                     dof[v] = ((cy - ty0) * a.W + (cx - tx0)) * a.Cout;
-                    dvalid |= (ok ? 1u : 0u) << v;
+                    dvalid[st] |= (ok ? 1u : 0u) << v;
                 }
-                xvalid = 0;
+                xvalid[st] = 0;
 #pragma unroll
                 for (int v = 0; v < X_PER; ++v) {
                     const int gy = ty0 + xpy[v], gx = tx0 + xpx[v];
@@ -1750,20 +1755,20 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
                         ((xin >> v) & 1u) && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
                     const int cy = min(max(gy, 0), a.H - 1), cx = min(max(gx, 0), a.W - 1);
                     xof[v] = ((cy - ty0) * a.W + (cx - tx0)) * Cs;
-                    xvalid |= (ok ? 1u : 0u) << v;
+                    xvalid[st] |= (ok ? 1u : 0u) << v;
                 }
             }
             const size_t dyo0 = ((size_t)(b * a.H + ty0) * a.W + tx0) * a.Cout + co0 + q4;
             const size_t xb = ((size_t)(b * a.H + ty0) * a.W + tx0) * Cs + cbase + q4;
 #pragma unroll
             for (int v = 0; v < DY_PER; ++v) {
-                if constexpr (DB16) rdy[v] = gld8(a.dy16 + dyo0 + dof[v]);
-                else rdy[v] = gld16(a.dy + dyo0 + dof[v]);
+                if constexpr (DB16) rdy[st][v] = gld8(a.dy16 + dyo0 + dof[v]);
+                else rdy[st][v] = gld16(a.dy + dyo0 + dof[v]);
             }
 #pragma unroll
             for (int v = 0; v < X_PER; ++v) {
-                if constexpr (XB16) rx[v] = gld8(xsrc16 + xb + xof[v]);
-                else rx[v] = gld16(xsrc + xb + xof[v]);
+                if constexpr (XB16) rx[st][v] = gld8(xsrc16 + xb + xof[v]);
+                else rx[st][v] = gld16(xsrc + xb + xof[v]);
             }
         };
         // record layout: [piece][64 ch] bf16 at byte piece*128 + ch*2
@@ -1774,7 +1779,8 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
 #pragma unroll
             for (int k = 0; k < NP; ++k) *reinterpret_cast<u32x2*>(r + 128 * k) = pc[k];
         };
-        auto lstore = [&](int buf) {
+        auto lstore = [&](int buf, auto S) {
+            constexpr int st = decltype(S)::value;
             char* dys = smem + buf * RECS * REC;
             char* xs = dys + P * REC;
 #pragma unroll
@@ -1783,11 +1789,11 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
                 const f32x4 z = {0.f, 0.f, 0.f, 0.f};
                 f32x4 d;
                 if constexpr (DB16)  // 4 bf16 widened (exact)
-                    d = f32x4{__uint_as_float(rdy[v].x << 16), __uint_as_float(rdy[v].x & 0xffff0000u),
-                              __uint_as_float(rdy[v].y << 16), __uint_as_float(rdy[v].y & 0xffff0000u)};
+                    d = f32x4{__uint_as_float(rdy[st][v].x << 16), __uint_as_float(rdy[st][v].x & 0xffff0000u),
+                              __uint_as_float(rdy[st][v].y << 16), __uint_as_float(rdy[st][v].y & 0xffff0000u)};
                 else
-                    d = rdy[v];
-                put(dys + (idx >> 4) * REC, idx & 15, ((dvalid >> v) & 1u) ? d : z);
+                    d = rdy[st][v];
+                put(dys + (idx >> 4) * REC, idx & 15, ((dvalid[st] >> v) & 1u) ? d : z);
             }
 #pragma unroll
             for (int v = 0; v < X_PER; ++v) {
@@ -1795,22 +1801,28 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
                 const f32x4 z = {0.f, 0.f, 0.f, 0.f};
                 f32x4 raw;
                 if constexpr (XB16)  // 4 bf16 widened (exact)
-                    raw = f32x4{__uint_as_float(rx[v].x << 16), __uint_as_float(rx[v].x & 0xffff0000u),
-                                __uint_as_float(rx[v].y << 16), __uint_as_float(rx[v].y & 0xffff0000u)};
+                    raw = f32x4{__uint_as_float(rx[st][v].x << 16), __uint_as_float(rx[st][v].x & 0xffff0000u),
+                                __uint_as_float(rx[st][v].y << 16), __uint_as_float(rx[st][v].y & 0xffff0000u)};
                 else
-                    raw = rx[v];
-                const f32x4 val = ((xvalid >> v) & 1u) ? act_floor4(raw, xa, xlo) : z;
+                    raw = rx[st][v];
+                const f32x4 val = ((xvalid[st] >> v) & 1u) ? act_floor4(raw, xa[st], xlo[st]) : z;
                 put(idx < X_Q ? xs + (idx >> 4) * REC : dummy, idx & 15, val);
             }
         };
+        using Set0 = std::integral_constant<int, 0>;
+        using SetL = std::integral_constant<int, NSET - 1>;  // set of odd steps
         LCur lc;
         item_range(item0, lc.c);
         lderive(lc);
-        gload(lc);
+        gload(lc, Set0{});
         vm_wait<0>();
-        lstore(0);
+        lstore(0, Set0{});
         ladvance(lc);
-        gload(lc);  // step 1
+        gload(lc, SetL{});  // step 1
+        if constexpr (NSET == 2) {
+            ladvance(lc);
+            gload(lc, Set0{});  // step 2 (set 0 was stored above)
+        }
         lds_barrier();
 #ifdef X6W_STAMP
         // diagnostic build: loader cycles waiting for global loads / at the barrier
@@ -1825,14 +1837,26 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
 #else
 #define ST_WAIT(acc, stmt) stmt
 #endif
-        for (int k = 0; k < total; ++k) {
-            ST_WAIT(st_vm, vm_wait<0>());
-            lstore((k + 1) & 1);  // step k+1
+        // step k: write step k+1 (its loads retired: with two sets, step k+2's stay in
+        // flight -- loads retire in issue order), then issue step k+1+NSET into the freed set
+        auto lstep = [&](int k, auto S) {
+            if constexpr (NSET == 2) {
+                ST_WAIT(st_vm, vm_wait<LOADS>());
+            } else {
+                ST_WAIT(st_vm, vm_wait<0>());
+            }
+            lstore((k + 1) & 1, S);  // step k+1
             ladvance(lc);
-#ifndef X6W_NOLOAD  // diagnostic build: re-store step 1's registers (results are wrong)
-            gload(lc);            // step k+2, in flight across the barrier
-#endif
+            gload(lc, S);            // step k+1+NSET, in flight across the barrier
             ST_WAIT(st_bar, lds_barrier());
+        };
+        if constexpr (NSET == 2) {
+            for (int k = 0; k < total; k += 2) {
+                lstep(k, SetL{});                         // step k+1 (odd): set 1
+                if (k + 1 < total) lstep(k + 1, Set0{});  // step k+2 (even): set 0
+            }
+        } else {
+            for (int k = 0; k < total; ++k) lstep(k, Set0{});
         }
 #undef ST_WAIT
         vm_wait<0>();  // no load outlives the workgroup (nothing may run before this wait:
