@@ -178,7 +178,7 @@ def roofline_from(timer, steps, every, math):
     achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
     peak = {"x6": BF16_PEAK_TFLOPS / X6_PRODUCTS, "bf16": BF16_PEAK_TFLOPS}.get(
         math, FP32_PEAK_TFLOPS)
-    traffic, src = pmc_traffic(dom) if math == "x6" else (None, None)
+    traffic, src = pmc_traffic(dom, bf16=math == "bf16")
     roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2),
             "peak": round(peak, 1), "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
             "traffic": traffic, "traffic_source": src,
@@ -192,12 +192,14 @@ def roofline_from(timer, steps, every, math):
     return roof, kernels
 
 
-def pmc_traffic(family):
-    """HBM bytes per launch of a kernel family from the newest committed PMC summary
-    (profiles/*_pmc.json, written by tools/pmc_summary.py from separate FETCH_SIZE /
-    WRITE_SIZE passes with the gfx950 x2 read correction); None when absent."""
+def pmc_traffic(family, bf16=False):
+    """HBM bytes per launch of a kernel family from the newest committed PMC summary of
+    the same arithmetic (profiles/*_pmc.json, written by tools/pmc_summary.py from separate
+    FETCH_SIZE / WRITE_SIZE passes with the gfx950 x2 read correction; the bf16 runs'
+    summaries carry "bf16" in their name); None when absent."""
     # newest = last by name (r1c < r1d < ...): a checkout gives every file the same mtime
-    files = sorted((ROOT / "profiles").glob("*_pmc.json"), key=lambda p: p.name)
+    files = sorted((p for p in (ROOT / "profiles").glob("*_pmc.json") if ("bf16" in p.name) == bf16),
+                   key=lambda p: p.name)
     if not files:
         return None, None
     rows = json.load(open(files[-1]))
