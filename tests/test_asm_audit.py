@@ -121,3 +121,29 @@ def test_no_vmem_operand_overwritten_by_packed_valu(all_asm):
     from vmem_war_scan import scan
     hits = {name: len(scan(s)) for name, s in all_asm.items()}
     assert not any(hits.values()), hits
+
+
+def test_vmem_war_scan_finds_the_pattern(tmp_path):
+    """tools/vmem_war_scan.py itself: a packed-FP32 write to a VGPR a just-issued global
+    load reads as its address is flagged (the corrupting sequence of DESIGN.md §6a);
+    the same write after the load retired (s_waitcnt vmcnt(0)), to a different
+    register, or by a plain VALU, is not."""
+    sys.path.insert(0, str(ROOT / "tools"))
+    from vmem_war_scan import scan
+    asm = tmp_path / "k.s"
+    asm.write_text("""k_bad:
+\tglobal_load_dword v24, v[28:29], off
+\tv_mov_b32_e32 v1, 0
+\tv_pk_mul_f32 v[28:29], v[6:7], v[32:33]
+\ts_endpgm
+k_ok:
+\tglobal_load_dword v24, v[28:29], off
+\ts_waitcnt vmcnt(0)
+\tv_pk_mul_f32 v[28:29], v[6:7], v[32:33]
+\tglobal_load_dword v25, v[30:31], off
+\tv_pk_mul_f32 v[40:41], v[6:7], v[32:33]
+\tv_mov_b32_e32 v30, 0
+\ts_endpgm
+""")
+    hits = scan(asm)
+    assert [h[0] for h in hits] == ["k_bad"], hits
