@@ -545,20 +545,48 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
                 sx += xh;
             }
         };
+        if (a.bnb_y.h) {
+            // bf16 y: the item's tile was DMA'd into the staging area during its last step
+            // (conv3x3_fwd_x6r_kernel, x6_dma_bnb_y); lane (h, c) reads channel c of its
+            // pixels (2-byte gathers from HBM ran the data gradient at half the forward's
+            // speed).  The partials of every m-tile first, then the fp32 output leaves
+            // through the same staging area as 16-byte stores of 4 channels (4 per lane and
+            // m-tile instead of 16 4-byte ones; pitch 32 floats: conflict-free both ways)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) {
+                if (wm * MT + mt >= vh) break;  // uniform
+                const __bf16* t16 = reinterpret_cast<const __bf16*>(stg) + mt * 1024 + (lane & 31);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    acc[mt][r] += bv;
+                    part(mt, r, (float)t16[((r & 3) + 8 * (r >> 2) + 4 * h) * 32]);
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // y reads done: reuse the area
+            const int l32 = lane & 31;
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) {
+                const int py = wm * MT + mt;
+                if (py >= vh) break;  // uniform
+#pragma unroll
+                for (int r = 0; r < 16; ++r) stg[((r & 3) + 8 * (r >> 2) + 4 * h) * 32 + l32] = acc[mt][r];
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                const size_t rowb = (size_t)((b * a.H + ty0 + py) * a.W + tx0) * ostride + ocol0 + wn * 32;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int p = (lane >> 3) + 8 * j, k = lane & 7;
+                    const f32x4 v = *reinterpret_cast<const f32x4*>(stg + p * 32 + 4 * k);
+                    if (fullw || p < vw) *reinterpret_cast<f32x4*>(out + rowb + (size_t)p * ostride + 4 * k) = v;
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads before the next m-tile's writes
+            }
+        }
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
             const int py = wm * MT + mt;
             if (py >= vh) break;  // uniform
             if (a.bnb_y.h) {
-                // bf16 y: the item's tile was DMA'd into the staging area during its last
-                // step (conv3x3_fwd_x6r_kernel, x6_dma_bnb_y); lane (h, c) reads channel c
-                // of its pixels (2-byte gathers from HBM ran the data gradient at half the
-                // forward's speed)
-                store_rows(std::integral_constant<bool, false>{}, mt, mt + 1);
-                const __bf16* t16 = reinterpret_cast<const __bf16*>(stg) + mt * 1024 + (lane & 31);
-#pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    part(mt, r, (float)t16[((r & 3) + 8 * (r >> 2) + 4 * h) * 32]);
+                break;  // (done above)
             } else {
                 float yv[16];
                 const size_t yrow = (size_t)((b * a.H + ty0 + py) * a.W + tx0 + 4 * h) * a.Cout + n;
