@@ -214,6 +214,33 @@ int ugpg_bn_relu_bwd_partials(const float* part, int nslots, const float* da, co
                               float* dy, void* dy_bf16, float* dgamma, float* dbeta,
                               float* dconv_bias, int accumulate_params, void* ws, size_t ws_bytes,
                               void* stream);
+/* The same with the last producer of da folded in (its gradient is never stored):
+ * da_eff = da (nullable: no base gradient) + the gradient the route recomputes per pixel,
+ * summed in the order that producer's own entry sums it, so the result is bit-identical
+ * to the producer writing da followed by ugpg_bn_relu_bwd_partials:
+ *   UGPG_ROUTE_MAXPOOL2: MaxPool2d(2)'s backward routes src (NHWC [B][H/2][W/2][C]) to each
+ *     window's argmax pixel (B*H*W == npix); part from ugpg_maxpool2_bwd_partials.
+ *     Replaces max_pool2d_with_indices_backward behind Down (UG_unet_parts.py:45-52).
+ *   UGPG_ROUTE_HEAD: the 1x1 head's input gradient sum_k src[p][k] * w[k][c] (src = dh,
+ *     [npix][nc]; w [nc][C]); part from ugpg_head_bwd_bnb with accumulate_da bit 2
+ *     (UGPG_HEAD_DA_DEFERRED).  Replaces OutConv's input gradient (UG_unet_parts.py:84-90). */
+#define UGPG_ROUTE_MAXPOOL2 1
+#define UGPG_ROUTE_HEAD 2
+typedef struct {
+    int kind;               /* UGPG_ROUTE_* */
+    const float* src;       /* the pooled output's gradient, or the head's dh (fp32) */
+    const uint8_t* argmax;  /* MAXPOOL2: ugpg_maxpool2_fwd's window argmax, src's shape */
+    const float* w;         /* HEAD: the head weight [nc][C] */
+    int nc;                 /* HEAD: classes (1..4) */
+    int B, H, W;            /* MAXPOOL2: the pooled input's (= the BatchNorm's) shape */
+} ugpg_bwd_route_t;
+int ugpg_bn_relu_bwd_partials_routed(const ugpg_bwd_route_t* route, const float* part,
+                                     int nslots, const float* da, const float* y,
+                                     const void* y_bf16, int64_t npix, int C, const float* mean,
+                                     const float* invstd, const float* scale, const float* shift,
+                                     float* dy, void* dy_bf16, float* dgamma, float* dbeta,
+                                     float* dconv_bias, int accumulate_params, void* ws,
+                                     size_t ws_bytes, void* stream);
 int ugpg_bn_relu_bwd(const float* da, const float* y, const void* y_bf16, int64_t npix, int C,
                      const float* mean, const float* invstd, const float* scale,
                      const float* shift, float* dy, void* dy_bf16, float* dgamma, float* dbeta,
@@ -232,6 +259,12 @@ int ugpg_maxpool2_bwd(const float* dout, const uint8_t* argmax, int B, int H, in
 /* The same, also writing the BatchNorm-backward partials of din (see ugpg_bnb_t). */
 int ugpg_maxpool2_bwd_bnb(const float* dout, const uint8_t* argmax, int B, int H, int W, int C,
                           float* din, int accumulate, const ugpg_bnb_t* bnb, void* stream);
+/* Only the BatchNorm-backward partials of din_base (nullable: zero) + the routed gradient;
+ * nothing is written but bnb->part.  The apply recomputes the routing
+ * (ugpg_bn_relu_bwd_partials_routed), so the pool's full-resolution gradient never goes
+ * to HBM. */
+int ugpg_maxpool2_bwd_partials(const float* dout, const uint8_t* argmax, int B, int H, int W,
+                               int C, const float* din_base, const ugpg_bnb_t* bnb, void* stream);
 
 /* ---- align_corners=True bilinear resize, NHWC (UG_unet_parts.py:78, K9) ---- */
 /* out == NULL: the result is stored in bf16 at out_bf16 (the bf16 arithmetic's storage of
@@ -285,7 +318,11 @@ int ugpg_head_bwd(ugpg_src_t src, int64_t npix, const float* w, int nc, const fl
                   float* dw, float* db, float* da, int accumulate_da, void* ws, size_t ws_bytes,
                   void* stream);
 /* The same, also writing the BatchNorm-backward partials of da (ugpg_bnb_t; bnb->y must
- * be src.data, the BN input the head reads lazily): nslots = ugpg_head_bwd_bnb_slots. */
+ * be src.data, the BN input the head reads lazily): nslots = ugpg_head_bwd_bnb_slots.
+ * accumulate_da | UGPG_HEAD_DA_DEFERRED: da is not written (read as the base gradient when
+ * accumulate_da & 1; may be NULL otherwise) -- the partials are those of base + dh @ w,
+ * which ugpg_bn_relu_bwd_partials_routed(UGPG_ROUTE_HEAD) recomputes. */
+#define UGPG_HEAD_DA_DEFERRED 2
 int ugpg_head_bwd_bnb_slots(int64_t npix);
 int ugpg_head_bwd_bnb(ugpg_src_t src, int64_t npix, const float* w, int nc, const float* dh,
                       float* dw, float* db, float* da, int accumulate_da, void* ws,

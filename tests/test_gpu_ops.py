@@ -320,6 +320,40 @@ def test_maxpool2_bwd_fused_bn_partials(dev, C, acc):
         close(a_, b_, 1e-5, f"maxpool-fused partials: {name}")
 
 
+@pytest.mark.parametrize("C,acc,H,W,y16", [(64, 0, 18, 22, False), (64, 1, 19, 22, False),
+                                           (128, 1, 18, 21, True), (512, 0, 8, 8, True),
+                                           (64, 1, 32, 32, True)])
+def test_maxpool2_bwd_deferred_route_bit_identical(dev, C, acc, H, W, y16):
+    """maxpool2_bwd(defer=True) + bn_relu_bwd(route=...) -- the routed gradient recomputed by
+    the apply, never stored -- equals maxpool2_bwd(bnb=...) writing din followed by
+    bn_relu_bwd(part=...) bit for bit (fp32 and bf16 storage of y, odd sizes, with and
+    without a base gradient)."""
+    from ugpg import ops
+    B = 2
+    x = nhwc(rnd((B, C, H, W), 60, "x")).to(dev)
+    _, am = ops.maxpool2_fwd(ops.Act(x))
+    dout = nhwc(rnd((B, C, H // 2, W // 2), 61, "dp")).to(dev)
+    base = nhwc(rnd((B, C, H, W), 62, "base")).to(dev)
+    y = nhwc(rnd((B, C, H, W), 63, "y") * 2 + 0.3).to(dev)
+    if y16:
+        y = y.to(torch.bfloat16)
+    st = [rnd((C,), 64 + i, f"s{i}").abs().to(dev) + 0.1 for i in range(4)]
+    st[3] = st[3] - 0.5
+    outs = []
+    for defer in (False, True):
+        d = base.clone()
+        part = ops.maxpool2_bwd(dout, am, H, W, d, acc, bnb=(y, *st), defer=defer)
+        if defer:
+            assert torch.equal(d, base)  # nothing written
+        dy = torch.empty(d.shape, device=dev, dtype=torch.bfloat16 if y16 else torch.float32)
+        dg, dbt, dcb = (torch.empty(C, device=dev) for _ in range(3))
+        ops.bn_relu_bwd(d if (acc or not defer) else None, y, *st, dy, dg, dbt, dcb, part=part,
+                        route=("pool", dout, am, H, W) if defer else None)
+        outs.append((part.cpu(), dy.cpu(), dg.cpu(), dbt.cpu(), dcb.cpu()))
+    for name, a_, b_ in zip(("partials", "dy", "dgamma", "dbeta", "dconv_bias"), *outs):
+        assert torch.equal(a_, b_), f"deferred pool backward differs: {name}"
+
+
 @pytest.mark.parametrize("C,nc,acc", [(64, 1, 0), (64, 2, 1), (128, 1, 1)])
 def test_head_bwd_fused_bn_partials(dev, C, nc, acc):
     """head_bwd(bnb=...) = head_bwd + the standalone BatchNorm-backward reduction."""
@@ -344,6 +378,39 @@ def test_head_bwd_fused_bn_partials(dev, C, nc, acc):
     assert all(torch.equal(x_, y_) for x_, y_ in zip(res[0][:3], res[1][:3]))
     for name, a_, b_ in zip(("dy", "dgamma", "dbeta"), res[0][3:], res[1][3:]):
         close(a_, b_, 1e-5, f"head-fused partials: {name}")
+
+
+@pytest.mark.parametrize("C,nc,acc,y16", [(64, 1, 0, False), (64, 2, 1, False), (128, 1, 1, True),
+                                          (64, 4, 0, True), (256, 3, 1, False)])
+def test_head_bwd_deferred_route_bit_identical(dev, C, nc, acc, y16):
+    """head_bwd(bnb=..., defer=True) + bn_relu_bwd(route=("head", dh, w)) -- the head's input
+    gradient recomputed by the apply, never stored -- equals head_bwd(bnb=...) writing da
+    followed by bn_relu_bwd(part=...) bit for bit, dW and db included."""
+    from ugpg import ops
+    B, H, W = 2, 20, 24
+    y = nhwc(rnd((B, C, H, W), 80, "y") * 2 + 0.3).to(dev)
+    if y16:
+        y = y.to(torch.bfloat16)
+    mean, invstd = rnd((C,), 81, "m").to(dev), rnd((C,), 82, "i").abs().to(dev) + 0.2
+    sc, sh = rnd((C,), 83, "s").abs().to(dev) + 0.1, rnd((C,), 84, "h").to(dev)
+    a = ops.Act(y, sc, sh)
+    w = rnd((nc, C), 85, "w", 0.1).to(dev)
+    dh = rnd((B * H * W, nc), 86, "dh").to(dev)
+    base = nhwc(rnd((B, C, H, W), 87, "base")).to(dev)
+    res = []
+    for defer in (False, True):
+        da = base.clone()
+        dw, db = torch.empty(nc, C, device=dev), torch.empty(nc, device=dev)
+        part = ops.head_bwd(a, w, dh, dw, db, da, acc, bnb=(mean, invstd), defer=defer)
+        if defer:
+            assert torch.equal(da, base)  # nothing written
+        dy = torch.empty(da.shape, device=dev, dtype=torch.bfloat16 if y16 else torch.float32)
+        dg, dbt, dcb = (torch.empty(C, device=dev) for _ in range(3))
+        ops.bn_relu_bwd(da if (acc or not defer) else None, y, mean, invstd, sc, sh, dy, dg, dbt,
+                        dcb, part=part, route=("head", dh, w) if defer else None)
+        res.append((part.cpu(), dw.cpu(), db.cpu(), dy.cpu(), dg.cpu(), dbt.cpu(), dcb.cpu()))
+    for name, a_, b_ in zip(("partials", "dw", "db", "dy", "dgamma", "dbeta", "dconv_bias"), *res):
+        assert torch.equal(a_, b_), f"deferred head backward differs: {name}"
 
 
 @pytest.mark.parametrize("h,C,acc", [(16, 512, 0), (32, 256, 1), (13, 64, 1)])

@@ -234,18 +234,91 @@ __global__ void bn_bwd_finalize_kernel(const float* part, int nblk, int C, int64
 // TY: the storage of y (float, or __bf16 under the bf16 arithmetic)
 // TO: the storage of dy (float, or __bf16 = RNE of the same fp32 value: under the bf16
 // arithmetic exactly what the data and weight gradients read)
-template <bool NT, typename TY, typename TO>
+// ROUTE (ugpg_bn_relu_bwd_partials_routed): da is recomputed here from what its last
+// producer read instead of read back from HBM, then the base gradient (da != NULL) added --
+// the same values summed in the same order as that producer, so the result is
+// bit-identical to the producer writing da and this kernel reading it.
+//   ROUTE_POOL: dout[pooled pixel] where the window's argmax selects this pixel (else 0)
+//   ROUTE_HEAD: sum_k dh[p][k] * w[k][c], products and sums rounded separately, k in order
+constexpr int ROUTE_NONE = 0, ROUTE_POOL = 1, ROUTE_HEAD = 2;
+// g + d*w with the product rounded (head_bwd_kernel's arithmetic; ops.hip is built without
+// contraction, this file with it)
+__device__ __forceinline__ float add_prod_rn(float g, float d, float w) {
+#pragma clang fp contract(off)
+    return g + d * w;
+}
+struct Route {
+    const float* src;   // POOL: NHWC [B][H/2][W/2][C]; HEAD: dh [npix][nc]
+    const uint8_t* am;  // POOL: the window argmax (maxpool2_fwd)
+    const float* w;     // HEAD: [nc][C]
+    int nc, H, W;
+};
+template <bool NT, typename TY, typename TO, int ROUTE = ROUTE_NONE>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const float* da, const TY* __restrict__ y,
                                                            int64_t npix, int C, const float* mean,
                                                            const float* invstd, const float* scale,
                                                            const float* shift, const float* coef,
-                                                           TO* dy) {
+                                                           TO* dy, Route rt = {}) {
     const int64_t n4 = npix * C / 4;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i0 >= n4) return;
     auto ld4 = [](const float* p, int c) { return *reinterpret_cast<const f32x4*>(p + c); };
     const int c = (int)((i0 * 4) % C);  // fixed: stride * 4 is a multiple of C
+    // ROUTE: this thread's pixel pi, advanced by pstride pixels per grid stride; POOL also
+    // keeps its (x, row, image) position, stepped without divisions
+    const uint32_t pix0 = (uint32_t)((i0 * 4) / C), pstride = (uint32_t)(stride * 4 / C);
+    const uint32_t W = (uint32_t)rt.W, H = (uint32_t)rt.H, Ho = H / 2, Wo = W / 2;
+    uint32_t px = 0, py = 0, pb = 0, xs = 0, ys = 0, bs = 0;
+    if constexpr (ROUTE == ROUTE_POOL) {
+        px = pix0 % W;
+        py = (pix0 / W) % H;
+        pb = pix0 / W / H;
+        xs = pstride % W;
+        ys = (pstride / W) % H;
+        bs = pstride / W / H;
+    }
+    auto advance = [&]() {
+        if constexpr (ROUTE == ROUTE_POOL) {
+            px += xs;
+            const uint32_t carry = px >= W ? 1u : 0u;
+            px -= carry * W;
+            py += ys + carry;
+            const uint32_t cy = py >= H ? 1u : 0u;
+            py -= cy * H;
+            pb += bs + cy;
+        }
+    };
+    f32x4 wv[4];
+    if constexpr (ROUTE == ROUTE_HEAD)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (k < rt.nc) wv[k] = ld4(rt.w + (size_t)k * C, c);
+    auto routed = [&](uint32_t p) {
+        f32x4 g = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (ROUTE == ROUTE_HEAD) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (k >= rt.nc) break;
+                const float d = rt.src[(size_t)p * rt.nc + k];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) g[j] = add_prod_rn(g[j], d, wv[k][j]);
+            }
+            return g;
+        }
+        const uint32_t oy = py >> 1, ox = px >> 1;
+        if (oy < Ho && ox < Wo) {
+            const int k = (int)((py & 1) * 2 + (px & 1));
+            const size_t o = ((size_t)(pb * Ho + oy) * Wo + ox) * C + c;
+            const f32x4 d = *reinterpret_cast<const f32x4*>(rt.src + o);
+            const uchar4 m = *reinterpret_cast<const uchar4*>(rt.am + o);
+            g[0] = m.x == k ? d[0] : 0.f;
+            g[1] = m.y == k ? d[1] : 0.f;
+            g[2] = m.z == k ? d[2] : 0.f;
+            g[3] = m.w == k ? d[3] : 0.f;
+        }
+        return g;
+    };
     const f32x4 sc = ld4(scale, c), sh = ld4(shift, c), mu = ld4(mean, c), is = ld4(invstd, c),
                 k0 = ld4(coef, c), k1 = ld4(coef, C + c);
     auto one = [&](f32x4 d, f32x4 v) {
@@ -283,19 +356,34 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const float* da, cons
                          __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
         }
     };
+    auto DA = [&](int64_t k, uint32_t p) {  // da (read once: streaming load)
+        if constexpr (ROUTE != ROUTE_NONE) {
+            f32x4 g = routed(p);
+            if (da) g += NT ? __builtin_nontemporal_load(D + k) : D[k];
+            return g;
+        } else {
+            return NT ? __builtin_nontemporal_load(D + k) : D[k];
+        }
+    };
     int64_t i = i0;
+    uint32_t pi = pix0;
     for (; i + 3 * stride < n4; i += 4 * stride) {
         f32x4 d[4], v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            // da and y are read once: streaming loads (NT)
-            d[u] = NT ? __builtin_nontemporal_load(D + i + u * stride) : D[i + u * stride];
+            d[u] = DA(i + u * stride, pi);
             v[u] = Y(i + u * stride);
+            pi += pstride;
+            advance();
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) store(i + u * stride, one(d[u], v[u]));
     }
-    for (; i < n4; i += stride) store(i, one(D[i], Y(i)));
+    for (; i < n4; i += stride) {
+        store(i, one(DA(i, pi), Y(i)));
+        pi += pstride;
+        advance();
+    }
 }
 
 __global__ void bn_relu_apply_kernel(YRef x, const float* sc, const float* sh,
@@ -320,21 +408,38 @@ static unsigned apply_grid(int64_t n4) {
 }
 // the apply reads da and y with streaming (nontemporal) loads -- their last use -- so dy,
 // read next by the data and weight gradients, stays in the caches (step -0.55 %)
+template <int ROUTE>
+void launch_bn_apply_t(unsigned ga, hipStream_t st, const float* da, YRef y, int64_t npix,
+                       int C, const float* mean, const float* invstd, const float* scale,
+                       const float* shift, const float* coef, float* dy, __bf16* dy16,
+                       Route rt) {
+    if (y.f && dy)
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<true, float, float, ROUTE>), dim3(ga), dim3(256),
+                           0, st, da, y.f, npix, C, mean, invstd, scale, shift, coef, dy, rt);
+    else if (y.f)
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<true, float, __bf16, ROUTE>), dim3(ga), dim3(256),
+                           0, st, da, y.f, npix, C, mean, invstd, scale, shift, coef, dy16, rt);
+    else if (dy)
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<true, __bf16, float, ROUTE>), dim3(ga), dim3(256),
+                           0, st, da, y.h, npix, C, mean, invstd, scale, shift, coef, dy, rt);
+    else
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<true, __bf16, __bf16, ROUTE>), dim3(ga),
+                           dim3(256), 0, st, da, y.h, npix, C, mean, invstd, scale, shift, coef,
+                           dy16, rt);
+}
 void launch_bn_apply(unsigned ga, hipStream_t st, const float* da, YRef y, int64_t npix,
                      int C, const float* mean, const float* invstd, const float* scale,
-                     const float* shift, const float* coef, float* dy, __bf16* dy16) {
-    if (y.f && dy)
-        hipLaunchKernelGGL((bn_bwd_apply_kernel<true, float, float>), dim3(ga), dim3(256), 0, st,
-                           da, y.f, npix, C, mean, invstd, scale, shift, coef, dy);
-    else if (y.f)
-        hipLaunchKernelGGL((bn_bwd_apply_kernel<true, float, __bf16>), dim3(ga), dim3(256), 0, st,
-                           da, y.f, npix, C, mean, invstd, scale, shift, coef, dy16);
-    else if (dy)
-        hipLaunchKernelGGL((bn_bwd_apply_kernel<true, __bf16, float>), dim3(ga), dim3(256), 0, st,
-                           da, y.h, npix, C, mean, invstd, scale, shift, coef, dy);
+                     const float* shift, const float* coef, float* dy, __bf16* dy16,
+                     int kind = ROUTE_NONE, Route rt = {}) {
+    if (kind == ROUTE_POOL)
+        launch_bn_apply_t<ROUTE_POOL>(ga, st, da, y, npix, C, mean, invstd, scale, shift, coef,
+                                      dy, dy16, rt);
+    else if (kind == ROUTE_HEAD)
+        launch_bn_apply_t<ROUTE_HEAD>(ga, st, da, y, npix, C, mean, invstd, scale, shift, coef,
+                                      dy, dy16, rt);
     else
-        hipLaunchKernelGGL((bn_bwd_apply_kernel<true, __bf16, __bf16>), dim3(ga), dim3(256), 0, st,
-                           da, y.h, npix, C, mean, invstd, scale, shift, coef, dy16);
+        launch_bn_apply_t<ROUTE_NONE>(ga, st, da, y, npix, C, mean, invstd, scale, shift, coef,
+                                      dy, dy16, rt);
 }
 constexpr int64_t kBwdBlocks = 2048, kBwdPpt = 8;
 namespace {
@@ -451,16 +556,17 @@ extern "C" size_t ugpg_bn_relu_bwd_partials_workspace(int C) {
     return C > 0 ? (size_t)2 * C * sizeof(float) : 0;
 }
 
-// finalize + apply of ugpg_bn_relu_bwd from partials a data gradient wrote (bnb_part)
-extern "C" int ugpg_bn_relu_bwd_partials(const float* part, int nslots, const float* da,
-                                         const float* y_f32, const void* y_bf16, int64_t npix,
-                                         int C, const float* mean, const float* invstd,
-                                         const float* scale, const float* shift, float* dy,
-                                         void* dy_bf16, float* dgamma, float* dbeta, float* dbias,
-                                         int acc, void* ws, size_t ws_bytes, void* stream) {
+// finalize + apply of ugpg_bn_relu_bwd from partials a data gradient wrote (bnb_part);
+// rt: da routed from a max-pool's output gradient (da = NULL: no base gradient)
+static int bn_relu_bwd_partials(int kind, const Route& rt, const float* part, int nslots,
+                                const float* da, const float* y_f32, const void* y_bf16,
+                                int64_t npix, int C, const float* mean, const float* invstd,
+                                const float* scale, const float* shift, float* dy, void* dy_bf16,
+                                float* dgamma, float* dbeta, float* dbias, int acc, void* ws,
+                                size_t ws_bytes, void* stream) {
     const YRef y = yref(y_f32, y_bf16);
-    if (!part || nslots <= 0 || !da || (!y.f && !y.h) || !dy == !dy_bf16 || !mean || !invstd ||
-        !scale || !shift || C % 4 || C <= 0 || C > 1024 || npix <= 0) {
+    if (!part || nslots <= 0 || (!da && kind == ROUTE_NONE) || (!y.f && !y.h) || !dy == !dy_bf16 || !mean ||
+        !invstd || !scale || !shift || C % 4 || C <= 0 || C > 1024 || npix <= 0) {
         set_error("bn_relu_bwd_partials: bad arguments (C=%d nslots=%d)", C, nslots);
         return UGPG_ERR_INVALID;
     }
@@ -477,8 +583,42 @@ extern "C" int ugpg_bn_relu_bwd_partials(const float* part, int nslots, const fl
     const unsigned q = (unsigned)(C / std::gcd(1024, C));
     const unsigned ga = (apply_grid(npix * C / 4) + q - 1) / q * q;
     launch_bn_apply(ga, st, da, y, npix, C, mean, invstd, scale, shift, coef, dy,
-                    static_cast<__bf16*>(dy_bf16));
+                    static_cast<__bf16*>(dy_bf16), kind, rt);
     return check_launch("bn_bwd_apply");
+}
+
+extern "C" int ugpg_bn_relu_bwd_partials(const float* part, int nslots, const float* da,
+                                         const float* y_f32, const void* y_bf16, int64_t npix,
+                                         int C, const float* mean, const float* invstd,
+                                         const float* scale, const float* shift, float* dy,
+                                         void* dy_bf16, float* dgamma, float* dbeta, float* dbias,
+                                         int acc, void* ws, size_t ws_bytes, void* stream) {
+    return bn_relu_bwd_partials(ROUTE_NONE, Route{}, part, nslots, da, y_f32, y_bf16, npix, C, mean, invstd,
+                                scale, shift, dy, dy_bf16, dgamma, dbeta, dbias, acc, ws,
+                                ws_bytes, stream);
+}
+
+extern "C" int ugpg_bn_relu_bwd_partials_routed(const ugpg_bwd_route_t* route, const float* part,
+                                                int nslots, const float* da, const float* y_f32,
+                                                const void* y_bf16, int64_t npix, int C,
+                                                const float* mean, const float* invstd,
+                                                const float* scale, const float* shift, float* dy,
+                                                void* dy_bf16, float* dgamma, float* dbeta,
+                                                float* dbias, int acc, void* ws, size_t ws_bytes,
+                                                void* stream) {
+    const bool pool = route && route->kind == UGPG_ROUTE_MAXPOOL2 && route->argmax &&
+                      route->B > 0 && route->H > 0 && route->W > 0 &&
+                      (int64_t)route->B * route->H * route->W == npix;
+    const bool head = route && route->kind == UGPG_ROUTE_HEAD && route->w && route->nc >= 1 &&
+                      route->nc <= 4;
+    if (!route || !route->src || (!pool && !head) || npix > INT32_MAX) {
+        set_error("bn_relu_bwd_partials_routed: bad route (npix=%lld)", (long long)npix);
+        return UGPG_ERR_INVALID;
+    }
+    const Route rt{route->src, route->argmax, route->w, route->nc, route->H, route->W};
+    return bn_relu_bwd_partials(pool ? ROUTE_POOL : ROUTE_HEAD, rt, part, nslots, da, y_f32,
+                                y_bf16, npix, C, mean, invstd, scale, shift, dy, dy_bf16, dgamma,
+                                dbeta, dbias, acc, ws, ws_bytes, stream);
 }
 
 extern "C" int ugpg_bn_relu_apply(ugpg_src_t src, int64_t npix, float* out, void* stream) {

@@ -196,6 +196,9 @@ __global__ void maxpool2_bwd_kernel(const float* dout, const uint8_t* am, int B,
 // maxpool backward fused with the BatchNorm-backward partials of its output (the BN of
 // the block whose activation was pooled: this gather is the last writer of its da).
 // Block = a contiguous pixel range, thread = 4 channels of every slots-th pixel.
+// STORE false: the partials only (din is read when acc, never written) -- the routed
+// gradient is recomputed by the BatchNorm-backward apply (ugpg_bn_relu_bwd_partials_routed)
+template <bool STORE>
 __global__ void __launch_bounds__(256)
     maxpool2_bwd_bnb_kernel(const float* dout, const uint8_t* am, int B, int H, int W, int C,
                             float* din, int acc, BnbArgs bnb) {
@@ -224,7 +227,7 @@ __global__ void __launch_bounds__(256)
             }
             f32x4* dst = reinterpret_cast<f32x4*>(din + p * C + c);
             if (acc) g += *dst;
-            *dst = g;
+            if constexpr (STORE) *dst = g;
             st.add(g, bnb.y.ld4(p * C + c));
         }
     }
@@ -936,8 +939,8 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(YRef x, const float* sc,
                 gw[k][j] += d[k] * v;
             }
             f32x4* dst = reinterpret_cast<f32x4*>(da + p * C + c);
-            if (acc_da) g += *dst;
-            *dst = g;
+            if (acc_da & 1) g += *dst;
+            if (!(acc_da & UGPG_HEAD_DA_DEFERRED)) *dst = g;  // (deferred: the apply recomputes it)
             if constexpr (BNB) bacc[j].add(g, xv[j]);
         }
         if (l16 == 0)
@@ -1603,9 +1606,22 @@ extern "C" int ugpg_maxpool2_bwd_bnb(const float* dout, const uint8_t* am, int B
     UGPG_REQUIRE(dout && am && din && B > 0 && H > 0 && W > 0 &&
                      bnb_args(bnb, (int64_t)B * H * W, C, b),
                  "maxpool2_bwd_bnb");
-    hipLaunchKernelGGL(maxpool2_bwd_bnb_kernel, dim3(b.nblk), dim3(256), 0, as_stream(stream),
-                       dout, am, B, H, W, C, din, acc, b);
+    hipLaunchKernelGGL(maxpool2_bwd_bnb_kernel<true>, dim3(b.nblk), dim3(256), 0,
+                       as_stream(stream), dout, am, B, H, W, C, din, acc, b);
     return check_launch("maxpool2_bwd_bnb");
+}
+
+extern "C" int ugpg_maxpool2_bwd_partials(const float* dout, const uint8_t* am, int B, int H,
+                                          int W, int C, const float* din_base,
+                                          const ugpg_bnb_t* bnb, void* stream) {
+    BnbArgs b;
+    UGPG_REQUIRE(dout && am && B > 0 && H > 0 && W > 0 &&
+                     bnb_args(bnb, (int64_t)B * H * W, C, b),
+                 "maxpool2_bwd_partials");
+    hipLaunchKernelGGL(maxpool2_bwd_bnb_kernel<false>, dim3(b.nblk), dim3(256), 0,
+                       as_stream(stream), dout, am, B, H, W, C, const_cast<float*>(din_base),
+                       din_base ? 1 : 0, b);
+    return check_launch("maxpool2_bwd_partials");
 }
 
 extern "C" int ugpg_bilinear_nhwc_fwd(ugpg_src_t s, int B, int Hi, int Wi, float* out, int Ho,
@@ -1803,8 +1819,10 @@ extern "C" int ugpg_head_bwd_bnb(ugpg_src_t s, int64_t npix, const float* w, int
 static int head_bwd_common(ugpg_src_t s, int64_t npix, const float* w, int nc, const float* dh,
                            float* dw, float* db, float* da, int acc_da, void* ws,
                            size_t ws_bytes, const ugpg_bnb_t* bnbd, void* stream) {
-    UGPG_REQUIRE((s.data || s.data_bf16) && w && dh && dw && da && s.C % 64 == 0 && s.C <= 64 * HEAD_CJ_MAX &&
-                     nc >= 1 && nc <= HEAD_NC_MAX,
+    const bool deferred = acc_da & UGPG_HEAD_DA_DEFERRED;
+    UGPG_REQUIRE((s.data || s.data_bf16) && w && dh && dw && (da || (deferred && !(acc_da & 1))) &&
+                     (!deferred || bnbd) && (acc_da & ~3) == 0 && s.C % 64 == 0 &&
+                     s.C <= 64 * HEAD_CJ_MAX && nc >= 1 && nc <= HEAD_NC_MAX,
                  "head_bwd");
     BnbArgs bnb{};
     if (bnbd) {

@@ -36,6 +36,12 @@ class Bnb(C.Structure):
                 ("shift", _p), ("part", _p), ("nslots", _i)]
 
 
+class BwdRoute(C.Structure):
+    """ugpg_bwd_route_t."""
+    _fields_ = [("kind", _i), ("src", _p), ("argmax", _p), ("w", _p), ("nc", _i), ("B", _i),
+                ("H", _i), ("W", _i)]
+
+
 class PackItem(C.Structure):
     """ugpg_pack_item_t."""
     _fields_ = [("w", _p), ("wpk", _p), ("Cout", _i), ("Cin", _i), ("Cin_pad", _i), ("mode", _i)]
@@ -66,10 +72,13 @@ SIGNATURES = {
     "ugpg_bn_relu_bwd_partials_workspace": (_sz, [_i]),
     "ugpg_bn_relu_bwd_partials": (_i, [_p, _i, _p, _p, _p, _i64, _i, _p, _p, _p, _p, _p, _p, _p,
                                        _p, _p, _i, _p, _sz, _p]),
+    "ugpg_bn_relu_bwd_partials_routed": (_i, [C.POINTER(BwdRoute), _p, _i, _p, _p, _p, _i64, _i, _p,
+                                              _p, _p, _p, _p, _p, _p, _p, _p, _i, _p, _sz, _p]),
     "ugpg_bn_relu_apply": (_i, [Src, _i64, _p, _p]),
     "ugpg_maxpool2_fwd": (_i, [Src, _i, _i, _i, _p, _p, _p, _p]),
     "ugpg_maxpool2_bwd": (_i, [_p, _p, _i, _i, _i, _i, _p, _i, _p]),
     "ugpg_maxpool2_bwd_bnb": (_i, [_p, _p, _i, _i, _i, _i, _p, _i, C.POINTER(Bnb), _p]),
+    "ugpg_maxpool2_bwd_partials": (_i, [_p, _p, _i, _i, _i, _i, _p, C.POINTER(Bnb), _p]),
     "ugpg_bnb_slots": (_i, [_i64, _i]),
     "ugpg_bilinear_nhwc_fwd": (_i, [Src, _i, _i, _i, _p, _i, _i, _p, _p]),
     "ugpg_bilinear_nhwc_bwd": (_i, [_p, _i, _i, _i, _i, _p, _i, _i, _i, _p]),

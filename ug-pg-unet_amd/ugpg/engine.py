@@ -24,6 +24,11 @@ from .ops import Act
 # A/B switch: BN1's backward reduction fused into the data gradient of conv2
 _FUSE_BN_BWD = os.environ.get("UGPG_FUSE_BN_BWD", "1") != "0"
 _FUSE_BN_BWD_MIN_K = int(os.environ.get("UGPG_FUSE_BN_BWD_MIN_K", "64"))
+# A/B switches: the max-pool backward's routed gradient / the last head's input gradient
+# recomputed by the BatchNorm-backward apply instead of written to HBM
+# (maxpool2_bwd / head_bwd(defer=True) + bn_relu_bwd(route=...))
+_DEFER_POOL_BWD = os.environ.get("UGPG_DEFER_POOL_BWD", "1") != "0"
+_DEFER_HEAD_BWD = os.environ.get("UGPG_DEFER_HEAD_BWD", "1") != "0"
 
 
 def _store16(W: int) -> bool:
@@ -64,6 +69,7 @@ class BlockCtx:
     st2: tuple = None
     extra: dict = field(default_factory=dict)
     part2: torch.Tensor = None  # BN2-backward partials written by the last producer of da2
+    route2: tuple = None  # (route, has_base): the deferred last producer of da2 (bn_relu_bwd)
 
 
 def _grad_like(y):
@@ -127,11 +133,13 @@ def double_conv_forward(mod, srcs, ctx: BlockCtx, save: bool):
     return cur[0]
 
 
-def _bn_relu_wgrad(conv, bn, y, st, in_srcs, da, grads, part=None):
+def _bn_relu_wgrad(conv, bn, y, st, in_srcs, da, grads, part=None, route=None):
     """dy = dL/d(conv output) from da = dL/d(relu(bn(y))) -- in place, or, where the bf16
     arithmetic stores the activations in bf16 (y is bf16), into a bf16 tensor: exactly the
     operand its weight and data gradients read -- then dW, db.  Returns dy.
-    part: BatchNorm-backward partials written by the data gradient that produced da."""
+    part: BatchNorm-backward partials written by the data gradient that produced da.
+    route: the deferred last producer of da (BlockCtx.route2): da holds only the base
+    gradient (nothing when route[1] is false) and the apply adds the producer's gradient."""
     mean, invstd, scale, shift = st
     if mean is None:
         raise RuntimeError("backward through an eval-mode BatchNorm is not supported")
@@ -140,8 +148,9 @@ def _bn_relu_wgrad(conv, bn, y, st, in_srcs, da, grads, part=None):
     dy = da
     if y.dtype == torch.bfloat16 and all(s.C % 64 == 0 for s in in_srcs):
         dy = ops.empty(*da.shape, like=da, dtype=torch.bfloat16)
-    ops.bn_relu_bwd(da, y, mean, invstd, scale, shift, dy, grads.get(bn.weight),
-                    grads.get(bn.bias), db, part=part)
+    base = da if route is None or route[1] else None
+    ops.bn_relu_bwd(base, y, mean, invstd, scale, shift, dy, grads.get(bn.weight),
+                    grads.get(bn.bias), db, part=part, route=None if route is None else route[0])
     dw = grads.get(conv.weight)
     if dw is not None:
         co, ci = conv.weight.shape[0], conv.weight.shape[1]
@@ -159,7 +168,8 @@ def double_conv_backward(mod, ctx: BlockCtx, da2, targets, acc_flags, grads, pad
     B, H, W, cout = ctx.y2.shape
     a1 = Act(ctx.y1, ctx.st1[2], ctx.st1[3])
     # stage 2: BN2/ReLU backward, wgrad(conv2), dgrad(conv2) -> dL/d(a1)
-    dy2 = _bn_relu_wgrad(c2, b2, ctx.y2, ctx.st2, [a1], da2, grads, part=ctx.part2)
+    dy2 = _bn_relu_wgrad(c2, b2, ctx.y2, ctx.st2, [a1], da2, grads, part=ctx.part2,
+                         route=ctx.route2)
     cmid = c2.weight.shape[1]
     da1 = ops.empty(B, H, W, cmid, like=da2)
     npix = B * H * W
@@ -326,10 +336,14 @@ class UNetGraph:
                 c = ctxs[hd.block]
                 fuse = (_FUSE_BN_BWD and hd.block not in first_use and last_head[hd.block] == hi
                         and c.st2 is not None and c.st2[0] is not None and a.y is c.y2)
-                part = ops.head_bwd(a, w, dh.contiguous(), dw_flat, db, da[hd.block], acc,
-                                    bnb=c.st2[:2] if fuse else None)
+                dh = dh.contiguous()
+                defer = fuse and _DEFER_HEAD_BWD
+                part = ops.head_bwd(a, w, dh, dw_flat, db, da[hd.block], acc,
+                                    bnb=c.st2[:2] if fuse else None, defer=defer)
                 if part is not None:
                     c.part2 = part
+                if defer:  # the block's BN2-backward apply recomputes dh @ w
+                    c.route2 = (("head", dh, w), acc)
             if on_done is not None:
                 on_done([grads.get(p) for hd in self.heads for p in hd.mod.parameters()])
         else:
@@ -356,9 +370,17 @@ class UNetGraph:
                 if not acc:
                     da[src] = _grad_like(outs[src].y)
                 st = bn2_state(src, bi)
-                part = ops.maxpool2_bwd(dp, ctx.extra["argmax"], H, W, da[src], acc, bnb=st)
-                if part is not None:
-                    ctxs[src].part2 = part
+                am = ctx.extra["argmax"]
+                if st is not None and _DEFER_POOL_BWD:
+                    # the last contribution to da[src]: only its partials here; the apply of
+                    # src's BN2 backward recomputes the routing (no full-resolution write)
+                    ctxs[src].part2 = ops.maxpool2_bwd(dp, am, H, W, da[src], acc, bnb=st,
+                                                       defer=True)
+                    ctxs[src].route2 = (("pool", dp, am, H, W), acc)
+                else:
+                    part = ops.maxpool2_bwd(dp, am, H, W, da[src], acc, bnb=st)
+                    if part is not None:
+                        ctxs[src].part2 = part
             else:
                 skip, low = blk.inputs
                 acc_s = da[skip] is not None

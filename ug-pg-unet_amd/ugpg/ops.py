@@ -11,7 +11,7 @@ import os
 
 import torch
 
-from ._C import Bnb, ConvDesc, PackItem, Src, WgradDesc, check, lib
+from ._C import Bnb, BwdRoute, ConvDesc, PackItem, Src, WgradDesc, check, lib
 
 F32 = torch.float32
 
@@ -351,12 +351,31 @@ def bn_eval_params(gamma, beta, rm, rv, eps, owner=None):
 
 
 def bn_relu_bwd(da, y, mean, invstd, scale, shift, dy, dgamma, dbeta, dconv_bias=None,
-                accumulate=0, part=None):
+                accumulate=0, part=None, route=None):
     """part: partials the data gradient producing `da` wrote (conv3x3_fwd(bnb=...)):
     only the finalize and apply passes run.  dy: fp32, or a bf16 tensor receiving dy
-    rounded to bf16 (what the bf16 arithmetic's data and weight gradients read)."""
+    rounded to bf16 (what the bf16 arithmetic's data and weight gradients read).
+    route: the deferred last producer of da, which returned `part` and wrote no da:
+    ("pool", dout, argmax, H, W) from maxpool2_bwd(defer=True) or ("head", dh, w) from
+    head_bwd(defer=True); the apply adds its gradient to da (da None: nothing to add)."""
     c = y.shape[-1]
     npix = y.numel() // c
+    if route is not None:
+        if route[0] == "pool":
+            _, dout, am, H, W = route
+            r = BwdRoute(1, ptr(dout), ptr(am), None, 0, npix // (H * W), H, W)
+        elif route[0] == "head":
+            _, dh, w = route
+            r = BwdRoute(2, ptr(dh), None, _f32(w), w.shape[0], 0, 0, 0)
+        else:
+            raise ValueError(f"unknown backward route {route[0]!r}")
+        ws = workspace(lib.ugpg_bn_relu_bwd_partials_workspace(c), y.device)
+        check(lib.ugpg_bn_relu_bwd_partials_routed(
+            C.byref(r), ptr(part), part.numel() // (3 * c), ptr(da), *_yargs(y), npix, c, ptr(mean),
+            ptr(invstd), ptr(scale), ptr(shift), *_yargs(dy), ptr(dgamma), ptr(dbeta),
+            ptr(dconv_bias), int(accumulate), ptr(ws), ws.numel(), stream()),
+            "bn_relu_bwd_partials_routed")
+        return
     if part is not None:
         ws = workspace(lib.ugpg_bn_relu_bwd_partials_workspace(c), y.device)
         check(lib.ugpg_bn_relu_bwd_partials(
@@ -396,10 +415,19 @@ def bnb_desc(bn_state, npix, c, like, nslots=None):
     return d, part
 
 
-def maxpool2_bwd(dout, am, H, W, din, accumulate, bnb=None):
+def maxpool2_bwd(dout, am, H, W, din, accumulate, bnb=None, defer=False):
     """bnb: (y, mean, invstd, scale, shift) of the BatchNorm whose output was pooled ->
-    also returns its backward partials (for bn_relu_bwd(part=...))."""
+    also returns its backward partials (for bn_relu_bwd(part=...)).  defer (with bnb): din
+    is not written (read as the base gradient when accumulate); the partials are those of
+    din + the routed gradient, which bn_relu_bwd(part=..., route=(dout, am, H, W))
+    recomputes."""
     B, _, _, c = dout.shape
+    if bnb is not None and defer:
+        d, part = bnb_desc(bnb, B * H * W, c, dout)
+        check(lib.ugpg_maxpool2_bwd_partials(ptr(dout), ptr(am), B, H, W, c,
+                                             ptr(din) if accumulate else None, C.byref(d), stream()),
+              "maxpool2_bwd_partials")
+        return part
     if bnb is not None:
         d, part = bnb_desc(bnb, B * H * W, c, din)
         check(lib.ugpg_maxpool2_bwd_bnb(ptr(dout), ptr(am), B, H, W, c, ptr(din), int(accumulate),
@@ -512,9 +540,11 @@ def heads_split_bwd(dlogits, hres):
     return dhs
 
 
-def head_bwd(a: Act, w, dh, dw, db, da, accumulate, bnb=None):
+def head_bwd(a: Act, w, dh, dw, db, da, accumulate, bnb=None, defer=False):
     """bnb: (mean, invstd) of the BatchNorm behind `a` (its scale/shift are a's) -> also
-    returns the BatchNorm-backward partials of da (for bn_relu_bwd(part=...))."""
+    returns the BatchNorm-backward partials of da (for bn_relu_bwd(part=...)).  defer (with
+    bnb): da is not written (read as the base gradient when accumulate); the partials are
+    those of da + dh @ w, which bn_relu_bwd(part=..., route=("head", dh, w)) recomputes."""
     B, H, W, c = a.shape
     nc = w.shape[0]
     npix = B * H * W
@@ -527,8 +557,9 @@ def head_bwd(a: Act, w, dh, dw, db, da, accumulate, bnb=None):
         d.mean, d.invstd, d.scale, d.shift = (ptr(t) for t in (*bnb, a.scale, a.shift))
         d.part, d.nslots = ptr(part), n
         check(lib.ugpg_head_bwd_bnb(a.src(), npix, _f32(w), nc, ptr(dh), ptr(dw), ptr(db),
-                                    ptr(da), int(accumulate), ptr(ws), ws.numel(), C.byref(d),
-                                    stream()), "head_bwd_bnb")
+                                    ptr(da) if accumulate or not defer else None,
+                                    int(accumulate) | (2 if defer else 0), ptr(ws), ws.numel(),
+                                    C.byref(d), stream()), "head_bwd_bnb")
         return part
     check(lib.ugpg_head_bwd(a.src(), npix, _f32(w), nc, ptr(dh), ptr(dw), ptr(db), ptr(da),
                             int(accumulate), ptr(ws), ws.numel(), stream()), "head_bwd")
