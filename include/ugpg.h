@@ -220,7 +220,7 @@ int ugpg_bn_relu_bwd_partials(const float* part, int nslots, const float* da, co
  * to the producer writing da followed by ugpg_bn_relu_bwd_partials:
  *   UGPG_ROUTE_MAXPOOL2: MaxPool2d(2)'s backward routes src (NHWC [B][H/2][W/2][C]) to each
  *     window's argmax pixel (B*H*W == npix); part from ugpg_maxpool2_bwd_partials.
- *     Replaces max_pool2d_with_indices_backward behind Down (UG_unet_parts.py:45-52).
+ *     Replaces max_pool2d_with_indices_backward behind Down (UG_unet_parts.py:44-55).
  *   UGPG_ROUTE_HEAD: the 1x1 head's input gradient sum_k src[p][k] * w[k][c] (src = dh,
  *     [npix][nc]; w [nc][C]); part from ugpg_head_bwd_bnb with accumulate_da bit 2
  *     (UGPG_HEAD_DA_DEFERRED).  Replaces OutConv's input gradient (UG_unet_parts.py:84-90). */
