@@ -313,6 +313,9 @@ def main():
 
     roof, kernels = (None, None) if timer is None else \
         roofline_from(timer, args.steps, args.roofline_every, ops.conv_math())
+    # the step's whole-FLOP rate against the peak of the arithmetic the convs run
+    step_peak = {"x6": BF16_PEAK_TFLOPS / X6_PRODUCTS, "bf16": BF16_PEAK_TFLOPS}.get(
+        args.conv_math, FP32_PEAK_TFLOPS)
 
     result = {
         "metric": METRIC, "value": round(value, 3), "unit": "images/sec", "n_gpus": world,
@@ -325,11 +328,12 @@ def main():
                    "per_gpu_batch": B, "global_batch": B * world, "resolution": R,
                    "parallelism": f"dp{world}",
                    "baseline_config": ("BASELINE.json configs[2] arithmetic (bf16 conv operands, "
-                                       "fp32 accumulation and storage)" if args.conv_math == "bf16"
+                                       "fp32 accumulation, bf16 activation storage)" if args.conv_math == "bf16"
                                        else "BASELINE.json configs[1]")},
         "step_roofline": {"gflop_per_image": UG_STEP_GFLOP,
                           "achieved_tflops_per_gpu": round(value / world * UG_STEP_GFLOP / 1e3, 2),
-                          "frac_of_fp32_peak": round(value / world * UG_STEP_GFLOP / 1e3 / FP32_PEAK_TFLOPS, 4)},
+                          "peak_tflops": round(step_peak, 1),
+                          "frac": round(value / world * UG_STEP_GFLOP / 1e3 / step_peak, 4)},
         "roofline": roof,
         "kernels": kernels,
         "last_step_metrics": {"loss": last[0], "base_loss": last[1], "dice": last[2],

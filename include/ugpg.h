@@ -62,8 +62,11 @@ typedef struct {
  *                  rounding); needs K channels % 16 == 0 and N % 64 == 0.
  *   UGPG_WFMT_BF16: bf16 arithmetic (BASELINE.json configs[2]) -- operands rounded
  *                  to bf16 (round to nearest even), one v_mfma_f32_32x32x16_bf16
- *                  product per k-step, fp32 accumulation and fp32 storage (what
- *                  torch.autocast(bfloat16) does to a conv); same shape rules.
+ *                  product per k-step, fp32 accumulation; the output is stored in
+ *                  bf16 when out_bf16 is set (out[0] == NULL: 2 bytes per value,
+ *                  BatchNorm partials of the rounded values -- what
+ *                  torch.autocast(bfloat16) does to a conv output), else in fp32
+ *                  (the data gradients); same shape rules.
  * Input = channel-concat of src[0] and src[1] (src[1].data may be NULL):
  * this is the concat-free `torch.cat([x2, x1], dim=1)` of Up (UG_unet_parts.py:80).
  * Cin = src[0].C + src[1].C must be a multiple of 8 (pad the image to 8 channels).

@@ -11,7 +11,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "ug-pg-unet_amd")]
 
 
-def main(outdir, math="x6"):
+def main(outdir, math="x6", exchange="fp32"):
+    os.environ["UGPG_GRAD_BF16"] = "1" if exchange == "bf16" else "0"
     import torch
     import torch.distributed as dist
     from torch.utils.data import DataLoader, TensorDataset
@@ -24,7 +25,7 @@ def main(outdir, math="x6"):
     torch.manual_seed(1000 + rank)               # replicas start different on purpose
     import ugpg
     from ugpg import ops
-    ops.set_conv_math(math)  # "bf16": config 3 -- bf16 convs AND bf16 gradient exchange
+    ops.set_conv_math(math)  # "bf16": config 3's arithmetic (exchange: fp32 default, bf16 opt-in)
     tr = ugpg.UncertaintyGuidedProgressiveTrainer(3, 1, device="cuda", uncertainty_alpha=1.0)
     p0 = {k: v.detach().cpu().clone() for k, v in tr.models[3].state_dict().items()}
     stage = c["stage"]
@@ -71,4 +72,4 @@ def main(outdir, math="x6"):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], *(sys.argv[2:3]))
+    main(sys.argv[1], *(sys.argv[2:4]))

@@ -110,23 +110,27 @@ def test_dp_two_ranks_match_shard_mean(tmp_path):
         assert abs(p.norm().item() - fx[f"post/{k}"][0]) <= 1e-4 * fx[f"post/{k}"][0] + 1e-6, k
 
 
-def test_dp_two_ranks_bf16_exchange(tmp_path):
-    """Config 3's data parallelism on the HIP path: bf16 conv arithmetic AND the bf16
-    gradient exchange (dist._Bf16Work: RNE cast kernels around the all-reduce, summed back
-    into the fp32 flat buffer) in two fresh processes (gloo, both on cuda:0) on the halves
-    of the G8 batch.  The exchanged gradient must equal bf16(bf16(g_0) + bf16(g_1)) of the
-    two ranks' own gradients bit for bit, on both ranks; each rank's own gradient must be
-    the bf16 oracle's for its shard within the bf16 floor rule (the oracle's spread under
-    ulp-level weight perturbations, x3)."""
+@pytest.mark.parametrize("exchange", ["fp32", "bf16"])
+def test_dp_two_ranks_bf16_exchange(tmp_path, exchange):
+    """Config 3's data parallelism on the HIP path: bf16 conv arithmetic in two fresh
+    processes (gloo, both on cuda:0) on the halves of the G8 batch, with the default fp32
+    gradient exchange (the exchanged gradient must equal g_0 + g_1 in fp32) and the opt-in
+    bf16 exchange (dist._Bf16Work: RNE cast kernels around the all-reduce, summed back into
+    the fp32 flat buffer; it must equal bf16(bf16(g_0) + bf16(g_1)) bit for bit), on both
+    ranks; each rank's own gradient must be the bf16 oracle's for its shard within the
+    bf16 floor rule (the oracle's spread under ulp-level weight perturbations, x3)."""
     from oracle.make_goldens import G8 as c
     from tests._parity import FLOOR_PERTURBATIONS
-    res = _run_ranks(tmp_path, "bf16")
+    res = _run_ranks(tmp_path, "bf16", exchange)
     for k, v in res[0]["grads"].items():
         assert torch.equal(v, res[1]["grads"][k]), f"exchanged gradient differs across ranks: {k}"
     for k, v in res[0]["grads"].items():
-        q = lambda t: t.to(torch.bfloat16)
-        want = (q(res[0]["local"][k]).float() + q(res[1]["local"][k]).float()).to(torch.bfloat16)
-        assert torch.equal(v, want.float()), f"bf16 exchange of {k}"
+        if exchange == "bf16":
+            q = lambda t: t.to(torch.bfloat16)
+            want = (q(res[0]["local"][k]).float() + q(res[1]["local"][k]).float()).to(torch.bfloat16)
+        else:
+            want = res[0]["local"][k] + res[1]["local"][k]
+        assert torch.equal(v, want.float()), f"{exchange} exchange of {k}"
     # each rank's own gradient vs the bf16 oracle on its shard
     state = det_state(c["stage"], 3, 1, seed=c["w_seed"])
     prev = det_state(c["stage"] - 1, 3, 1, seed=c["prev_seed"])

@@ -277,7 +277,7 @@ def _oracle_ug(state4, state3, x, y, cw, dtype=torch.float64):
     return oracle(state4, x, y, prev, cw, dtype)
 
 
-@pytest.mark.parametrize("res", [224])
+@pytest.mark.parametrize("res", [224, 256])
 def test_config4_bs16_full_ug_step(dev, res):
     """BASELINE config 4 as the trainer runs it (the bs16 test above feeds random
     `prev` logits): HerlevTrainer.uncertainty_guided_forward_pass at bs16 -- the Stage-3

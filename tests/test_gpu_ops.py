@@ -19,6 +19,16 @@ def nhwc(t):  # NCHW cpu -> NHWC contiguous
     return t.permute(0, 2, 3, 1).contiguous()
 
 
+def rnd_nhwc(shape, seed, name, dev):
+    """NHWC normal tensor on dev: detgen's for small shapes, a seeded device generator for
+    the large ones (bit-identity tests only need fixed inputs)."""
+    B, C, H, W = shape
+    if B * C * H * W > (1 << 22):
+        g = torch.Generator(device=dev).manual_seed(seed)
+        return torch.randn((B, H, W, C), generator=g, device=dev)
+    return nhwc(rnd(shape, seed, name)).to(dev)
+
+
 def nchw(t):
     return t.permute(0, 3, 1, 2).contiguous()
 
@@ -320,21 +330,28 @@ def test_maxpool2_bwd_fused_bn_partials(dev, C, acc):
         close(a_, b_, 1e-5, f"maxpool-fused partials: {name}")
 
 
-@pytest.mark.parametrize("C,acc,H,W,y16", [(64, 0, 18, 22, False), (64, 1, 19, 22, False),
-                                           (128, 1, 18, 21, True), (512, 0, 8, 8, True),
-                                           (64, 1, 32, 32, True)])
-def test_maxpool2_bwd_deferred_route_bit_identical(dev, C, acc, H, W, y16):
+# large shapes: n4 = B*H*W*C/4 above 4x the apply's 524,288-thread grid, so
+# every thread runs the 4-way unrolled loop and steps its (x, row, image) position across
+# row and image boundaries; odd sizes whose pixel count is not a multiple of the grid's
+# pixel stride; the real step's shape (bs16 x 256^2 x 64)
+ROUTE_BIG = [(4, 64, 1, 250, 254, True), (4, 64, 0, 250, 254, False), (3, 64, 1, 255, 253, False),
+             (16, 64, 1, 256, 256, True), (5, 128, 1, 129, 127, True)]
+
+
+@pytest.mark.parametrize("B,C,acc,H,W,y16", [(2, 64, 0, 18, 22, False), (2, 64, 1, 19, 22, False),
+                                             (2, 128, 1, 18, 21, True), (2, 512, 0, 8, 8, True),
+                                             (2, 64, 1, 32, 32, True)] + ROUTE_BIG)
+def test_maxpool2_bwd_deferred_route_bit_identical(dev, B, C, acc, H, W, y16):
     """maxpool2_bwd(defer=True) + bn_relu_bwd(route=...) -- the routed gradient recomputed by
     the apply, never stored -- equals maxpool2_bwd(bnb=...) writing din followed by
     bn_relu_bwd(part=...) bit for bit (fp32 and bf16 storage of y, odd sizes, with and
-    without a base gradient)."""
+    without a base gradient, grid-stride loops over many rows and images)."""
     from ugpg import ops
-    B = 2
-    x = nhwc(rnd((B, C, H, W), 60, "x")).to(dev)
+    x = rnd_nhwc((B, C, H, W), 60, "x", dev)
     _, am = ops.maxpool2_fwd(ops.Act(x))
-    dout = nhwc(rnd((B, C, H // 2, W // 2), 61, "dp")).to(dev)
-    base = nhwc(rnd((B, C, H, W), 62, "base")).to(dev)
-    y = nhwc(rnd((B, C, H, W), 63, "y") * 2 + 0.3).to(dev)
+    dout = rnd_nhwc((B, C, H // 2, W // 2), 61, "dp", dev)
+    base = rnd_nhwc((B, C, H, W), 62, "base", dev)
+    y = rnd_nhwc((B, C, H, W), 63, "y", dev) * 2 + 0.3
     if y16:
         y = y.to(torch.bfloat16)
     st = [rnd((C,), 64 + i, f"s{i}").abs().to(dev) + 0.1 for i in range(4)]
@@ -380,23 +397,26 @@ def test_head_bwd_fused_bn_partials(dev, C, nc, acc):
         close(a_, b_, 1e-5, f"head-fused partials: {name}")
 
 
-@pytest.mark.parametrize("C,nc,acc,y16", [(64, 1, 0, False), (64, 2, 1, False), (128, 1, 1, True),
-                                          (64, 4, 0, True), (256, 3, 1, False)])
-def test_head_bwd_deferred_route_bit_identical(dev, C, nc, acc, y16):
+@pytest.mark.parametrize("B,H,W,C,nc,acc,y16", [(2, 20, 24, 64, 1, 0, False), (2, 20, 24, 64, 2, 1, False),
+                                                (2, 20, 24, 128, 1, 1, True), (2, 20, 24, 64, 4, 0, True),
+                                                (2, 20, 24, 256, 3, 1, False),
+                                                (4, 250, 254, 64, 1, 1, True), (3, 255, 253, 64, 2, 0, False),
+                                                (16, 256, 256, 64, 1, 0, True)])
+def test_head_bwd_deferred_route_bit_identical(dev, B, H, W, C, nc, acc, y16):
     """head_bwd(bnb=..., defer=True) + bn_relu_bwd(route=("head", dh, w)) -- the head's input
     gradient recomputed by the apply, never stored -- equals head_bwd(bnb=...) writing da
-    followed by bn_relu_bwd(part=...) bit for bit, dW and db included."""
+    followed by bn_relu_bwd(part=...) bit for bit, dW and db included (large shapes: the
+    apply's grid-stride loop)."""
     from ugpg import ops
-    B, H, W = 2, 20, 24
-    y = nhwc(rnd((B, C, H, W), 80, "y") * 2 + 0.3).to(dev)
+    y = rnd_nhwc((B, C, H, W), 80, "y", dev) * 2 + 0.3
     if y16:
         y = y.to(torch.bfloat16)
     mean, invstd = rnd((C,), 81, "m").to(dev), rnd((C,), 82, "i").abs().to(dev) + 0.2
     sc, sh = rnd((C,), 83, "s").abs().to(dev) + 0.1, rnd((C,), 84, "h").to(dev)
     a = ops.Act(y, sc, sh)
     w = rnd((nc, C), 85, "w", 0.1).to(dev)
-    dh = rnd((B * H * W, nc), 86, "dh").to(dev)
-    base = nhwc(rnd((B, C, H, W), 87, "base")).to(dev)
+    dh = rnd_nhwc((B, nc, H, W), 86, "dh", dev).reshape(B * H * W, nc)
+    base = rnd_nhwc((B, C, H, W), 87, "base", dev)
     res = []
     for defer in (False, True):
         da = base.clone()

@@ -2,12 +2,11 @@
 bench's workload, alternating blocks of steps between two settings so that clock drift
 (DVFS, temperature) hits both sides alike.
 
-    python tools/ab_step.py --a "engine._FUSE_BN_BWD=0" --b "engine._FUSE_BN_BWD=1"
     python tools/ab_step.py --a "lib:exp/a.so" --b "lib:exp/b.so"
 
-A setting is `module._NAME=value` (an attribute of ugpg.<module>, int-valued) or
-`lib:path` (a libugpg build, e.g. a `build.py -D ... --out` variant); several
-comma-separated.
+A setting is `lib:path` (a libugpg build, e.g. a `build.py -D ... --out` variant) or
+`module._NAME=value` (an int-valued attribute of ugpg.<module>, for a local experiment
+patch: the shipped Python layer has no A/B switches); several comma-separated.
 """
 import argparse
 import os

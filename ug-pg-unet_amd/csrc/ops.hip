@@ -771,7 +771,6 @@ struct HeadSet {
 // indices / weights computed once per head, 32-bit offsets within a head; the same
 // arithmetic and head order as before (per output: ly0*(lx0*a + lx1*b) + ly1*(...), summed
 // over heads in order), so the logits are bit-identical to the one-output-per-thread form.
-#ifndef HEADS_COMBINE_V1
 __global__ void __launch_bounds__(256) heads_combine_kernel(HeadSet hs, int B, int H, int W, int nc,
                                                             float* logits) {
     const int W4 = W >> 2;
@@ -814,8 +813,10 @@ __global__ void __launch_bounds__(256) heads_combine_kernel(HeadSet hs, int B, i
         *reinterpret_cast<f32x4*>(logits + r * W + x0o) = s;
     }
 }
-#else
-__global__ void heads_combine_kernel(HeadSet hs, int B, int H, int W, int nc, float* logits) {
+
+// One output per thread: widths that are not a multiple of 4 (any even width reaches here
+// through PGUNet1's single max-pool, as in the reference).  Same arithmetic and order.
+__global__ void heads_combine1_kernel(HeadSet hs, int B, int H, int W, int nc, float* logits) {
     const int64_t total = (int64_t)B * nc * H * W;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
          i += (int64_t)gridDim.x * blockDim.x) {
@@ -844,7 +845,6 @@ __global__ void heads_combine_kernel(HeadSet hs, int B, int H, int W, int nc, fl
         logits[i] = s;
     }
 }
-#endif
 
 // dh (NHWC, R x R, nc) from NCHW dlogits (H x W): the transpose of the align-corners
 // upsample R -> H.  One block per (b, iy); for R < 256 the threads split the output
@@ -1763,14 +1763,13 @@ extern "C" int ugpg_heads_combine(const float* const* h, const int* hres, int n,
         hs.h[i] = i < n ? h[i] : nullptr;
         hs.res[i] = i < n ? hres[i] : 0;
     }
-#ifndef HEADS_COMBINE_V1
-    UGPG_REQUIRE(W % 4 == 0, "heads_combine: width");
-    const int64_t total = (int64_t)B * nc * H * W / 4;
-#else
     const int64_t total = (int64_t)B * nc * H * W;
-#endif
-    hipLaunchKernelGGL(heads_combine_kernel, dim3(stream_grid(total)), dim3(256), 0,
-                       as_stream(stream), hs, B, H, W, nc, logits);
+    if (W % 4 == 0)
+        hipLaunchKernelGGL(heads_combine_kernel, dim3(stream_grid(total / 4)), dim3(256), 0,
+                           as_stream(stream), hs, B, H, W, nc, logits);
+    else
+        hipLaunchKernelGGL(heads_combine1_kernel, dim3(stream_grid(total)), dim3(256), 0,
+                           as_stream(stream), hs, B, H, W, nc, logits);
     return check_launch("heads_combine");
 }
 

@@ -254,13 +254,12 @@ _SIDE = None
 
 
 def grad_bf16() -> bool:
-    """Exchange gradient buckets in bf16 (BASELINE configs[2], 'bf16 DP')?  UGPG_GRAD_BF16
-    = 1 / 0, default: with the bf16 conv arithmetic (ops.set_conv_math("bf16"))."""
-    v = os.environ.get("UGPG_GRAD_BF16", "auto")
-    if v == "auto":
-        from . import ops
-        return ops.conv_math() == "bf16"
-    return v == "1"
+    """Exchange gradient buckets in bf16?  Opt-in only (UGPG_GRAD_BF16=1).  The default is
+    fp32 for every arithmetic, as torch's DDP under autocast exchanges the fp32 .grad: the
+    bf16 exchange errs by up to 2^-8 * sum_r |g_r| per element, above the config-3 parity
+    floor (G4c) of the output heads at any N > 1 (tests/test_dist_gloo.py::
+    test_bf16_exchange_error_bound)."""
+    return os.environ.get("UGPG_GRAD_BF16", "0") == "1"
 
 
 class _Bf16Work:
@@ -410,25 +409,39 @@ def _has_distributed_sampler(loader) -> bool:
     return False
 
 
-def check_same_batch(t: torch.Tensor):
-    """Raise unless every rank holds the same global batch `t` (a float64 checksum,
-    all-reduced MAX of (s, -s)).  Without a DistributedSampler the ranks must draw
-    identical batches (same shuffle seed and augmentation RNG); a per-rank seed would
-    otherwise train silently on overlapping shards.  One tiny collective per call."""
+def _batch_checksum(t: torch.Tensor) -> float:
+    """Order-sensitive float64 checksum of a batch: each row's sum weighted by its position
+    (1..n), so two ranks holding the same rows in a different order -- which shard_batch
+    would split into different, overlapping shards -- disagree."""
+    if t.dim() == 0 or t.shape[0] == 0:
+        return float(t.detach().double().sum().item())
+    rows = t.detach().double().reshape(t.shape[0], -1).sum(1)
+    w = torch.arange(1, t.shape[0] + 1, dtype=torch.float64, device=rows.device)
+    return float((rows * w).sum().item())
+
+
+def check_same_batch(*tensors: torch.Tensor):
+    """Raise unless every rank holds the same global batch (inputs and targets: an
+    order-sensitive float64 checksum per tensor, all-reduced MAX of (s, -s)).  Without a
+    DistributedSampler the ranks must draw identical batches (same shuffle seed and
+    augmentation RNG); a per-rank seed would otherwise train silently on overlapping
+    shards.  One tiny collective per call."""
     _, ws = world()
     if ws <= 1:
         return
-    s = float(t.detach().double().sum().item())
+    sums = [_batch_checksum(t) for t in tensors]
     dev = torch.device("cuda", torch.cuda.current_device()) \
         if dist.get_backend() == "nccl" else torch.device("cpu")
-    v = torch.tensor([s, -s], dtype=torch.float64, device=dev)
+    v = torch.tensor(sums + [-s for s in sums], dtype=torch.float64, device=dev)
     dist.all_reduce(v, op=dist.ReduceOp.MAX)
-    hi, lo = float(v[0]), -float(v[1])
-    if hi - lo > 1e-6 * max(1.0, abs(hi)):
-        raise RuntimeError(
-            "ugpg data parallel: ranks drew different global batches (checksums "
-            f"{lo!r} .. {hi!r}); seed the DataLoader / augmentation identically on every "
-            "rank or use a DistributedSampler")
+    n = len(sums)
+    for i in range(n):
+        hi, lo = float(v[i]), -float(v[n + i])
+        if hi - lo > 1e-6 * max(1.0, abs(hi)):
+            raise RuntimeError(
+                "ugpg data parallel: ranks drew different global batches (checksums "
+                f"{lo!r} .. {hi!r}); seed the DataLoader / augmentation identically on every "
+                "rank or use a DistributedSampler")
 
 
 def shard_batch(loader, *tensors, check=False):
@@ -445,7 +458,7 @@ def shard_batch(loader, *tensors, check=False):
     if ws <= 1 or _has_distributed_sampler(loader):
         return tensors
     if check:
-        check_same_batch(tensors[0])
+        check_same_batch(*tensors)
     n = tensors[0].shape[0]
     per = n // ws
     if per == 0:

@@ -13,22 +13,12 @@ PyTorch arithmetic runs anywhere on the path.
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass, field
 
 import torch
 
 from . import ops
 from .ops import Act
-
-# A/B switch: BN1's backward reduction fused into the data gradient of conv2
-_FUSE_BN_BWD = os.environ.get("UGPG_FUSE_BN_BWD", "1") != "0"
-_FUSE_BN_BWD_MIN_K = int(os.environ.get("UGPG_FUSE_BN_BWD_MIN_K", "64"))
-# A/B switches: the max-pool backward's routed gradient / the last head's input gradient
-# recomputed by the BatchNorm-backward apply instead of written to HBM
-# (maxpool2_bwd / head_bwd(defer=True) + bn_relu_bwd(route=...))
-_DEFER_POOL_BWD = os.environ.get("UGPG_DEFER_POOL_BWD", "1") != "0"
-_DEFER_HEAD_BWD = os.environ.get("UGPG_DEFER_HEAD_BWD", "1") != "0"
 
 
 def _store16(W: int) -> bool:
@@ -177,10 +167,8 @@ def double_conv_backward(mod, ctx: BlockCtx, da2, targets, acc_flags, grads, pad
     # the data gradient also reduces BN1's backward sums over da1 while each tile is in
     # registers (ugpg_conv_t.bnb_*), so BN1's backward is finalize + apply only
     part = bnb = None
-    # (tools/ab_step.py, interleaved: -0.9 % step time fusing every layer, -0.2 % with
-    # K >= 128 only; the K = 64 items are 4 steps long, so the extra epilogue pass costs
-    # those dgrads most of what the separate reduction did -- UGPG_FUSE_BN_BWD_MIN_K)
-    if ctx.st1[0] is not None and _FUSE_BN_BWD and cout >= _FUSE_BN_BWD_MIN_K:
+    # (in-process A/B: -0.9 % of the step fusing every layer, -0.2 % with K >= 128 only)
+    if ctx.st1[0] is not None:
         part = ops.empty(3 * cmid * ops.conv_ntiles(B, H, W, cout, cmid, wpk2), like=da2)
         bnb = (ctx.y1, *ctx.st1, part)
     ops.conv3x3_fwd([Act(dy2)], wpk2, None, cmid, [da1], flops=2.0 * npix * cmid * 9 * cout,
@@ -318,7 +306,7 @@ class UNetGraph:
 
         def bn2_state(src, bi):
             c = ctxs[src]
-            if not _FUSE_BN_BWD or first_use.get(src) != bi or c.st2 is None or c.st2[0] is None:
+            if first_use.get(src) != bi or c.st2 is None or c.st2[0] is None:
                 return None
             return (c.y2, *c.st2)
         if self.heads:
@@ -334,15 +322,17 @@ class UNetGraph:
                 dw_flat = dw.view(w.shape) if dw is not None else torch.empty_like(w)
                 db = grads.get(conv.bias)
                 c = ctxs[hd.block]
-                fuse = (_FUSE_BN_BWD and hd.block not in first_use and last_head[hd.block] == hi
-                        and c.st2 is not None and c.st2[0] is not None and a.y is c.y2)
+                # the last head of a block no block consumes (the top decoder block): it
+                # writes only the BN2-backward partials, and the block's BN2-backward apply
+                # recomputes dh @ w per pixel instead of reading a full-resolution da
+                defer = (hd.block not in first_use and last_head[hd.block] == hi
+                         and c.st2 is not None and c.st2[0] is not None and a.y is c.y2)
                 dh = dh.contiguous()
-                defer = fuse and _DEFER_HEAD_BWD
                 part = ops.head_bwd(a, w, dh, dw_flat, db, da[hd.block], acc,
-                                    bnb=c.st2[:2] if fuse else None, defer=defer)
+                                    bnb=c.st2[:2] if defer else None, defer=defer)
                 if part is not None:
                     c.part2 = part
-                if defer:  # the block's BN2-backward apply recomputes dh @ w
+                if defer:
                     c.route2 = (("head", dh, w), acc)
             if on_done is not None:
                 on_done([grads.get(p) for hd in self.heads for p in hd.mod.parameters()])
@@ -371,9 +361,10 @@ class UNetGraph:
                     da[src] = _grad_like(outs[src].y)
                 st = bn2_state(src, bi)
                 am = ctx.extra["argmax"]
-                if st is not None and _DEFER_POOL_BWD:
+                if st is not None:
                     # the last contribution to da[src]: only its partials here; the apply of
-                    # src's BN2 backward recomputes the routing (no full-resolution write)
+                    # src's BN2 backward recomputes the routing (no full-resolution write:
+                    # DESIGN §3, maxpool2 row)
                     ctxs[src].part2 = ops.maxpool2_bwd(dp, am, H, W, da[src], acc, bnb=st,
                                                        defer=True)
                     ctxs[src].route2 = (("pool", dp, am, H, W), acc)

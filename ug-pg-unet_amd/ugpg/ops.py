@@ -128,7 +128,6 @@ def conv_pack_k(cin: int) -> int:
 # packs made ahead for the running forward/backward (see prepack / UNetGraph); a miss
 # (or None) packs on the spot, so the table only saves launches, never changes results
 _PREPACK = None
-_PREPACK_ON = os.environ.get("UGPG_PREPACK", "1") != "0"  # A/B switch
 
 
 def _pack_key(w, cin_pad, mode):
@@ -149,7 +148,7 @@ def prepack(specs):
     Every writer of parameters bumps the version (ugpg's optimizers, broadcasts,
     load_state_dict), so a stale pack is never used."""
     table = {}
-    if _conv_math not in ("x6", "bf16") or not specs or not _PREPACK_ON:
+    if _conv_math not in ("x6", "bf16") or not specs:
         return table
     items, outs = [], []
     for p, cin_pad, mode in specs:
@@ -326,9 +325,6 @@ def bn_finalize(stats, ntiles, gamma, beta, rm, rv, nbt, momentum, eps):
     return mean, invstd, scale, shift
 
 
-_EVAL_CACHE_ON = os.environ.get("UGPG_BN_EVAL_CACHE", "1") != "0"  # A/B switch
-
-
 def bn_eval_params(gamma, beta, rm, rv, eps, owner=None):
     """(scale, shift) of an eval-mode BatchNorm.  With `owner` (the module) the result is
     cached on it, keyed on the storage and version counter of gamma, beta and the running
@@ -336,7 +332,7 @@ def bn_eval_params(gamma, beta, rm, rv, eps, owner=None):
     broadcasts, load_state_dict's copy_) -- so a frozen previous stage (the U-map
     producer) costs no launch per step."""
     key = None
-    if owner is not None and _EVAL_CACHE_ON:
+    if owner is not None:
         key = tuple((t.data_ptr(), t._version) for t in (gamma, beta, rm, rv)) + (float(eps),)
         hit = getattr(owner, "_ugpg_eval_params", None)
         if hit is not None and hit[0] == key:

@@ -11,7 +11,6 @@ host once per batch instead of the reference's six ``.item()``/``.cpu()`` calls.
 from __future__ import annotations
 
 import json
-import os
 import time
 from pathlib import Path
 
@@ -33,13 +32,6 @@ try:  # plotting is optional, as in the reference
     MATPLOTLIB_AVAILABLE = True
 except Exception:  # pragma: no cover
     MATPLOTLIB_AVAILABLE = False
-
-
-# the U map's previous-stage forward on a second stream (UncertaintyGuidedProgressive
-# Trainer._umap_on_side) with UGPG_UMAP_STREAM=1.  Off by default: bit-identical either way,
-# but worth only 0.3 % (x6) / 0.6 % (bf16) of the step (in-process A/B, profiles/r4e_ab_*,
-# r4f_ab_*), and overlapping launches blur the per-kernel timing the bench reports
-_UMAP_SIDE = int(os.environ.get("UGPG_UMAP_STREAM", "0"))
 
 
 class MetricsReadback:
@@ -140,52 +132,15 @@ class UncertaintyGuidedProgressiveTrainer:
         print(f"Weight transfer completed for stage {new_stage}")
 
     # ------------------------------------------------------------ hot path
-    def _umap_on_side(self, data, stage):
-        """Enqueue the U map (the previous stage's eval forward) on a second HIP stream,
-        concurrently with the current stage's forward: the two are independent until the
-        loss.  Ordering and allocator rules:
-          1. side waits for the current stream: `data` (resized / copied on the current
-             stream) is complete before the previous-stage model reads it;
-          2. data.record_stream(side): its block is not handed to a new current-stream
-             allocation while the side stream may still read it;
-          3. the caller makes the current stream wait for side before the loss reads U,
-             and U.record_stream(current): U's block (side-stream pool) is not recycled
-             by a later side-stream allocation while its current-stream readers are pending.
-        The previous stage's persistent state (flat parameters, weight packs, eval
-        BatchNorm coefficients) is built on the current stream first (prepare_eval).
-        Results are bit-identical to the one-stream order (tests/test_gpu_models.py) now
-        that no kernel has the packed-FP32 hazard of DESIGN.md §6a, which concurrent
-        kernels exposed."""
-        cur = torch.cuda.current_stream(data.device)
-        prev = self.models[stage - 1]
-        prev.eval()
-        prev.prepare_eval()
-        side = self.__dict__.get("_side")
-        if side is None or side.device != data.device:
-            side = self._side = torch.cuda.Stream(device=data.device)
-        side.wait_stream(cur)
-        with torch.cuda.stream(side):
-            umap = self.uncertainty_loss.generate_uncertainty_map(
-                data, prev, self.stage_configs[stage - 1]["resolution"],
-                self.stage_configs[stage]["resolution"])
-        data.record_stream(side)
-        return umap, cur, side
-
     def _forward_device(self, data, target, stage, mbuf):
         """Forward + uncertainty map + weighted loss; results stay on the device.
         mbuf: 8-float device buffer [final, base, dice, acc, wrong, u_mean, u_std, 0]."""
         umap = None
-        if stage > 1 and _UMAP_SIDE and data.is_cuda:
-            umap, cur, side = self._umap_on_side(data, stage)
-            output = self.current_model(data)
-            cur.wait_stream(side)
-            umap.record_stream(cur)
-        else:
-            output = self.current_model(data)
-            if stage > 1:
-                umap = self.uncertainty_loss.generate_uncertainty_map(
-                    data, self.models[stage - 1], self.stage_configs[stage - 1]["resolution"],
-                    self.stage_configs[stage]["resolution"])
+        output = self.current_model(data)
+        if stage > 1:
+            umap = self.uncertainty_loss.generate_uncertainty_map(
+                data, self.models[stage - 1], self.stage_configs[stage - 1]["resolution"],
+                self.stage_configs[stage]["resolution"])
         final, base = weighted_loss_tensors(self.base_criterion, output, target, umap,
                                             self.uncertainty_alpha,
                                             out=mbuf[0:2] if mbuf is not None else None)
