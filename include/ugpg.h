@@ -479,6 +479,20 @@ int ugpg_augment_geom(const uint8_t* img, const uint8_t* mask, int S, int64_t B,
 int ugpg_augment_color(const uint8_t* img, const uint8_t* mask, int S, int64_t B,
                        const void* params, const unsigned* lsum, const float* u8_to_f32,
                        float* out, float* out_mask, void* stream);
+/* XML annotation polygons -> mask: replaces the reference's per-region
+ * `ImageDraw.Draw(mask).polygon(points, fill=1)` loop (MoNuSegImprove/
+ * monuseg_dataset.py:117-132, aug_monuseg_dataset.py:89-111) with Pillow 12's scan
+ * converter reproduced bit for bit (oracle/polygon_ref.py lists its rules).  npoly
+ * polygons; polygon p = vertices [off[p], off[p+1]) of xy (x, y pairs of doubles: the
+ * XML's float values; >= 2 vertices each, as PIL requires); each is filled with `ink`
+ * into mask (H x W uint8, row-major), which is not cleared first (the reference draws
+ * every region into one mask).  ws: device workspace of at least
+ * ugpg_rasterize_polygons_ws_size(nverts, npoly) bytes (nverts = off[npoly]), else
+ * UGPG_ERR_WORKSPACE. */
+size_t ugpg_rasterize_polygons_ws_size(int64_t nverts, int64_t npoly);
+int ugpg_rasterize_polygons(const double* xy, const int64_t* off, int64_t npoly, int64_t nverts,
+                            uint8_t* mask, int H, int W, int ink, void* ws, size_t ws_bytes,
+                            void* stream);
 
 #ifdef __cplusplus
 }

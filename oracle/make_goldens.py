@@ -26,6 +26,8 @@ Fixture map:
   g10_monuseg_eval.npz    MoNuSegEvaluator.calculate_metrics and predict_image, run for real
   g11_checkpoint_interop.json  checkpoints round-trip reference <-> ugpg (asserted when generated)
   g4b_pgunet4_bs16.npz    config 2 at bs16 x 256^2: checksums, fp32 noise floors
+  g13_polygons.npz        MoNuSeg mask rasterisation: PIL ImageDraw.polygon masks of
+                          oracle/polygon_cases.canvases() (no reference import needed)
 """
 from __future__ import annotations
 
@@ -946,6 +948,31 @@ def g4c(RU):
         fx[f"floor16/{k}"] = np.array([floor[k], g0[k].abs().max().item()])
         fx[f"grad16/{k}"] = tstats(k, g0[k])
     save_npz("g4c_bf16_floor.npz", **fx)
+
+
+def g13(RU=None):
+    """MoNuSeg mask rasterisation (monuseg_dataset.py:126-132): masks
+    drawn by the reference's own rasteriser, PIL ImageDraw.polygon(fill=1) of the
+    installed Pillow, for oracle/polygon_cases.canvases() -- one 1000 x 1000 canvas of 600
+    nuclei and 360 small canvases of odd polygons.  The restatement in
+    oracle/polygon_ref.py must reproduce every mask (asserted here and in
+    tests/test_polygon_oracle.py); the GPU kernel is held to the same masks."""
+    import PIL
+    from oracle import polygon_cases as PC
+    from oracle import polygon_ref as PR
+    cases = PC.canvases()
+    fx = PC.pack(cases)
+    bits, off = [], [0]
+    for H, W, polys in cases:
+        m = PC.render_pil(H, W, polys)
+        assert np.array_equal(m, PR.rasterize(H, W, polys)), "polygon restatement != PIL"
+        b = np.packbits(m.reshape(-1).astype(bool))
+        bits.append(b)
+        off.append(off[-1] + len(b))
+    fx["mask_bits"] = np.concatenate(bits)
+    fx["mask_off"] = np.asarray(off, np.int64)
+    fx["pillow_version"] = np.array(PIL.__version__)
+    save_npz("g13_polygons.npz", **fx)
 
 
 def g0(RU):

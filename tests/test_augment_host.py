@@ -75,11 +75,16 @@ def test_xml_annotations_rasterise_like_the_reference(tmp_path):
                    '<Vertex X="11.5" Y="18.4"/></Vertices></Region>'
                    '<Region><Vertices><Vertex X="1" Y="1"/><Vertex X="2" Y="2"/></Vertices></Region>'
                    '</Regions></Annotation></Annotations>')
-    m = A.parse_xml_annotations(str(xml), (32, 24))
+    polys = A.xml_polygons(str(xml))  # regions with < 3 vertices skipped, as the reference
+    assert polys == [[(3.2, 4.9), (20.7, 6.1), (11.5, 18.4)]]
     from PIL import ImageDraw
+    from oracle import polygon_ref as PR
     ref = Image.fromarray(np.zeros((24, 32), np.uint8))
     ImageDraw.Draw(ref).polygon([(3.2, 4.9), (20.7, 6.1), (11.5, 18.4)], fill=1)
-    assert m.shape == (24, 32) and np.array_equal(m, np.asarray(ref)) and m.sum() > 0
+    m = PR.rasterize(24, 32, polys)   # the restatement the GPU kernel is held to
+    assert np.array_equal(m, np.asarray(ref)) and m.sum() > 0
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        A.rasterize_polygons(polys, 24, 32, "cpu")
 
 
 def test_parameter_records_match_the_library_layout():

@@ -75,7 +75,11 @@ def _write_dataset(root, split_dir, n, size, rng):
 
 
 def test_datasets_match_reference_behaviour(dev, tmp_path):
-    from ugpg.augment import AugMoNuSegDataset, MoNuSegDataset, parse_xml_annotations
+    from ugpg.augment import AugMoNuSegDataset, MoNuSegDataset, xml_polygons
+    from oracle.polygon_cases import render_pil
+
+    def parse_xml_annotations(path, size):  # the reference's PIL rasterisation
+        return render_pil(size[1], size[0], xml_polygons(path))
     rng = np.random.default_rng(11)
     _write_dataset(str(tmp_path), ("train", "aug"), 3, 120, rng)
     _write_dataset(str(tmp_path), ("test",), 2, 120, rng)

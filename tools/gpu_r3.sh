@@ -40,6 +40,7 @@ for s in "$@"; do
             step ab 400 python tools/conv_bench.py --rounds ${ROUNDS:-4} --maths ${MATHS:-x6,bf16} --layers ${layers:-inc.3,down1.0,down2.3,up4.0,up4.3} --libs $libs ${EXTRA:-} ;;
     abstep:*) IFS=@ read -r sa sb <<< "${s#abstep:}"
             step abstep 400 python tools/ab_step.py --a "$sa" --b "$sb" ${EXTRA:-} ;;
+    convbench) step convbench 500 python tools/conv_bench.py --rounds 3 --maths ${MATHS:-bf16,x6} ${EXTRA:-} ;;
     bench) step bench 600 python bench.py ;;
     bench_bf16) step bench_bf16 300 python bench.py --conv-math bf16 --no-cpu-baseline --secondary-steps 0 ;;
     herlev256) step herlev256 600 python bench.py --workload herlev --res 256 ;;

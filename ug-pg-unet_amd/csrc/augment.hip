@@ -11,8 +11,8 @@
 // ImagingBlend's float32 blend with truncation, the L conversion
 // (299/587/114 in 16-bit fixed point), and RGB<->HSV as in Convert.c.  Floating-point
 // steps use explicit _rn intrinsics so no FMA contraction changes a rounding.
-// The XML polygon rasterisation stays with PIL on the host (done once per image and
-// cached: the per-epoch work is the random transforms).
+// The XML polygon rasterisation (monuseg_dataset.py:126-132, PIL ImageDraw.polygon) is
+// Pillow's scan converter reproduced bit for bit (poly_edges_kernel / poly_scan_kernel).
 #include <algorithm>
 
 #include "common.h"
@@ -272,6 +272,166 @@ __global__ void augment_color_kernel(const uint8_t* __restrict__ img, const uint
     }
 }
 
+// ---------------------------------------------------------------------------
+// Filled polygons, Pillow 12's scan converter (libImaging/Draw.c ImagingDrawPolygon +
+// polygon_generic + hline8; restated and pinned in oracle/polygon_ref.py, whose header
+// lists the rules).  Float steps in float with explicit _rn intrinsics (no contraction),
+// the negative-argument rounding macros in double, as Pillow's x86 build evaluates them.
+struct PolyEdge {
+    int x0, y0, xmin, ymin, xmax, ymax;
+    float dx;
+    int pad;
+};
+struct PolyInfo {
+    int nedges, ymin, ymax, pad;
+};
+
+// C (int) of a double on x86: toward zero, out of range -> INT_MIN
+__device__ __forceinline__ int trunc_int_x86(double v) {
+    return (v > -2147483649.0 && v < 2147483648.0) ? (int)v : (int)0x80000000u;
+}
+__device__ __forceinline__ void poly_hline(uint8_t* mask, int H, int W, int x0, int y, int x1,
+                                           uint8_t ink) {
+    if (y < 0 || y >= H) return;
+    if (x0 < 0) {
+        if (x1 < 0) return;
+        x0 = 0;
+    } else if (x0 >= W || x1 < 0) {
+        return;
+    }
+    if (x1 >= W) x1 = W - 1;
+    uint8_t* row = mask + (size_t)y * W;
+    for (int x = x0; x <= x1; ++x) row[x] = ink;
+}
+__device__ __forceinline__ float poly_x_at(const PolyEdge& e, int y) {
+    return __fadd_rn(__fmul_rn((float)(y - e.y0), e.dx), (float)e.x0);
+}
+__device__ __forceinline__ int poly_round_up(float f) {
+    if (f >= 0.f) return (int)floorf(__fadd_rn(f, 0.5f));
+    return -(int)floor(__dadd_rn(fabs((double)f), 0.5));
+}
+__device__ __forceinline__ int poly_round_down(float f) {
+    if (f >= 0.f) return (int)ceilf(__fsub_rn(f, 0.5f));
+    return -(int)ceil(__dsub_rn(fabs((double)f), 0.5));
+}
+
+// one thread per polygon: vertices -> edges (in order; consecutive horizontal edges in the
+// same direction merged), horizontal edges drawn as spans, the row range recorded
+__global__ void poly_edges_kernel(const double* __restrict__ xy, const int64_t* __restrict__ off,
+                                  int64_t npoly, PolyEdge* __restrict__ edges,
+                                  PolyInfo* __restrict__ info, uint8_t* mask, int H, int W,
+                                  uint8_t ink) {
+    const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (p >= npoly) return;
+    const int64_t v0 = off[p];
+    const int count = (int)(off[p + 1] - v0);
+    if (count < 2) {  // (the host refuses these; PIL raises) -- no rows
+        info[p] = PolyInfo{0, 1, 0, 0};
+        return;
+    }
+    PolyEdge* e = edges + v0;
+    auto X = [&](int i) { return trunc_int_x86(xy[2 * (v0 + i)]); };
+    auto Y = [&](int i) { return trunc_int_x86(xy[2 * (v0 + i) + 1]); };
+    auto add = [&](int n, int x0, int y0, int x1, int y1) {
+        PolyEdge q;
+        q.xmin = x0 <= x1 ? x0 : x1;
+        q.xmax = x0 <= x1 ? x1 : x0;
+        q.ymin = y0 <= y1 ? y0 : y1;
+        q.ymax = y0 <= y1 ? y1 : y0;
+        q.dx = y0 == y1 ? 0.f : __fdiv_rn((float)(x1 - x0), (float)(y1 - y0));
+        q.x0 = x0;
+        q.y0 = y0;
+        q.pad = 0;
+        e[n] = q;
+    };
+    int n = 0, i = 0;
+    for (i = 0; i < count - 1; ++i) {
+        const int x0 = X(i), y0 = Y(i), x1 = X(i + 1), y1 = Y(i + 1);
+        if (y0 == y1 && i != 0 && y0 == Y(i - 1)) {
+            const int xp = X(i - 1);
+            if (x1 > x0 && x0 > xp) {
+                e[n - 1].xmax = x1;
+                continue;
+            }
+            if (x1 < x0 && x0 < xp) {
+                e[n - 1].xmin = x1;
+                continue;
+            }
+        }
+        add(n++, x0, y0, x1, y1);
+    }
+    if (X(i) != X(0) || Y(i) != Y(0)) add(n++, X(i), Y(i), X(0), Y(0));
+    // the row range over every edge; horizontal edges are drawn here and dropped from the
+    // table (compacted in place, order kept)
+    int ymin = H - 1, ymax = 0, m = 0;
+    for (int k = 0; k < n; ++k) {
+        const PolyEdge q = e[k];
+        ymin = min(ymin, q.ymin);
+        ymax = max(ymax, q.ymax);
+        if (q.ymin == q.ymax) {
+            poly_hline(mask, H, W, q.xmin, q.ymin, q.xmax, ink);
+            continue;
+        }
+        e[m++] = q;
+    }
+    info[p] = PolyInfo{m, max(ymin, 0), min(ymax, H), 0};
+}
+
+// one 64-lane workgroup per polygon, a row per lane: the row's edge crossings (with the
+// corner rule), sorted, filled pairwise; lane scratch = 2 * (vertex count) floats
+__global__ void __launch_bounds__(64) poly_scan_kernel(const int64_t* __restrict__ off,
+                                                       const PolyEdge* __restrict__ edges,
+                                                       const PolyInfo* __restrict__ info,
+                                                       float* __restrict__ scratch, uint8_t* mask,
+                                                       int H, int W, uint8_t ink) {
+    const int64_t p = blockIdx.x;
+    const int64_t v0 = off[p];
+    const int cap = 2 * (int)(off[p + 1] - v0);
+    const PolyInfo pi = info[p];
+    const PolyEdge* e = edges + v0;
+    float* xx = scratch + 128 * v0 + (int64_t)threadIdx.x * cap;
+    for (int y = pi.ymin + (int)threadIdx.x; y <= pi.ymax; y += 64) {
+        int j = 0;
+        for (int i = 0; i < pi.nedges; ++i) {
+            const PolyEdge cur = e[i];
+            if (y < cur.ymin || y > cur.ymax) continue;
+            float x = poly_x_at(cur, y);
+            if (y == cur.ymax && y < pi.ymax) {
+                xx[j++] = x;
+                xx[j++] = x;
+                continue;
+            }
+            if ((y == cur.ymin || y == cur.ymax) && cur.dx != 0.f) {
+                const int adj = y == cur.ymax ? y - 1 : y + 1;
+                for (int k = 0; k < i; ++k) {
+                    const PolyEdge o = e[k];
+                    if (!((y == o.ymin || y == o.ymax) && o.dx != 0.f)) continue;
+                    if (roundf(x) != roundf(poly_x_at(o, y))) continue;
+                    if (adj < o.ymin || adj > o.ymax) continue;
+                    const float ac = poly_x_at(cur, adj), ao = poly_x_at(o, adj);
+                    if (x > __fadd_rn(ac, 1.f) && x > __fadd_rn(ao, 1.f))
+                        x = __fadd_rn(roundf(fmaxf(ac, ao)), 1.f);
+                    else if (x < __fsub_rn(ac, 1.f) && x < __fsub_rn(ao, 1.f))
+                        x = __fsub_rn(roundf(fminf(ac, ao)), 1.f);
+                    break;
+                }
+            }
+            xx[j++] = x;
+        }
+        for (int a = 1; a < j; ++a) {  // insertion sort (a handful of crossings per row)
+            const float v = xx[a];
+            int b = a - 1;
+            while (b >= 0 && xx[b] > v) {
+                xx[b + 1] = xx[b];
+                --b;
+            }
+            xx[b + 1] = v;
+        }
+        for (int a = 1; a < j; a += 2)
+            poly_hline(mask, H, W, poly_round_up(xx[a - 1]), y, poly_round_down(xx[a]), ink);
+    }
+}
+
 }  // namespace ugpg
 
 using namespace ugpg;
@@ -344,4 +504,35 @@ extern "C" int ugpg_augment_color(const uint8_t* img, const uint8_t* mask, int S
                        as_stream(stream), img, mask, S, B, static_cast<const AugColor*>(params),
                        lsum, u8_to_f32, out, out_mask);
     return check_launch("augment_color");
+}
+
+extern "C" size_t ugpg_rasterize_polygons_ws_size(int64_t nverts, int64_t npoly) {
+    if (nverts < 0 || npoly < 0) return 0;
+    // edges (<= vertices), per-polygon info, per-lane crossing scratch (64 lanes x 2 x n)
+    return (size_t)nverts * sizeof(PolyEdge) + (size_t)npoly * sizeof(PolyInfo) +
+           (size_t)nverts * 128 * sizeof(float);
+}
+
+extern "C" int ugpg_rasterize_polygons(const double* xy, const int64_t* off, int64_t npoly,
+                                       int64_t nverts, uint8_t* mask, int H, int W, int ink,
+                                       void* ws, size_t ws_bytes, void* stream) {
+    if (!xy || !off || !mask || !ws || npoly <= 0 || nverts < 2 * npoly || H <= 0 || W <= 0 ||
+        ink < 0 || ink > 255 || npoly > (1ll << 31) - 1) {
+        set_error("rasterize_polygons: bad arguments");
+        return UGPG_ERR_INVALID;
+    }
+    if (ws_bytes < ugpg_rasterize_polygons_ws_size(nverts, npoly)) {
+        set_error("rasterize_polygons: workspace too small");
+        return UGPG_ERR_WORKSPACE;
+    }
+    hipStream_t st = as_stream(stream);
+    PolyEdge* edges = static_cast<PolyEdge*>(ws);
+    PolyInfo* info = reinterpret_cast<PolyInfo*>(edges + nverts);
+    float* scratch = reinterpret_cast<float*>(info + npoly);
+    hipLaunchKernelGGL(poly_edges_kernel, dim3((unsigned)cdiv(npoly, 64)), dim3(64), 0, st, xy, off,
+                       npoly, edges, info, mask, H, W, (uint8_t)ink);
+    if (int r = check_launch("rasterize_polygons(edges)")) return r;
+    hipLaunchKernelGGL(poly_scan_kernel, dim3((unsigned)npoly), dim3(64), 0, st, off, edges, info,
+                       scratch, mask, H, W, (uint8_t)ink);
+    return check_launch("rasterize_polygons(scan)");
 }

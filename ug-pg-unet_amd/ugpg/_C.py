@@ -132,6 +132,8 @@ SIGNATURES = {
     "ugpg_augment_param_sizes": (_i, [C.POINTER(_i), C.POINTER(_i)]),
     "ugpg_augment_geom": (_i, [_p, _p, _i, _i64, _p, _p, _p, _p, _p]),
     "ugpg_augment_color": (_i, [_p, _p, _i, _i64, _p, _p, _p, _p, _p, _p]),
+    "ugpg_rasterize_polygons_ws_size": (_sz, [_i64, _i64]),
+    "ugpg_rasterize_polygons": (_i, [_p, _p, _i64, _i64, _p, _i, _i, _i, _p, _sz, _p]),
 }
 
 

@@ -7,12 +7,13 @@ XML polygons rasterised with ``ImageDraw.polygon(fill=1)`` (:89-111), then per s
 NEAREST, ``TF.adjust_brightness/contrast/saturation/hue`` and ``ToTensor`` (:113-148),
 the random parameters drawn from ``random.Random(torch.randint(0, 2**32))``.
 
-Here the decode (PIL ``Image.open``) and the polygon rasterisation (PIL, exactly the
-reference's call) run once per image on the host and are cached; every random
-transform runs on the GPU (``csrc/augment.hip``) with PIL's own 8-bit arithmetic, so
-the tensors equal the reference's bit for bit for the same torch RNG state
-(``tests/test_gpu_augment.py`` checks against PIL).  The product path needs the HIP
-library: there is no CPU fallback.
+Here the decode (PIL ``Image.open``) runs once per image on the host; the XML polygons
+are rasterised on the GPU by Pillow's own scan converter reproduced bit for bit
+(``rasterize_polygons``, ``ugpg_rasterize_polygons``); image and mask are cached in HBM,
+and every random transform runs on the GPU (``csrc/augment.hip``) with PIL's own 8-bit
+arithmetic, so the tensors equal the reference's bit for bit for the same torch RNG
+state (``tests/test_gpu_augment.py`` and ``tests/test_gpu_polygons.py`` check against
+PIL).  The product path needs the HIP library: there is no CPU fallback.
 """
 from __future__ import annotations
 
@@ -247,20 +248,62 @@ class MoNuSegAugmenter:
         return out, omask
 
 
-# ----------------------------------------------------------------- datasets
-def parse_xml_annotations(xml_path: str, image_size: Tuple[int, int]) -> np.ndarray:
-    """aug_monuseg_dataset.py:89-111: every Region with >= 3 vertices filled with 1
-    by PIL ImageDraw (the reference's own rasteriser)."""
-    from PIL import Image, ImageDraw
+# ----------------------------------------------------------------- masks
+def rasterize_polygons(polygons, H: int, W: int, device, ink: int = 1,
+                       out: torch.Tensor = None) -> torch.Tensor:
+    """Fill every polygon (a sequence of (x, y) floats) with `ink` into an (H, W) uint8
+    device mask, exactly as ``ImageDraw.Draw(mask).polygon(points, fill=ink)`` called
+    per polygon in order does (monuseg_dataset.py:126-132): one launch pair for all of
+    them.  `out` (default: a new zero mask) is drawn into, not cleared."""
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        raise RuntimeError("rasterize_polygons: the HIP kernel needs a GPU tensor device "
+                           "(no CPU fallback)")
+    mask = torch.zeros(H, W, dtype=torch.uint8, device=dev) if out is None else out
+    if mask.shape != (H, W) or mask.dtype != torch.uint8 or not mask.is_contiguous():
+        raise ValueError("rasterize_polygons: out must be a contiguous (H, W) uint8 tensor")
+    polys = [p for p in polygons]
+    if not polys:
+        return mask
+    counts = [len(p) for p in polys]
+    if min(counts) < 2:
+        # PIL: "coordinate list must contain at least 2 coordinates"
+        raise TypeError("coordinate list must contain at least 2 coordinates")
+    off = np.zeros(len(polys) + 1, np.int64)
+    np.cumsum(counts, out=off[1:])
+    xy = np.asarray([c for p in polys for pt in p for c in pt], np.float64)
+    xy_d = torch.from_numpy(xy).to(dev)
+    off_d = torch.from_numpy(off).to(dev)
+    nv, npoly = int(off[-1]), len(polys)
+    wsb = int(lib.ugpg_rasterize_polygons_ws_size(nv, npoly))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    check(lib.ugpg_rasterize_polygons(xy_d.data_ptr(), off_d.data_ptr(), npoly, nv,
+                                      mask.data_ptr(), H, W, int(ink), ws.data_ptr(), wsb, st),
+          "rasterize_polygons")
+    return mask
+
+
+def xml_polygons(xml_path: str):
+    """The reference's region list (aug_monuseg_dataset.py:89-111 / monuseg_dataset.py:
+    114-126): the float vertices of every Region with >= 3 vertices, in file order."""
     root = ET.parse(xml_path).getroot()
-    mask = Image.fromarray(np.zeros(image_size[::-1], dtype=np.uint8))
-    draw = ImageDraw.Draw(mask)
+    polys = []
     for region in root.findall(".//Region"):
         vertices = region.findall(".//Vertex")
         if len(vertices) < 3:
             continue
-        draw.polygon([(float(v.attrib["X"]), float(v.attrib["Y"])) for v in vertices], fill=1)
-    return np.array(mask)
+        polys.append([(float(v.attrib["X"]), float(v.attrib["Y"])) for v in vertices])
+    return polys
+
+
+# ----------------------------------------------------------------- datasets
+def parse_xml_annotations(xml_path: str, image_size: Tuple[int, int], device="cuda") -> torch.Tensor:
+    """aug_monuseg_dataset.py:89-111 / monuseg_dataset.py:97-135: the binary mask
+    (H, W) uint8 of every Region with >= 3 vertices filled with 1, rasterised on the GPU
+    (``rasterize_polygons``: PIL ImageDraw's result bit for bit).  image_size = (W, H)."""
+    W, H = image_size
+    return rasterize_polygons(xml_polygons(xml_path), H, W, device)
 
 
 class _MoNuSegBase:
@@ -292,10 +335,9 @@ class _MoNuSegBase:
             from PIL import Image
             image_path, annotation_path = self.samples[idx]
             image = Image.open(image_path).convert("RGB")
-            mask = parse_xml_annotations(annotation_path, image.size)
             dev = self.device
-            self._cache[idx] = (torch.from_numpy(np.array(image)).to(dev),
-                                torch.from_numpy(mask).to(dev))
+            mask = parse_xml_annotations(annotation_path, image.size, dev)
+            self._cache[idx] = (torch.from_numpy(np.array(image)).to(dev), mask)
         return self._cache[idx]
 
     def _augmenter(self):
