@@ -16,11 +16,16 @@ import pytest
 ROOT = Path(__file__).resolve().parent.parent
 CSRC = ROOT / "ug-pg-unet_amd" / "csrc"
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+X6R = "_ZN4ugpg22conv3x3_fwd_x6r_kernelIL{}EEEvNS_11ConvFwdArgsE"
 KERNELS = [
-    "_ZN4ugpg22conv3x3_fwd_x6r_kernelILi3ELb1ELi32ELi8ELb0EEEvNS_11ConvFwdArgsE",
-    "_ZN4ugpg22conv3x3_fwd_x6r_kernelILi3ELb1ELi16ELi8ELb0EEEvNS_11ConvFwdArgsE",
-    "_ZN4ugpg22conv3x3_fwd_x6r_kernelILi1ELb0ELi32ELi8ELb0EEEvNS_11ConvFwdArgsE",
-    "_ZN4ugpg22conv3x3_fwd_x6r_kernelILi1ELb0ELi32ELi8ELb1EEEvNS_11ConvFwdArgsE",
+    X6R.format("i3ELb1ELi32ELi8ELb0ELi1"),
+    X6R.format("i3ELb1ELi16ELi8ELb0ELi1"),
+    X6R.format("i1ELb0ELi32ELi8ELb0ELi1"),
+    X6R.format("i1ELb0ELi32ELi8ELb1ELi1"),
+    X6R.format("i1ELb0ELi32ELi8ELb0ELi2"),    # single-piece 256 x 128 items
+    X6R.format("i1ELb0ELi32ELi8ELb1ELi2"),
+    X6R.format("i1ELb0ELi32ELi16ELb0ELi1"),   # single-piece 512 x 64 items
+    X6R.format("i1ELb0ELi32ELi16ELb1ELi1"),
     "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi3ELi0EEEvNS_9WgradArgsE",
     "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi1ELi0EEEvNS_9WgradArgsE",
     "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi1ELi1EEEvNS_9WgradArgsE",

@@ -77,6 +77,7 @@ CONV_CASES = [
     (1, 16, 16, 512, 512, 512, True),  # Up-shaped 16-wide concat: 4-way split-K forward/dgrad
     (2, 45, 70, 8, 0, 64, False),      # image layer, ragged 8 x 32 tiles (direct fp32 kernel)
     (3, 16, 40, 512, 0, 64, True),     # 16-high, 40-wide: 8 x 32 items, ragged columns
+    (2, 250, 254, 64, 0, 64, True),    # bf16: 16 x 32-pixel items, ragged rows and columns
 ]
 BIG = {5, 6, 7}
 
@@ -259,7 +260,11 @@ def test_bn_relu_bwd(dev, C, npix):
 # (B, H, W, K = channels of dy, C = channels of da): the fused epilogue on the 8 x 32
 # and 8 x 16 persistent forms (ragged tiles included), the separate pass elsewhere
 BNB_CASES = [(2, 32, 32, 64, 64), (1, 20, 37, 64, 64), (2, 16, 16, 128, 128),
-             (1, 24, 18, 128, 64), (2, 8, 8, 128, 64)]
+             (1, 24, 18, 128, 64), (2, 8, 8, 128, 64),
+             # the bf16 arithmetic's wide single-piece forms (512 x 64 and 256 x 128 items),
+             # with y stored in bf16 (fused) and in fp32 (their partials come from the pass)
+             (2, 256, 256, 64, 64, True), (2, 256, 256, 64, 64), (4, 128, 128, 128, 128, True),
+             (4, 128, 128, 128, 128), (2, 250, 254, 64, 64, True)]
 
 
 @pytest.mark.parametrize("case", BNB_CASES)
@@ -268,10 +273,13 @@ def test_dgrad_fused_bn_bwd_partials(dev, case, math):
     data gradient is unchanged and the BatchNorm backward (dy, dgamma, dbeta, the conv
     bias grad) equals the standalone reduction's up to summation order."""
     from ugpg import ops
-    B, H, W, K, Cc = case
+    B, H, W, K, Cc = case[:5]
+    y16 = len(case) > 5 and case[5]
     dy2 = rnd((B, K, H, W), 30, "dy2")
     w = rnd((K, Cc, 3, 3), 31, "w", 0.05)
     y = rnd((B, Cc, H, W), 32, "y") * 2 + 0.3
+    if y16:
+        y = y.to(torch.bfloat16).float()
     gam, bet = rnd((Cc,), 33, "g", 0.3) + 1, rnd((Cc,), 34, "b", 0.3)
     yd = y.double()
     mean = yd.mean((0, 2, 3))
@@ -281,6 +289,8 @@ def test_dgrad_fused_bn_bwd_partials(dev, case, math):
     f = lambda t: t.float().to(dev)
     st = [f(mean), f(invstd), f(scale), f(shift)]
     ys, d2 = nhwc(y).to(dev), nhwc(dy2).to(dev)
+    if y16:
+        ys = ys.to(torch.bfloat16)
     wpk = ops.pack_conv3x3(w.to(dev), Cc, 1)
     nt = ops.conv_ntiles(B, H, W, K, Cc, wpk)
     part = torch.full((3 * Cc * nt,), float("nan"), device=dev)  # every slot must be written
@@ -480,7 +490,11 @@ def test_bf16_casts(dev):
 
 
 @pytest.mark.parametrize("case", [(2, 32, 40, 64, 0, 128), (1, 36, 64, 64, 64, 64),
-                                  (2, 40, 48, 8, 0, 64)])
+                                  (2, 40, 48, 8, 0, 64),
+                                  # the wide single-piece forms: 512 x 64 items (ragged
+                                  # rows too) and 256 x 128 items with a concat input
+                                  (2, 256, 256, 64, 0, 64), (2, 250, 254, 64, 0, 64),
+                                  (4, 128, 128, 64, 64, 128)])
 def test_conv_bf16_storage(dev, case):
     """bf16 activation storage (the bf16 arithmetic's, config 3): a conv whose output is
     stored in bf16 only writes exactly bf16(the fp32 output) -- persistent single-piece

@@ -14,7 +14,9 @@ import argparse
 import re
 import sys
 
-VMEM = re.compile(r"^(global_load\w*|global_store\w*|buffer_\w+|global_atomic\w*|flat_\w+)\b")
+# (scratch_* count in vmcnt too: a spill reload inside a loader pipeline would shift every
+# counted wait after it)
+VMEM = re.compile(r"^(global_load\w*|global_store\w*|buffer_\w+|global_atomic\w*|flat_\w+|scratch_\w+)\b")
 WAIT = re.compile(r"s_waitcnt\s+vmcnt\((\d+)\)")
 REG = re.compile(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b")
 LABEL = re.compile(r"^(\.?[\w.$]+):")
@@ -73,7 +75,8 @@ def step(state, s, line, report):
     m = VMEM.match(s)
     if m:
         parts = [p.strip() for p in operands.split(",")]
-        if m.group(1).startswith("global_load") and "lds" not in m.group(1):
+        if (m.group(1).startswith("global_load") or m.group(1).startswith("scratch_load")) \
+                and "lds" not in m.group(1):
             dst, srcs = regs(parts[0]), regs(",".join(parts[1:]))
         else:
             dst, srcs = frozenset(), regs(operands)

@@ -203,9 +203,15 @@ struct PackBatch {
     int n;
 };
 void launch_pack_x6_batch(const PackItem* items, int n, int np, hipStream_t st);
-int fwd_x6_tile_w(int W, int np);  // 32 or 16 (np = bf16 pieces: 3 split, 1 bf16)
-int fwd_x6_tile_h(int W, int np);  // 4, 8 or 16
-int fwd_x6_stat_slots(int ntiles, int W, int np);  // BatchNorm partial slots the forward writes
+// the split-bf16 / bf16 forward form of a shape (np = bf16 pieces: 3 split, 1 bf16; N =
+// output channels): pixel tile th x tw, 64-column weight slabs per item, pixel groups
+// (BatchNorm partial slots) per tile, persistent kernel or the single-stage one
+struct X6Form {
+    int th, tw, nslab, wm;
+    bool persistent;
+};
+X6Form x6_fwd_form(int B, int H, int W, int N, int np);
+int fwd_x6_stat_slots(const X6Form& f, int B, int H, int W);  // BatchNorm partial slots written
 void launch_wgrad_x6(const WgradArgs& a, int np, hipStream_t st);
 // split plan of the persistent split-bf16 wgrad (deterministic: planned for `cus` CUs)
 void wgrad_x6w_plan(int ntiles, int Cout, int Cin, int cus, int& nsplit, int& tps);

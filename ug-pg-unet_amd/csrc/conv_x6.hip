@@ -409,8 +409,8 @@ constexpr int X6_STG_WAVE = 2048;  // floats: 32 x 40 fp32, or the bf16 y tile o
 // wave's 32 channels) DMA'd into the wave's staging area as [mt][pixel][channel] bf16
 // (2 KiB per m-tile; 16 bytes per lane: pixel (lane>>2) + 16j, channels 8(lane&3)..)
 template <int TH, int TW, int MT>
-__device__ __forceinline__ void x6_dma_bnb_y(const ConvFwdArgs& a, int b, int ty0, int tx0, int n0,
-                                             int wm, int wn, float* stg) {
+__device__ __forceinline__ void x6_dma_bnb_y(const ConvFwdArgs& a, int b, int ty0, int tx0, int c0,
+                                             int wm, float* stg) {
     const int lane = threadIdx.x & 63;
     const int vh = min(TH, a.H - ty0), vw = min(TW, a.W - tx0);
 #pragma unroll
@@ -420,14 +420,17 @@ __device__ __forceinline__ void x6_dma_bnb_y(const ConvFwdArgs& a, int b, int ty
         for (int j = 0; j < 2; ++j) {
             const int px = min((lane >> 2) + 16 * j, vw - 1), k = lane & 3;
             const __bf16* g = a.bnb_y.h + ((size_t)(b * a.H + ty0 + py) * a.W + tx0 + px) * a.Cout +
-                              n0 + wn * 32 + 8 * k;
+                              c0 + 8 * k;
             glds16(g, reinterpret_cast<char*>(stg) + (mt * 2 + j) * 1024);
         }
     }
 }
-template <int TH, int TW, int MT>
+// Y32: the BatchNorm-backward partials may read an fp32 y (the 4 x 2-tile single-piece
+// forms need a bf16 y -- the host routes the rest to the 4 x 1 form -- which keeps this
+// path, and its registers, out of them)
+template <int TH, int TW, int MT, int WM = 2, bool Y32 = true>
 __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&acc)[MT], int tile,
-                                                 int b, int ty0, int tx0, int n0, int wm, int wn,
+                                                 int b, int ty0, int tx0, int c0, int wm,
                                                  float* stg) {
     static_assert(TW == 32, "one image row per 32-pixel MFMA tile");
     const int lane = threadIdx.x & 63, h = lane >> 5;
@@ -435,20 +438,20 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
     const bool fullw = vw == TW;
     float* out;
     int ostride, ocol0, oacc;
-    if (n0 < a.split) {
+    if (c0 < a.split) {  // (a 32-wide n-tile never straddles the split: split % 64 == 0)
         out = a.out0;
         ostride = a.split;
-        ocol0 = n0;
+        ocol0 = c0;
         oacc = a.acc0;
     } else {
         out = a.out1;
         ostride = a.Cout - a.split;
-        ocol0 = n0 - a.split;
+        ocol0 = c0 - a.split;
         oacc = a.acc1;
     }
-    const int nl = wn * 32 + (lane & 31);
-    const float bv = a.bias ? a.bias[n0 + nl] : 0.f;
-    const int lane_off = 4 * h * ostride + ocol0 + nl;
+    const int l32 = lane & 31;
+    const float bv = a.bias ? a.bias[c0 + l32] : 0.f;
+    const int lane_off = 4 * h * ostride + ocol0 + l32;
     // bf16 storage only (out0 == nullptr, one output): the stored -- rounded -- values are
     // the ones the BatchNorm statistics describe
     const bool only16 = out == nullptr;
@@ -480,12 +483,14 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
                     psum += v;
                 }
             }
+            // one m-tile's loads in flight at a time (the accumulate path's 64 loads at once
+            // cost the 4 x 2-tile forms their register headroom)
+            asm volatile("" ::: "memory");
         }
     };
     // bf16-only storage through the staging area (no accumulate, no bnb: the host allows
     // bf16-only outputs on forwards only)
     auto store16_rows = [&]() {
-        const int l32 = lane & 31;
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
             const int py = wm * MT + mt;
@@ -503,7 +508,7 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
                 stg[(p0 + 1) * X6_STG_PITCH + l32] = v1;
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            const size_t rowb = (size_t)((b * a.H + ty0 + py) * a.W + tx0) * ostride + ocol0 + wn * 32;
+            const size_t rowb = (size_t)((b * a.H + ty0 + py) * a.W + tx0) * ostride + ocol0;
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 const int p = (lane >> 2) + 16 * j, k = lane & 3;
@@ -530,7 +535,7 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
     if (bnb) {
         // BatchNorm-backward partials of the stored output (as x6q_epilogue_wave): this
         // lane's channel over its pixels, the two pixel halves (h) combined by a shuffle
-        const int n = n0 + nl;
+        const int n = c0 + l32;
         const float mu = a.bnb_mean[n], is = a.bnb_invstd[n], sc = a.bnb_scale[n],
                     sh = a.bnb_shift[n];
         float sg = 0.f, sgx = 0.f, sx = 0.f;
@@ -561,9 +566,9 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
                     acc[mt][r] += bv;
                     part(mt, r, (float)t16[((r & 3) + 8 * (r >> 2) + 4 * h) * 32]);
                 }
+                asm volatile("" ::: "memory");  // (as store_rows: one m-tile's reads at a time)
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // y reads done: reuse the area
-            const int l32 = lane & 31;
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt) {
                 const int py = wm * MT + mt;
@@ -571,7 +576,7 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
 #pragma unroll
                 for (int r = 0; r < 16; ++r) stg[((r & 3) + 8 * (r >> 2) + 4 * h) * 32 + l32] = acc[mt][r];
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                const size_t rowb = (size_t)((b * a.H + ty0 + py) * a.W + tx0) * ostride + ocol0 + wn * 32;
+                const size_t rowb = (size_t)((b * a.H + ty0 + py) * a.W + tx0) * ostride + ocol0;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int p = (lane >> 3) + 8 * j, k = lane & 7;
@@ -585,7 +590,7 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
         for (int mt = 0; mt < MT; ++mt) {
             const int py = wm * MT + mt;
             if (py >= vh) break;  // uniform
-            if (a.bnb_y.h) {
+            if (!Y32 || a.bnb_y.h) {
                 break;  // (done above)
             } else {
                 float yv[16];
@@ -605,7 +610,7 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
         sgx += __shfl_xor(sgx, 32, 64);
         sx += __shfl_xor(sx, 32, 64);
         if (lane < 32) {
-            const size_t S = 2 * (size_t)a.ntiles, slot = 2 * (size_t)tile + wm;
+            const size_t S = WM * (size_t)a.ntiles, slot = WM * (size_t)tile + wm;
             a.bnb_part[(0 * (size_t)a.Cout + n) * S + slot] = sg;
             a.bnb_part[(1 * (size_t)a.Cout + n) * S + slot] = sgx;
             a.bnb_part[(2 * (size_t)a.Cout + n) * S + slot] = sx;
@@ -633,7 +638,7 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
     }
     q += __shfl_xor(q, 32, 64);
     if (lane < 32) {
-        const size_t n = n0 + nl, S = 2 * (size_t)a.ntiles, slot = 2 * (size_t)tile + wm;
+        const size_t n = c0 + l32, S = WM * (size_t)a.ntiles, slot = WM * (size_t)tile + wm;
         a.stats[(0 * (size_t)a.Cout + n) * S + slot] = cnt;
         a.stats[(1 * (size_t)a.Cout + n) * S + slot] = s;
         a.stats[(2 * (size_t)a.Cout + n) * S + slot] = q;
@@ -916,7 +921,7 @@ extern "C" int ugpg_debug_clock(double* mhz) {
 // at bs16 (64 images' worth of 16 x 16 tiles x 8 column blocks = 128 items).  (Measured
 // and dropped: two compute waves per SIMD, 512-pixel single-piece items, column-block-major
 // item order.)
-template <int NP, bool M16, int TWT = 32, int THT = 256 / TWT, bool XB16 = false>
+template <int NP, bool M16, int TWT = 32, int THT = 256 / TWT, bool XB16 = false, int NSLAB = 1>
 __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) {
     constexpr int NCW = 4;  // compute waves (one per SIMD) + 4 loader waves
     static_assert(!M16 || NP == 3, "the 16x16x32 form pairs the split-bf16 products");
@@ -924,11 +929,22 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
     // per (pixel, 8 channels) instead of two
     static_assert(!XB16 || NP == 1, "bf16 sources only in the single-piece form");
     static_assert(TWT == 32 || (M16 && TWT == 16), "16-wide tiles only in the 16x16x32 form");
-    static_assert(THT * TWT == 256 || (M16 && THT * TWT == 128),
-                  "256-pixel items; 128 in the 16x16x32 form");
-    // 256-pixel items: 8 x 32 (images >= 32 wide) or 16 x 16 (16-31 wide, 16x16x32 form)
-    // MT: 32-pixel image rows per compute wave in the 32x32x16 form (two pixel halves)
-    constexpr int TW = TWT, TH = THT, BN = 64, BKC = 16, MT = TH / 2;
+    // items: 256 pixels (8 x 32, or 16 x 16 for 16-31 wide images in the 16x16x32 form;
+    // 128 = 8 x 16 there too) x 64 output channels; the single-piece form also runs
+    // 256 x 128 (NSLAB = 2 weight slabs of 64 columns) and 512 x 64 (16 x 32) items
+    static_assert(THT * TWT == 256 || (M16 && THT * TWT == 128) ||
+                      (NP == 1 && THT * TWT == 512 && NSLAB == 1),
+                  "item shapes");
+    static_assert(NSLAB == 1 || (NP == 1 && THT * TWT == 256 && NSLAB == 2), "64 x NSLAB columns");
+    constexpr int TW = TWT, TH = THT, BN = 64, BKC = 16, BNI = BN * NSLAB;
+    // 32x32x16 form: the compute waves as WM (pixel rows) x WN (columns); each covers
+    // MT 32-pixel image rows x NT 32-column n-tiles.  256 x 64 items: 2 x 2 waves of 4 x 1
+    // tiles (an A fragment feeds one MFMA); 256 x 128 and 512 x 64 items: 4 x 2 tiles per
+    // wave (each A fragment feeds two MFMAs, each B fragment four: 0.75 fragment reads per
+    // MFMA instead of 1.25 -- the single-piece form's LDS read traffic set its pace)
+    constexpr int WM = M16 ? 2 : TH / 4, WN = NCW / WM, MT = M16 ? TH / 2 : 4,
+                  NT = M16 ? 1 : BNI / (32 * WN);
+    static_assert(M16 || (WM * WN == NCW && NT >= 1 && MT * WM == TH), "wave grid");
     constexpr int HWD = TW + 2, HS = HWD;
     constexpr int NHALO = (TH + 2) * HWD;                   // 340 / 324 halo pixels
     // spare slot NHALO; plane pitch 348 = 4 (mod 8) for the 32x32 fragment pattern, 352
@@ -942,9 +958,9 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
     constexpr int A_ITEMS = (NHALO + 15) / 16 * 32;         // 704 / 672 incl. idle lanes
     constexpr int A_PER = (A_ITEMS + 255) / 256;            // 3
     constexpr int A_VECS = 2 * NP * NHP;
-    constexpr int R_VEC = NP * 2 * 3 * BN;                  // one kernel row of weights
+    constexpr int R_VEC = NP * 2 * 3 * BN;                  // one kernel row of a 64-column slab
     constexpr int R_PER = (R_VEC + 255) / 256;
-    constexpr int R_STR = R_VEC;                            // ring slot pitch
+    constexpr int R_STR = NSLAB * R_VEC;                    // ring slot pitch: the item's slabs
     // weight rows DMA'd LA rows ahead of the row the compute waves read (ring NSLOT >=
     // LA + 1).  Three rows = two phases of flight cover the DMA latency when a phase holds
     // 3 x 6 split-bf16 MFMA groups; the single-piece form's phases are a sixth as long,
@@ -955,7 +971,8 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
 #ifndef X6R_CTAB_MAX  // channels of both sources the single-piece LDS coefficient table holds
 #define X6R_CTAB_MAX 2048
 #endif
-    constexpr int LA = NP == 1 ? X6R_NP1_LA : 3;
+    // (the single-piece form's larger items have phases twice as long: three rows ahead)
+    constexpr int LA = NP == 1 && TH * TW * NSLAB == 256 ? X6R_NP1_LA : 3;
     static_assert(LA == 3 || LA == 6, "row lookahead: one or two steps");
     constexpr int NSLOT = LA == 3 ? 4 : 8;
     __shared__ __attribute__((aligned(16))) u32x4 smem[2 * A_VECS + NSLOT * R_STR + 1];
@@ -966,14 +983,14 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
     constexpr int CTAB_N = CTAB ? X6R_CTAB_MAX : 4;
     __shared__ __attribute__((aligned(16))) float ctab[2][CTAB_N];
     // the 32x32-form epilogue's per-wave staging of bf16-only outputs (x6_epilogue_wave)
-    constexpr int OSTG_N = M16 ? 4 : NCW * X6_STG_WAVE;
+    constexpr int OSTG_N = M16 ? 4 : NCW * NT * X6_STG_WAVE;
     __shared__ __attribute__((aligned(16))) float ostg[OSTG_N];
     u32x4* const Bring = smem + 2 * A_VECS;
     u32x4* const dummy = smem + 2 * A_VECS + NSLOT * R_STR;  // writes of idle lanes
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const bool loader = wave >= NCW;
-    const int NB = a.Cout / BN;
+    const int NB = a.Cout / BNI;
     const int nitems = a.ntiles * NB;
     const int nslots = gridDim.x >> 3;
     const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
@@ -1163,13 +1180,16 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
         static_assert(R_VEC % 64 == 0, "whole wave-instructions");
         const int lw = lt >> 6;
         auto dma_row = [&](const Cur& q, int ky, int slot) {
-            const u32x4* ws = static_cast<const u32x4*>(a.wpk) +
-                              (((size_t)q.nb * nchunk + q.c) * 3 + ky) * R_VEC;
-            u32x4* Bs = Bring + slot * R_STR;
 #pragma unroll
-            for (int v = 0; v < R_PER; ++v) {
-                const int base = v * 256 + (v + 1 < R_PER ? lw : lw % R_LASTW) * 64;
-                glds16(ws + base + lane, Bs + base);
+            for (int sb = 0; sb < NSLAB; ++sb) {
+                const u32x4* ws = static_cast<const u32x4*>(a.wpk) +
+                                  (((size_t)(q.nb * NSLAB + sb) * nchunk + q.c) * 3 + ky) * R_VEC;
+                u32x4* Bs = Bring + slot * R_STR + sb * R_VEC;
+#pragma unroll
+                for (int v = 0; v < R_PER; ++v) {
+                    const int base = v * 256 + (v + 1 < R_PER ? lw : lw % R_LASTW) * 64;
+                    glds16(ws + base + lane, Bs + base);
+                }
             }
         };
         // prologue: step 0 in LDS (halo buffer 0, rows 0-2), halos 1 and 2 in registers
@@ -1217,7 +1237,7 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
         // phase 2 reloads the freed register set with halo(k+3).  vmcnt counts the
         // loader's loads and DMAs together, in issue order: retiring a row retires every
         // older halo load too.
-        constexpr int R = R_PER, H = HALO_LOADS;
+        constexpr int R = NSLAB * R_PER, H = HALO_LOADS;  // loads per weight row / halo
         constexpr int HA = (A_PER + 1) / 2;  // halo vectors written in phase 0
 #ifdef X6R_STAMP
         // diagnostic build: loader cycles spent waiting for global loads / at barriers
@@ -1325,7 +1345,7 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
 #endif
 
     // ---------------------------------------------------------------- compute waves
-    const int wm = wave >> 1, wn = wave & 1;
+    const int wm = wave / WN, wn = wave % WN;
     if constexpr (M16) {
         // 16x16x32 form: D[oc][px] = W x A with the split-bf16 products paired along k:
         // k-groups (lanes 16g..16g+15) 0,1 = channels 0-7, 8-15 of one piece, 2,3 of
@@ -1442,30 +1462,42 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
         CS_STORE();
         return;
     } else {
-    f32x16 acc[MT];
+    // acc[nt][mt]: n-tile nt (columns (wn*NT + nt)*32 of the item) of m-tile mt (image row
+    // wm*MT + mt of the item)
+    f32x16 acc[NT][MT];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
+    for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[mt][r] = 0.f;
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[nt][mt][r] = 0.f;
     const int hl = lane >> 5;
     const int aoff = hl * NHP + (wm * MT) * HS + (lane & 31);  // + mt*HS + ky*HS + kx
-    const int boff = hl * 3 * BN + wn * 32 + (lane & 31);
+    // n-tile nt of this wave: 32 columns of the ring slot's slab (wn*NT + nt) / 2 (the
+    // wave's first column (wn*NT)*32 is a multiple of 64 when NT = 2)
+    const int boff0 = (NT == 1 ? wn * 32 : wn * (R_VEC * NT / 2)) + hl * 3 * BN + (lane & 31);
+    auto boff = [&](int nt) { return boff0 + (nt / 2) * R_VEC + (nt % 2) * 32; };
     auto ldfrag = [&](const u32x4* As, const u32x4* Bs, int ky, int kx, u32x4 (&af)[MT][NP],
-                      u32x4 (&bf)[NP]) {
+                      u32x4 (&bf)[NT][NP]) {
 #pragma unroll
         for (int q = 0; q < NP; ++q) {
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt) af[mt][q] = As[q * 2 * NHP + aoff + (mt + ky) * HS + kx];
-            bf[q] = Bs[q * 2 * 3 * BN + boff + kx * BN];
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) bf[nt][q] = Bs[q * 2 * 3 * BN + boff(nt) + kx * BN];
         }
     };
     // Every weight row a phase reads was completed a full phase earlier (the ring runs
     // one step ahead), so the fragments of the next phase's first tap are read BEFORE
     // the phase's barrier: the barriers only order the loaders' overwrites and expose
     // no LDS latency inside a step.
-    // single-piece pipeline state (fragments of the taps two ahead; see the loop)
-    u32x4 fa1[3][MT][NP], fb1[3][NP];
-    auto ldfrag1 = [&](int kk, int t, u32x4 (&af)[MT][NP], u32x4 (&bf)[NP]) {
+    // single-piece pipeline state: fragments read PD taps ahead into a ring of 3 sets
+    // (9 taps per step: the set of a tap is t % 3 in every step).  Two taps ahead where a
+    // tap is 4 MFMAs; one where it is 8 (whose 256 cycles cover the reads, and whose
+    // 128 accumulator registers leave room for only two sets in flight)
+    constexpr int PD = NT == 1 ? 2 : 1;
+    u32x4 fa1[3][MT][NP], fb1[3][NT][NP];
+    auto ldfrag1 = [&](int kk, int t, u32x4 (&af)[MT][NP], u32x4 (&bf)[NT][NP]) {
         const int ky = t / 3, kx = t % 3;
         ldfrag(smem + (kk & 1) * A_VECS, Bring + ((3 * kk + ky) % NSLOT) * R_STR, ky, kx, af, bf);
     };
@@ -1476,41 +1508,51 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
 #endif
     int cc = 0, item = item0;
     Pos cp = pos_of(item0);
-    if constexpr (NP == 1 && MT <= 4) {
-        ldfrag1(0, 0, fa1[0], fb1[0]);
-        ldfrag1(0, 1, fa1[1], fb1[1]);
+    // the wave's staging: NT areas of X6_STG_WAVE floats at ostg + (wave * NT + nt) * X6_STG_WAVE
+    if constexpr (NP == 1) {
+#pragma unroll
+        for (int t = 0; t < PD; ++t) ldfrag1(0, t, fa1[t], fb1[t]);
     }
     for (int k = 0; k < total; ++k) {
         const u32x4* Ac = smem + (k & 1) * A_VECS;
         if constexpr (NP == 1) {
             // the item's last step: its BatchNorm-backward y tile (bf16) goes to the staging
             // area now, so the epilogue finds it landed
-            if (cc == nchunk - 1 && a.bnb_part && a.bnb_y.h)
-                x6_dma_bnb_y<TH, TW, MT>(a, cp.b, cp.ty0, cp.tx0, cp.nb * BN, wm, wn,
-                                         ostg + wave * X6_STG_WAVE);
-            // single piece: 4 MFMAs per tap cannot cover the next tap's fragment reads, so
-            // the reads run two taps ahead, across the step boundary (the next step's first
-            // two taps are read in phase 2: halo(k+1) and row 3k+3 are visible from there)
+            if (cc == nchunk - 1 && a.bnb_part && a.bnb_y.h) {
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+                    x6_dma_bnb_y<TH, TW, MT>(a, cp.b, cp.ty0, cp.tx0,
+                                             cp.nb * BNI + (wn * NT + nt) * 32, wm,
+                                             ostg + (wave * NT + nt) * X6_STG_WAVE);
+            }
+            // single piece: the reads run PD taps ahead, across the step boundary (the next
+            // step's first taps are read in phase 2: halo(k+1) and row 3k+3 are visible there)
 #pragma unroll
             for (int t = 0; t < 9; ++t) {
-                if (t + 2 < 9) ldfrag1(k, t + 2, fa1[(t + 2) % 3], fb1[(t + 2) % 3]);
-                else ldfrag1(k + 1, t + 2 - 9, fa1[(t + 2) % 3], fb1[(t + 2) % 3]);
+                if (t + PD < 9) ldfrag1(k, t + PD, fa1[(t + PD) % 3], fb1[(t + PD) % 3]);
+                else if (NT == 1 || cc != nchunk - 1)  // (NT = 2: not across an epilogue)
+                    ldfrag1(k + 1, t + PD - 9, fa1[(t + PD) % 3], fb1[(t + PD) % 3]);
 #pragma unroll
-                for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma_xn<NP>(fa1[t % 3][mt], fb1[t % 3], acc[mt]);
-                constexpr int NM = MT, NR = MT + 1;
+                for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt)
+                        acc[nt][mt] = mfma_xn<NP>(fa1[t % 3][mt], fb1[t % 3][nt], acc[nt][mt]);
+                constexpr int NM = MT * NT, NR = MT + NT;
 #pragma unroll
                 for (int i = 0; i < NM; ++i) {
                     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
                     if (i < NR) {
-                        if (i == 0) __builtin_amdgcn_sched_group_barrier(0x100, NR - NM + 1, 0);
-                        else __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                        if (NR > NM && i == 0)
+                            __builtin_amdgcn_sched_group_barrier(0x100, NR - NM + 1, 0);
+                        else
+                            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                     }
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 if (t % 3 == 2) CS_WAIT(cs_bar, read_barrier());
             }
         } else {
-        u32x4 fa[2][MT][NP], fb[2][NP];
+        u32x4 fa[2][MT][NP], fb[2][NT][NP];
         ldfrag(Ac, Bring + ((3 * k) % NSLOT) * R_STR, 0, 0, fa[0], fb[0]);
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
@@ -1520,10 +1562,13 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
                        fb[(t + 1) & 1]);
             }
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma_xn<NP>(fa[t & 1][mt], fb[t & 1], acc[mt]);
+            for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+                    acc[nt][mt] = mfma_xn<NP>(fa[t & 1][mt], fb[t & 1][nt], acc[nt][mt]);
             // the next tap's fragment reads go out one per MFMA gap from the start of
             // this tap's MFMAs (fresh registers, landed long before their use)
-            constexpr int NM = MT * (NP == 3 ? 6 : 1), NR = (MT + 1) * NP;
+            constexpr int NM = MT * NT * (NP == 3 ? 6 : 1), NR = (MT + NT) * NP;
 #pragma unroll
             for (int i = 0; i < NM; ++i) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                     // MFMA
@@ -1537,16 +1582,31 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
         }
         }
         if (++cc == nchunk) {
-            CS_WAIT(cs_epi, (x6_epilogue_wave<TH, TW, MT>(a, acc, cp.tile, cp.b, cp.ty0, cp.tx0,
-                                                          cp.nb * BN, wm, wn,
-                                                          ostg + wave * X6_STG_WAVE)));
+            // (explicit calls: a loop around the inlined epilogue cost the allocator ~240
+            // spilled registers)
+            CS_WAIT(cs_epi, (x6_epilogue_wave<TH, TW, MT, WM, NT == 1>(
+                                a, acc[0], cp.tile, cp.b, cp.ty0, cp.tx0, cp.nb * BNI + wn * NT * 32,
+                                wm, ostg + wave * NT * X6_STG_WAVE)));
+            if constexpr (NT > 1)
+                CS_WAIT(cs_epi, (x6_epilogue_wave<TH, TW, MT, WM, NT == 1>(
+                                    a, acc[1], cp.tile, cp.b, cp.ty0, cp.tx0,
+                                    cp.nb * BNI + (wn * NT + 1) * 32, wm,
+                                    ostg + (wave * NT + 1) * X6_STG_WAVE)));
+            static_assert(NT <= 2, "two n-tiles at most");
+            if constexpr (NP == 1 && NT > 1) {
+                // the next step's first taps, not held in registers across the epilogue
+#pragma unroll
+                for (int t = 0; t < PD; ++t) ldfrag1(k + 1, t, fa1[t], fb1[t]);
+            }
             cc = 0;
             item += nslots;
             if (item < iend) cp = pos_of(item);
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
+            for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) acc[mt][r] = 0.f;
+                for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) acc[nt][mt][r] = 0.f;
         }
     }
 #ifdef X6R_CLOCK
@@ -2152,10 +2212,29 @@ __global__ void __launch_bounds__(256) pack_x6_tile_kernel(PackBatch pb, int np)
 // Measured and dropped (round 2): 16 x 16 items for the 16-wide layers, the 32x32x16 form
 // for split-bf16, 512-pixel single-piece items, two compute waves per SIMD.
 static bool use_x6r(int W, int np) { return W >= 32 || (np == 3 && W >= 16); }
-int fwd_x6_tile_w(int W, int np) { return W >= 32 ? 32 : 16; }
-int fwd_x6_tile_h(int W, int np) { return 8; }
-int fwd_x6_stat_slots(int ntiles, int W, int np) {
-    return use_x6r(W, np) ? 2 * ntiles : ntiles;  // persistent forms: one slot per pixel half
+//  - single-piece (bf16) images >= 32 wide: 256 x 128 items (8 x 32 pixels, two 64-column
+//    weight slabs) where N is a multiple of 128, 512 x 64 items (16 x 32 pixels) where
+//    N = 64 -- each compute wave 4 x 2 MFMA tiles, 0.75 LDS fragment reads per MFMA
+//    instead of 1.25 -- unless that leaves fewer items than a 256-CU device has: then the
+//    256 x 64 items.  The plan assumes 256 CUs whatever the device, so the BatchNorm
+//    partial order (the slot layout) is a function of the shape only.
+X6Form x6_fwd_form(int B, int H, int W, int N, int np) {
+    if (np == 3) {
+        if (W >= 32) return {8, 32, 1, 2, true};
+        if (W >= 16) return {8, 16, 1, 2, true};
+        return {8, 16, 1, 1, false};
+    }
+    if (W < 32) return {8, 16, 1, 1, false};
+    constexpr int64_t kPlanCUs = 256;
+    const int64_t tiles8 = (int64_t)B * cdiv(H, 8) * cdiv(W, 32);
+    const int64_t tiles16 = (int64_t)B * cdiv(H, 16) * cdiv(W, 32);
+    if (N % 128 == 0 && tiles8 * (N / 128) >= kPlanCUs) return {8, 32, 2, 2, true};
+    if (N % 128 != 0 && tiles16 * (N / 64) >= kPlanCUs) return {16, 32, 1, 4, true};
+    return {8, 32, 1, 2, true};
+}
+int fwd_x6_stat_slots(const X6Form& f, int B, int H, int W) {
+    const int ntiles = (int)(B * cdiv(H, f.th) * cdiv(W, f.tw));
+    return f.persistent ? f.wm * ntiles : ntiles;  // persistent forms: one slot per pixel group
 }
 
 // ---------------------------------------------------------------------------
@@ -2445,7 +2524,8 @@ bool launch_img_fwd(const ConvFwdArgs& a, bool wf32, hipStream_t st) {
 }
 
 int launch_fwd_x6(const ConvFwdArgs& a, int np, hipStream_t st) {
-    const int64_t items = (int64_t)a.ntiles * (a.Cout / 64);
+    const X6Form f = x6_fwd_form(a.B, a.H, a.W, a.Cout, np);
+    const int64_t items = (int64_t)a.ntiles * (a.Cout / (64 * f.nslab));
     if (np == 3 && use_x6r(a.W, np) && a.Cin == 16 && launch_img_fwd(a, false, st))
         return FWD_WROTE_OUT16;
     if (use_x6r(a.W, np)) {
@@ -2459,15 +2539,29 @@ int launch_fwd_x6(const ConvFwdArgs& a, int np, hipStream_t st) {
         else if (np == 3)
             hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<3, true>), dim3((unsigned)g), dim3(512), 0,
                                st, a);
-        else if (!a.src0 && a.src0_16 && (a.C1 == 0 || (!a.src1 && a.src1_16)))
-            hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 8, true>), dim3((unsigned)g),
-                               dim3(512), 0, st, a);
-        else
-            hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false>), dim3((unsigned)g), dim3(512), 0,
-                               st, a);
-        // every persistent form fuses the BatchNorm-backward partials into its epilogue;
-        // the 32x32x16 (single-piece) form also writes the bf16 copy of its output
-        return FWD_WROTE_BNB | (np == 3 ? 0 : FWD_WROTE_OUT16);
+        else {
+            const bool xb16 = !a.src0 && a.src0_16 && (a.C1 == 0 || (!a.src1 && a.src1_16));
+            const dim3 grid((unsigned)g), block(512);
+            // the 4 x 2-tile forms fuse the BatchNorm-backward partials of a bf16 y only
+            // (x6_epilogue_wave Y32); with an fp32 y the caller's reduction pass writes them
+            ConvFwdArgs b = a;
+            const bool wide = f.nslab == 2 || f.th == 16;
+            const bool nofuse = wide && a.bnb_part && !a.bnb_y.h;
+            if (nofuse) b.bnb_part = nullptr;
+            if (f.nslab == 2) {
+                if (xb16) hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 8, true, 2>), grid, block, 0, st, b);
+                else hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 8, false, 2>), grid, block, 0, st, b);
+            } else if (f.th == 16) {
+                if (xb16) hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 16, true>), grid, block, 0, st, b);
+                else hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 16, false>), grid, block, 0, st, b);
+            } else {
+                if (xb16) hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 8, true>), grid, block, 0, st, b);
+                else hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 8, false>), grid, block, 0, st, b);
+            }
+            return (nofuse ? 0 : FWD_WROTE_BNB) | FWD_WROTE_OUT16;
+        }
+        // every persistent form fuses the BatchNorm-backward partials into its epilogue
+        return FWD_WROTE_BNB;
     }
     // single-stage kernel: 8 x 16-pixel tiles (fwd_x6_tile_*)
     const unsigned grid = (unsigned)items;
