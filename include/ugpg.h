@@ -110,9 +110,10 @@ typedef struct {
     int bnb_slots;         /* capacity of bnb_part in slots */
     /* bf16 output (one output, no accumulate): with out[0] != NULL a copy written beside
      * it; with out[0] == NULL the only storage of the output (the bf16 arithmetic's
-     * activation storage: the BatchNorm partials then describe the rounded values) --
-     * supported by the persistent single-piece form (images >= 32 wide) and the
-     * image-layer kernel */
+     * activation storage: the BatchNorm partials then describe the rounded values; with
+     * bnb_part, the bf16 arithmetic's data gradient, whose BatchNorm-backward partials
+     * then describe the rounded da and need bnb_y_bf16) -- supported by the persistent
+     * single-piece form (images >= 32 wide) and the image-layer kernel */
     void* out_bf16;
 } ugpg_conv_t;
 
@@ -210,8 +211,11 @@ int ugpg_bnb_slots(int64_t npix, int C);
 /* (y: the BN input in fp32, or y == NULL and y_bf16 its bf16 storage) */
 /* dy: fp32, or dy == NULL and dy_bf16 receives it rounded to bf16 (nearest even) -- under
  * the bf16 arithmetic exactly the operand its data and weight gradients read (one of the
- * two, never both) */
-int ugpg_bn_relu_bwd_partials(const float* part, int nslots, const float* da, const float* y,
+ * two, never both).  da: fp32, or da == NULL and da_bf16 its bf16 storage (the bf16
+ * arithmetic's data gradient written by ugpg_conv3x3_fwd with out_bf16 and bnb_part; y and
+ * dy then in bf16 too). */
+int ugpg_bn_relu_bwd_partials(const float* part, int nslots, const float* da,
+                              const void* da_bf16, const float* y,
                               const void* y_bf16, int64_t npix, int C, const float* mean,
                               const float* invstd, const float* scale, const float* shift,
                               float* dy, void* dy_bf16, float* dgamma, float* dbeta,

@@ -167,10 +167,33 @@ def _bf16_store(y):
     return CONV_MATH == "bf16" and BF16_STORE and y.shape[-1] >= 32
 
 
+class _Bf16GradRound(torch.autograd.Function):
+    """Identity forward; the gradient rounded to bf16 (nearest even): the data gradient of
+    a conv stored in bf16, as torch.autocast's conv backward returns grad_input."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x
+
+    @staticmethod
+    def backward(ctx, g):
+        return _bq(g)
+
+
+# The build's bf16 arithmetic also stores the data gradient of each DoubleConv's second
+# conv -- dL/d(its input), the first BatchNorm+ReLU's output gradient -- in bf16 for images
+# >= 32 wide (the x6r single-piece epilogue writes da1 in bf16 with the BatchNorm-backward
+# partials of the rounded values; the BN1 backward reads it).  Off only for experiments.
+BF16_DGRAD_STORE = True
+
+
 def double_conv(P, prefix, x, training):
     """Two conv -> BN -> ReLU.  Under CONV_MATH "bf16" a conv output of an image >= 32
-    wide is stored in bf16 before its BatchNorm (see _bf16_store)."""
+    wide is stored in bf16 before its BatchNorm (see _bf16_store), and so is the data
+    gradient of the second conv (BF16_DGRAD_STORE)."""
     for conv_i, bn_i in ((0, 1), (3, 4)):
+        if conv_i == 3 and BF16_DGRAD_STORE and _bf16_store(x):
+            x = _Bf16GradRound.apply(x)
         y = conv3x3(x, P[f"{prefix}.{conv_i}.weight"], P[f"{prefix}.{conv_i}.bias"])
         if _bf16_store(y):
             y = _Bf16StoreST.apply(y)

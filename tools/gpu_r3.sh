@@ -34,6 +34,8 @@ for s in "$@"; do
             step wstamp_${lib}_${math} 300 env UGPG_LIB=exp/$lib.so python tools/clock_probe.py --stamps --wgrad --seconds 1 --math $math --out16 --layers inc.3,down1.3,down2.3,down3.3,up4.0 ;;
     stamp:*) IFS=: read -r _ lib math <<< "$s"
             step stamp_${lib}_${math} 300 env UGPG_LIB=exp/$lib.so python tools/clock_probe.py --stamps --seconds 1 --math $math --out16 --layers inc.3,down1.3,down2.3,down3.3,up4.0 ;;
+    tests:*@@*) f=${s#tests:}; file=${f%%@@*}; kx=${f#*@@}; n=$(basename "$file" .py)
+            step t_${n} 900 python -u -m pytest "$file" -k "$kx" -q -rf -x --timeout 400 --timeout-method thread -p no:cacheprovider ;;
     tests:*) f=${s#tests:}; n=$(basename "${f%% *}" .py); step t_${n%%::*} 900 python -u -m pytest $f -q -rf -x --timeout 400 --timeout-method thread -p no:cacheprovider ;;
     alltests) step alltests 1100 python -u -m pytest tests -m gpu -q -rf --timeout 500 --timeout-method thread -p no:cacheprovider ;;
     ab:*) IFS=: read -r _ libs layers <<< "$s"

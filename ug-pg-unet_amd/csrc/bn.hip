@@ -253,8 +253,9 @@ struct Route {
     const float* w;     // HEAD: [nc][C]
     int nc, H, W;
 };
-template <bool NT, typename TY, typename TO, int ROUTE = ROUTE_NONE>
-__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const float* da, const TY* __restrict__ y,
+// TD: the storage of da (float, or __bf16: the bf16 arithmetic's data gradient, ROUTE_NONE)
+template <bool NT, typename TY, typename TO, int ROUTE = ROUTE_NONE, typename TD = float>
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const TD* da, const TY* __restrict__ y,
                                                            int64_t npix, int C, const float* mean,
                                                            const float* invstd, const float* scale,
                                                            const float* shift, const float* coef,
@@ -331,7 +332,9 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const float* da, cons
         }
         return o;
     };
+    static_assert(std::is_same<TD, float>::value || ROUTE == ROUTE_NONE, "bf16 da: no route");
     const f32x4* D = reinterpret_cast<const f32x4*>(da);
+    const uint2* D16 = reinterpret_cast<const uint2*>(da);
     auto store = [&](int64_t k, f32x4 o) {
         if constexpr (std::is_same<TO, float>::value) {
             reinterpret_cast<f32x4*>(dy)[k] = o;
@@ -361,8 +364,14 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const float* da, cons
             f32x4 g = routed(p);
             if (da) g += NT ? __builtin_nontemporal_load(D + k) : D[k];
             return g;
-        } else {
+        } else if constexpr (std::is_same<TD, float>::value) {
             return NT ? __builtin_nontemporal_load(D + k) : D[k];
+        } else {  // 4 bf16 (exact widening)
+            const uint2 u = NT ? uint2{__builtin_nontemporal_load(&D16[k].x),
+                                       __builtin_nontemporal_load(&D16[k].y)}
+                               : D16[k];
+            return f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                         __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
         }
     };
     int64_t i = i0;
@@ -412,7 +421,15 @@ template <int ROUTE>
 void launch_bn_apply_t(unsigned ga, hipStream_t st, const float* da, YRef y, int64_t npix,
                        int C, const float* mean, const float* invstd, const float* scale,
                        const float* shift, const float* coef, float* dy, __bf16* dy16,
-                       Route rt) {
+                       Route rt, const __bf16* da16 = nullptr) {
+    if constexpr (ROUTE == ROUTE_NONE) {
+        if (da16) {  // (the host admits bf16 da with bf16 y and bf16 dy only)
+            hipLaunchKernelGGL((bn_bwd_apply_kernel<true, __bf16, __bf16, ROUTE_NONE, __bf16>),
+                               dim3(ga), dim3(256), 0, st, da16, y.h, npix, C, mean, invstd,
+                               scale, shift, coef, dy16, rt);
+            return;
+        }
+    }
     if (y.f && dy)
         hipLaunchKernelGGL((bn_bwd_apply_kernel<true, float, float, ROUTE>), dim3(ga), dim3(256),
                            0, st, da, y.f, npix, C, mean, invstd, scale, shift, coef, dy, rt);
@@ -430,7 +447,7 @@ void launch_bn_apply_t(unsigned ga, hipStream_t st, const float* da, YRef y, int
 void launch_bn_apply(unsigned ga, hipStream_t st, const float* da, YRef y, int64_t npix,
                      int C, const float* mean, const float* invstd, const float* scale,
                      const float* shift, const float* coef, float* dy, __bf16* dy16,
-                     int kind = ROUTE_NONE, Route rt = {}) {
+                     int kind = ROUTE_NONE, Route rt = {}, const __bf16* da16 = nullptr) {
     if (kind == ROUTE_POOL)
         launch_bn_apply_t<ROUTE_POOL>(ga, st, da, y, npix, C, mean, invstd, scale, shift, coef,
                                       dy, dy16, rt);
@@ -439,7 +456,7 @@ void launch_bn_apply(unsigned ga, hipStream_t st, const float* da, YRef y, int64
                                       dy, dy16, rt);
     else
         launch_bn_apply_t<ROUTE_NONE>(ga, st, da, y, npix, C, mean, invstd, scale, shift, coef,
-                                      dy, dy16, rt);
+                                      dy, dy16, rt, da16);
 }
 constexpr int64_t kBwdBlocks = 2048, kBwdPpt = 8;
 namespace {
@@ -563,11 +580,16 @@ static int bn_relu_bwd_partials(int kind, const Route& rt, const float* part, in
                                 int64_t npix, int C, const float* mean, const float* invstd,
                                 const float* scale, const float* shift, float* dy, void* dy_bf16,
                                 float* dgamma, float* dbeta, float* dbias, int acc, void* ws,
-                                size_t ws_bytes, void* stream) {
+                                size_t ws_bytes, void* stream, const void* da_bf16 = nullptr) {
     const YRef y = yref(y_f32, y_bf16);
-    if (!part || nslots <= 0 || (!da && kind == ROUTE_NONE) || (!y.f && !y.h) || !dy == !dy_bf16 || !mean ||
-        !invstd || !scale || !shift || C % 4 || C <= 0 || C > 1024 || npix <= 0) {
+    if (!part || nslots <= 0 || (!da && !da_bf16 && kind == ROUTE_NONE) || (da && da_bf16) ||
+        (!y.f && !y.h) || !dy == !dy_bf16 || !mean || !invstd || !scale || !shift || C % 4 ||
+        C <= 0 || C > 1024 || npix <= 0) {
         set_error("bn_relu_bwd_partials: bad arguments (C=%d nslots=%d)", C, nslots);
+        return UGPG_ERR_INVALID;
+    }
+    if (da_bf16 && (kind != ROUTE_NONE || y.f || dy)) {
+        set_error("bn_relu_bwd_partials: a bf16 da needs a bf16 y and a bf16 dy");
         return UGPG_ERR_INVALID;
     }
     const size_t need = ugpg_bn_relu_bwd_partials_workspace(C);
@@ -583,19 +605,20 @@ static int bn_relu_bwd_partials(int kind, const Route& rt, const float* part, in
     const unsigned q = (unsigned)(C / std::gcd(1024, C));
     const unsigned ga = (apply_grid(npix * C / 4) + q - 1) / q * q;
     launch_bn_apply(ga, st, da, y, npix, C, mean, invstd, scale, shift, coef, dy,
-                    static_cast<__bf16*>(dy_bf16), kind, rt);
+                    static_cast<__bf16*>(dy_bf16), kind, rt, static_cast<const __bf16*>(da_bf16));
     return check_launch("bn_bwd_apply");
 }
 
 extern "C" int ugpg_bn_relu_bwd_partials(const float* part, int nslots, const float* da,
-                                         const float* y_f32, const void* y_bf16, int64_t npix,
-                                         int C, const float* mean, const float* invstd,
+                                         const void* da_bf16, const float* y_f32,
+                                         const void* y_bf16, int64_t npix, int C,
+                                         const float* mean, const float* invstd,
                                          const float* scale, const float* shift, float* dy,
                                          void* dy_bf16, float* dgamma, float* dbeta, float* dbias,
                                          int acc, void* ws, size_t ws_bytes, void* stream) {
-    return bn_relu_bwd_partials(ROUTE_NONE, Route{}, part, nslots, da, y_f32, y_bf16, npix, C, mean, invstd,
-                                scale, shift, dy, dy_bf16, dgamma, dbeta, dbias, acc, ws,
-                                ws_bytes, stream);
+    return bn_relu_bwd_partials(ROUTE_NONE, Route{}, part, nslots, da, y_f32, y_bf16, npix, C,
+                                mean, invstd, scale, shift, dy, dy_bf16, dgamma, dbeta, dbias, acc,
+                                ws, ws_bytes, stream, da_bf16);
 }
 
 extern "C" int ugpg_bn_relu_bwd_partials_routed(const ugpg_bwd_route_t* route, const float* part,

@@ -840,6 +840,11 @@ extern "C" int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream) {
                   "one output and no accumulate");
         return UGPG_ERR_INVALID;
     }
+    if (bnb && b16_out && !p->bnb_y_bf16) {
+        set_error("conv3x3_fwd: a bf16-only output with BatchNorm-backward partials needs the "
+                  "BN input in bf16 (bnb_y_bf16)");
+        return UGPG_ERR_INVALID;
+    }
     if (p->stats && (p->out_split != p->Cout || p->accumulate[0])) {
         set_error("conv3x3_fwd: BatchNorm partials (stats) need one output and no accumulate");
         return UGPG_ERR_INVALID;

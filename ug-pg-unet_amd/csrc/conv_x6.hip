@@ -488,22 +488,28 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
             asm volatile("" ::: "memory");
         }
     };
-    // bf16-only storage through the staging area (no accumulate, no bnb: the host allows
-    // bf16-only outputs on forwards only)
-    auto store16_rows = [&]() {
+    // bf16-only storage through the staging area (no accumulate).  FINAL: acc already holds
+    // the rounded values with bias (the data gradient's epilogue with BatchNorm-backward
+    // partials rounds before its partials), else bias, rounding and the statistics sum here
+    auto store16_rows = [&](auto final_) {
+        constexpr bool FINAL = decltype(final_)::value;
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
             const int py = wm * MT + mt;
             if (py >= vh) break;  // uniform
 #pragma unroll
             for (int r = 0; r < 16; r += 2) {
-                float v0, v1;
-                pk_bf16(acc[mt][r] + bv, acc[mt][r + 1] + bv, v0, v1);
-                acc[mt][r] = v0;
-                acc[mt][r + 1] = v1;
+                float v0 = acc[mt][r], v1 = acc[mt][r + 1];
+                if constexpr (!FINAL) {
+                    pk_bf16(v0 + bv, v1 + bv, v0, v1);
+                    acc[mt][r] = v0;
+                    acc[mt][r + 1] = v1;
+                }
                 const int p0 = (r & 3) + 8 * (r >> 2) + 4 * h;  // r + 1: pixel p0 + 1
-                if (fullw || p0 < vw) psum += v0;
-                if (fullw || p0 + 1 < vw) psum += v1;
+                if constexpr (!FINAL) {
+                    if (fullw || p0 < vw) psum += v0;
+                    if (fullw || p0 + 1 < vw) psum += v1;
+                }
                 stg[p0 * X6_STG_PITCH + l32] = v0;
                 stg[(p0 + 1) * X6_STG_PITCH + l32] = v1;
             }
@@ -529,7 +535,7 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
     const bool bnb = a.bnb_part != nullptr && !oacc;  // (the host refuses bnb + accumulate)
     EPI_T(et0);
     if (oacc) store_rows(std::integral_constant<bool, true>{}, 0, MT);
-    else if (only16 && !bnb) store16_rows();
+    else if (only16 && !bnb) store16_rows(std::false_type{});
     else if (!bnb) store_rows(std::integral_constant<bool, false>{}, 0, MT);
     EPI_T(et1);
     if (bnb) {
@@ -562,15 +568,23 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
                 if (wm * MT + mt >= vh) break;  // uniform
                 const __bf16* t16 = reinterpret_cast<const __bf16*>(stg) + mt * 1024 + (lane & 31);
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    acc[mt][r] += bv;
+                for (int r = 0; r < 16; r += 2) {
+                    // bf16-only output (the bf16 arithmetic's data gradient): the partials
+                    // describe the stored, rounded values
+                    float v0 = acc[mt][r] + bv, v1 = acc[mt][r + 1] + bv;
+                    if (only16) pk_bf16(v0, v1, v0, v1);
+                    acc[mt][r] = v0;
+                    acc[mt][r + 1] = v1;
                     part(mt, r, (float)t16[((r & 3) + 8 * (r >> 2) + 4 * h) * 32]);
+                    part(mt, r + 1, (float)t16[(((r + 1) & 3) + 8 * ((r + 1) >> 2) + 4 * h) * 32]);
                 }
                 asm volatile("" ::: "memory");  // (as store_rows: one m-tile's reads at a time)
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // y reads done: reuse the area
+            if (only16) store16_rows(std::true_type{});
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt) {
+                if (only16) break;  // (stored above)
                 const int py = wm * MT + mt;
                 if (py >= vh) break;  // uniform
 #pragma unroll
@@ -988,7 +1002,9 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
     u32x4* const Bring = smem + 2 * A_VECS;
     u32x4* const dummy = smem + 2 * A_VECS + NSLOT * R_STR;  // writes of idle lanes
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // the wave index in an SGPR: role, wave-grid position and staging addresses are
+    // wave-uniform (scalar registers, scalar branches), not per-lane VGPR values
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const bool loader = wave >= NCW;
     const int NB = a.Cout / BNI;
     const int nitems = a.ntiles * NB;

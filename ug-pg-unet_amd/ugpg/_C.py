@@ -70,8 +70,8 @@ SIGNATURES = {
     "ugpg_bn_relu_bwd": (_i, [_p, _p, _p, _i64, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _p,
                               _sz, _p]),
     "ugpg_bn_relu_bwd_partials_workspace": (_sz, [_i]),
-    "ugpg_bn_relu_bwd_partials": (_i, [_p, _i, _p, _p, _p, _i64, _i, _p, _p, _p, _p, _p, _p, _p,
-                                       _p, _p, _i, _p, _sz, _p]),
+    "ugpg_bn_relu_bwd_partials": (_i, [_p, _i, _p, _p, _p, _p, _i64, _i, _p, _p, _p, _p, _p, _p,
+                                       _p, _p, _p, _i, _p, _sz, _p]),
     "ugpg_bn_relu_bwd_partials_routed": (_i, [C.POINTER(BwdRoute), _p, _i, _p, _p, _p, _i64, _i, _p,
                                               _p, _p, _p, _p, _p, _p, _p, _p, _i, _p, _sz, _p]),
     "ugpg_bn_relu_apply": (_i, [Src, _i64, _p, _p]),

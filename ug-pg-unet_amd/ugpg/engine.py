@@ -136,7 +136,8 @@ def _bn_relu_wgrad(conv, bn, y, st, in_srcs, da, grads, part=None, route=None):
     # the conv bias gradient (sum of dy) comes out of the BN-backward reduction
     db = grads.get(conv.bias) if conv.bias is not None else None
     dy = da
-    if y.dtype == torch.bfloat16 and all(s.C % 64 == 0 for s in in_srcs):
+    if y.dtype == torch.bfloat16 and all(s.C % 64 == 0 for s in in_srcs) and \
+            da.dtype != torch.bfloat16:
         dy = ops.empty(*da.shape, like=da, dtype=torch.bfloat16)
     base = da if route is None or route[1] else None
     ops.bn_relu_bwd(base, y, mean, invstd, scale, shift, dy, grads.get(bn.weight),
@@ -161,7 +162,6 @@ def double_conv_backward(mod, ctx: BlockCtx, da2, targets, acc_flags, grads, pad
     dy2 = _bn_relu_wgrad(c2, b2, ctx.y2, ctx.st2, [a1], da2, grads, part=ctx.part2,
                          route=ctx.route2)
     cmid = c2.weight.shape[1]
-    da1 = ops.empty(B, H, W, cmid, like=da2)
     npix = B * H * W
     wpk2 = ops.pack_conv3x3(c2.weight.detach(), cmid, 1)
     # the data gradient also reduces BN1's backward sums over da1 while each tile is in
@@ -171,6 +171,12 @@ def double_conv_backward(mod, ctx: BlockCtx, da2, targets, acc_flags, grads, pad
     if ctx.st1[0] is not None:
         part = ops.empty(3 * cmid * ops.conv_ntiles(B, H, W, cout, cmid, wpk2), like=da2)
         bnb = (ctx.y1, *ctx.st1, part)
+    # the bf16 arithmetic stores da1 in bf16 (autocast's conv backward returns a bf16
+    # grad_input; oracle.ref_cpu.BF16_DGRAD_STORE), with partials of the rounded values,
+    # where y1 is bf16 and BN1's apply writes a bf16 dy (sources of 64-channel multiples)
+    da16 = (bnb is not None and ctx.y1.dtype == torch.bfloat16 and _store16(W)
+            and wpk2.ugpg_fmt == ops.WFMT_BF16 and all(s.C % 64 == 0 for s in ctx.srcs))
+    da1 = ops.empty(B, H, W, cmid, like=da2, dtype=torch.bfloat16 if da16 else torch.float32)
     ops.conv3x3_fwd([Act(dy2)], wpk2, None, cmid, [da1], flops=2.0 * npix * cmid * 9 * cout,
                     bnb=bnb)
     # stage 1: BN1/ReLU backward, wgrad(conv1), dgrad(conv1) -> source targets

@@ -375,7 +375,7 @@ def bn_relu_bwd(da, y, mean, invstd, scale, shift, dy, dgamma, dbeta, dconv_bias
     if part is not None:
         ws = workspace(lib.ugpg_bn_relu_bwd_partials_workspace(c), y.device)
         check(lib.ugpg_bn_relu_bwd_partials(
-            ptr(part), part.numel() // (3 * c), ptr(da), *_yargs(y), npix, c, ptr(mean), ptr(invstd),
+            ptr(part), part.numel() // (3 * c), *_yargs(da), *_yargs(y), npix, c, ptr(mean), ptr(invstd),
             ptr(scale), ptr(shift), *_yargs(dy), ptr(dgamma), ptr(dbeta), ptr(dconv_bias),
             int(accumulate), ptr(ws), ws.numel(), stream()), "bn_relu_bwd_partials")
         return
