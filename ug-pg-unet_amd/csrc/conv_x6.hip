@@ -1545,9 +1545,61 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
             // step's first taps are read in phase 2: halo(k+1) and row 3k+3 are visible there)
 #pragma unroll
             for (int t = 0; t < 9; ++t) {
+              if constexpr (NT == 2) {
+                // 4 x 2 tiles, one tap ahead, m-tile-major MFMA order: the next tap's B
+                // fragments first, then after each m-tile's two MFMAs its next A fragment
+                // (into the register its current one frees), so 36 fragment registers are
+                // live instead of 48.  The item's last tap prefetches nothing across the
+                // epilogue; the step's last tap reads after its MFMAs (before the barrier).
+                const int tn = (t + 1) % 3;
+                const u32x4* An = smem + ((t + 1 < 9 ? k : k + 1) & 1) * A_VECS;
+                const u32x4* Bn = Bring + ((3 * (t + 1 < 9 ? k : k + 1) + ((t + 1) % 9) / 3) % NSLOT) * R_STR;
+                const int kyn = ((t + 1) % 9) / 3, kxn = (t + 1) % 3;
+                auto ldA = [&](int mt) {
+#pragma unroll
+                    for (int q = 0; q < NP; ++q)
+                        fa1[tn][mt][q] = An[q * 2 * NHP + aoff + (mt + kyn) * HS + kxn];
+                };
+                auto ldB = [&](int nt) {
+#pragma unroll
+                    for (int q = 0; q < NP; ++q)
+                        fb1[tn][nt][q] = Bn[q * 2 * 3 * BN + boff(nt) + kxn * BN];
+                };
+                if (t < 8) {
+                    ldB(0);
+                    ldB(1);
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt) {
+                        acc[0][mt] = mfma_xn<NP>(fa1[t % 3][mt], fb1[t % 3][0], acc[0][mt]);
+                        acc[1][mt] = mfma_xn<NP>(fa1[t % 3][mt], fb1[t % 3][1], acc[1][mt]);
+                        ldA(mt);
+                    }
+                    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // B reads
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMAs
+                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // A read
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                } else {
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt) {
+                        acc[0][mt] = mfma_xn<NP>(fa1[t % 3][mt], fb1[t % 3][0], acc[0][mt]);
+                        acc[1][mt] = mfma_xn<NP>(fa1[t % 3][mt], fb1[t % 3][1], acc[1][mt]);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (cc != nchunk - 1) {
+                        ldB(0);
+                        ldB(1);
+#pragma unroll
+                        for (int mt = 0; mt < MT; ++mt) ldA(mt);
+                    }
+                }
+                if (t % 3 == 2) CS_WAIT(cs_bar, read_barrier());
+                continue;
+              }
                 if (t + PD < 9) ldfrag1(k, t + PD, fa1[(t + PD) % 3], fb1[(t + PD) % 3]);
-                else if (NT == 1 || cc != nchunk - 1)  // (NT = 2: not across an epilogue)
-                    ldfrag1(k + 1, t + PD - 9, fa1[(t + PD) % 3], fb1[(t + PD) % 3]);
+                else ldfrag1(k + 1, t + PD - 9, fa1[(t + PD) % 3], fb1[(t + PD) % 3]);
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
