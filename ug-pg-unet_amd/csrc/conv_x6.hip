@@ -2293,6 +2293,9 @@ X6Form x6_fwd_form(int B, int H, int W, int N, int np) {
         return {8, 16, 1, 1, false};
     }
     if (W < 32) return {8, 16, 1, 1, false};
+#ifdef X6R_NO_WIDE  // A/B build: the 256 x 64 items everywhere
+    return {8, 32, 1, 2, true};
+#endif
     constexpr int64_t kPlanCUs = 256;
     const int64_t tiles8 = (int64_t)B * cdiv(H, 8) * cdiv(W, 32);
     const int64_t tiles16 = (int64_t)B * cdiv(H, 16) * cdiv(W, 32);
