@@ -167,3 +167,15 @@ k_ok:
 """)
     hits = scan(asm)
     assert [h[0] for h in hits] == ["k_bad"], hits
+
+
+def test_polygon_scan_has_no_fused_multiply_add(all_asm):
+    """Pillow's scan converter rounds x = (y - y0) * dx and + x0 separately (x86 SSE float);
+    a fused v_fma_f32 moved one boundary pixel in 4 of the 361 golden canvases (GPU run
+    s2 of round 4).  csrc/augment.hip turns contraction off in poly_x_at."""
+    import re
+    text = all_asm["augment.hip"].read_text()
+    start = text.index("_ZN4ugpg16poly_scan_kernel")
+    start = text.index("_ZN4ugpg16poly_scan_kernel", text.index(":", start))  # the label
+    body = text[start:text.index(".Lfunc_end", start)]
+    assert not re.findall(r"\bv_(?:fma|fmac|mad|mac)_f32", body)

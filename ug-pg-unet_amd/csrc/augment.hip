@@ -275,8 +275,9 @@ __global__ void augment_color_kernel(const uint8_t* __restrict__ img, const uint
 // ---------------------------------------------------------------------------
 // Filled polygons, Pillow 12's scan converter (libImaging/Draw.c ImagingDrawPolygon +
 // polygon_generic + hline8; restated and pinned in oracle/polygon_ref.py, whose header
-// lists the rules).  Float steps in float with explicit _rn intrinsics (no contraction),
+// lists the rules).  Float steps in float without contraction,
 // the negative-argument rounding macros in double, as Pillow's x86 build evaluates them.
+// (tests/test_asm_audit.py checks the scan kernel holds no fused multiply-add)
 struct PolyEdge {
     int x0, y0, xmin, ymin, xmax, ymax;
     float dx;
@@ -304,7 +305,11 @@ __device__ __forceinline__ void poly_hline(uint8_t* mask, int H, int W, int x0, 
     for (int x = x0; x <= x1; ++x) row[x] = ink;
 }
 __device__ __forceinline__ float poly_x_at(const PolyEdge& e, int y) {
-    return __fadd_rn(__fmul_rn((float)(y - e.y0), e.dx), (float)e.x0);
+    // separately rounded product and sum: contraction off here (HIP's __fmul_rn and
+    // __fadd_rn are plain operators, which -O3 fuses into one v_fma_f32)
+#pragma clang fp contract(off)
+    const float m = (float)(y - e.y0) * e.dx;
+    return m + (float)e.x0;
 }
 __device__ __forceinline__ int poly_round_up(float f) {
     if (f >= 0.f) return (int)floorf(__fadd_rn(f, 0.5f));

@@ -783,7 +783,7 @@ using namespace ugpg;
 extern "C" int ugpg_conv3x3_fwd_ntiles(int B, int H, int W, int Cin, int Cout, int wfmt) {
     if (wfmt == UGPG_WFMT_X6 || wfmt == UGPG_WFMT_BF16) {
         const int np = wfmt == UGPG_WFMT_X6 ? 3 : 1;
-        return fwd_x6_stat_slots(x6_fwd_form(B, H, W, Cout, np), B, H, W);
+        return fwd_x6_stat_slots(x6_fwd_form(B, H, W, Cin, Cout, np), B, H, W);
     }
     if (img_fwd_eligible(W, Cin, 0, Cout)) return img_fwd_slots(B, H, W, 2);
     const int cfg = pick_fwd_cfg(B, H, W, Cout, Cout);
@@ -918,7 +918,7 @@ extern "C" int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream) {
             set_error("conv3x3_fwd: the bf16 persistent form takes at most 2048 input channels");
             return UGPG_ERR_INVALID;
         }
-        const X6Form f = x6_fwd_form(p->B, p->H, p->W, p->Cout, np);
+        const X6Form f = x6_fwd_form(p->B, p->H, p->W, Cin, p->Cout, np);
         a.tiles_x = (int)cdiv(p->W, f.tw);
         a.tiles_y = (int)cdiv(p->H, f.th);
         a.ntiles = p->B * a.tiles_x * a.tiles_y;

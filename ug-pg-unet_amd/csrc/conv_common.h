@@ -210,7 +210,7 @@ struct X6Form {
     int th, tw, nslab, wm;
     bool persistent;
 };
-X6Form x6_fwd_form(int B, int H, int W, int N, int np);
+X6Form x6_fwd_form(int B, int H, int W, int K, int N, int np);  // K: input channels
 int fwd_x6_stat_slots(const X6Form& f, int B, int H, int W);  // BatchNorm partial slots written
 void launch_wgrad_x6(const WgradArgs& a, int np, hipStream_t st);
 // split plan of the persistent split-bf16 wgrad (deterministic: planned for `cus` CUs)

@@ -526,7 +526,11 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
                            (__builtin_bit_cast(unsigned, y) & 0xffff0000u);
                 };
                 const u32x4 w = {pk(lo.x, lo.y), pk(lo.z, lo.w), pk(hi.x, hi.y), pk(hi.z, hi.w)};
+#ifdef X6Q_NOSTORE  // diagnostic build: no output stores (results are wrong)
+                if (w[0] == 0x12345678u)
+#else
                 if (fullw || p < vw)
+#endif
                     *reinterpret_cast<u32x4*>(a.out0_16 + rowb + (size_t)p * ostride + 8 * k) = w;
             }
             asm volatile("" ::: "memory");  // the next m-tile's staging writes after these reads
@@ -632,6 +636,9 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
         return;
     }
     if (a.stats == nullptr) return;
+#ifdef X6Q_NOSTATS
+    return;
+#endif
     constexpr int WROWS = MT * 32 / TW;  // image rows of one wave's pixels
     const int rows = min(max(vh - wm * WROWS, 0), WROWS);
     const float cnt = (float)(rows * vw);
@@ -2286,7 +2293,7 @@ static bool use_x6r(int W, int np) { return W >= 32 || (np == 3 && W >= 16); }
 //    instead of 1.25 -- unless that leaves fewer items than a 256-CU device has: then the
 //    256 x 64 items.  The plan assumes 256 CUs whatever the device, so the BatchNorm
 //    partial order (the slot layout) is a function of the shape only.
-X6Form x6_fwd_form(int B, int H, int W, int N, int np) {
+X6Form x6_fwd_form(int B, int H, int W, int K, int N, int np) {
     if (np == 3) {
         if (W >= 32) return {8, 32, 1, 2, true};
         if (W >= 16) return {8, 16, 1, 2, true};
@@ -2300,7 +2307,11 @@ X6Form x6_fwd_form(int B, int H, int W, int N, int np) {
     const int64_t tiles8 = (int64_t)B * cdiv(H, 8) * cdiv(W, 32);
     const int64_t tiles16 = (int64_t)B * cdiv(H, 16) * cdiv(W, 32);
     if (N % 128 == 0 && tiles8 * (N / 128) >= kPlanCUs) return {8, 32, 2, 2, true};
-    if (N % 128 != 0 && tiles16 * (N / 64) >= kPlanCUs) return {16, 32, 1, 4, true};
+    // 512 x 64 items only where an item runs >= 16 K steps: with fewer the doubled
+    // per-item epilogue costs more than the halved fragment reads save (in-process A/B
+    // against 256 x 64 everywhere, profiles/r5b_ab_wide_forms_bf16.txt: K = 256 -3 %,
+    // K = 64/128 +4-10 %)
+    if (N % 128 != 0 && K >= 256 && tiles16 * (N / 64) >= kPlanCUs) return {16, 32, 1, 4, true};
     return {8, 32, 1, 2, true};
 }
 int fwd_x6_stat_slots(const X6Form& f, int B, int H, int W) {
@@ -2595,7 +2606,7 @@ bool launch_img_fwd(const ConvFwdArgs& a, bool wf32, hipStream_t st) {
 }
 
 int launch_fwd_x6(const ConvFwdArgs& a, int np, hipStream_t st) {
-    const X6Form f = x6_fwd_form(a.B, a.H, a.W, a.Cout, np);
+    const X6Form f = x6_fwd_form(a.B, a.H, a.W, a.Cin, a.Cout, np);
     const int64_t items = (int64_t)a.ntiles * (a.Cout / (64 * f.nslab));
     if (np == 3 && use_x6r(a.W, np) && a.Cin == 16 && launch_img_fwd(a, false, st))
         return FWD_WROTE_OUT16;
