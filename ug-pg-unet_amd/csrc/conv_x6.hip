@@ -427,15 +427,17 @@ __device__ __forceinline__ void x6_dma_bnb_y(const ConvFwdArgs& a, int b, int ty
 }
 // Y32: the BatchNorm-backward partials may read an fp32 y (the 4 x 2-tile single-piece
 // forms need a bf16 y -- the host routes the rest to the 4 x 1 form -- which keeps this
-// path, and its registers, out of them)
-template <int TH, int TW, int MT, int WM = 2, bool Y32 = true>
+// path, and its registers, out of them).  FW: the tile is known to lie wholly inside the
+// image width (the caller's uniform branch), so no store or statistics term carries a
+// per-pixel column guard (each was an exec-mask branch per value)
+template <int TH, int TW, int MT, int WM = 2, bool Y32 = true, bool FW = false>
 __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&acc)[MT], int tile,
                                                  int b, int ty0, int tx0, int c0, int wm,
                                                  float* stg) {
     static_assert(TW == 32, "one image row per 32-pixel MFMA tile");
     const int lane = threadIdx.x & 63, h = lane >> 5;
     const int vh = min(TH, a.H - ty0), vw = min(TW, a.W - tx0);
-    const bool fullw = vw == TW;
+    const bool fullw = FW || vw == TW;
     float* out;
     int ostride, ocol0, oacc;
     if (c0 < a.split) {  // (a 32-wide n-tile never straddles the split: split % 64 == 0)
@@ -671,7 +673,8 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
 // image row wm*4 + mt/2, columns (mt&1)*16 + 0..15) and n-tile nt (16 channels); lane
 // (g, l) holds channels 4g..4g+3 of pixel l -> one 16-byte store per tile.  BatchNorm
 // partials as x6_epilogue_wave (slot 2*tile + wm), reduced over the pixel lanes of
-// each DPP row.
+// each DPP row.  (A full-width specialisation as in x6_epilogue_wave measured neutral
+// here -- its column guard is one branch per m-tile -- and spilled; profiles/r5f_ab_fullwidth_epilogue_x6.txt.)
 template <int TH, int TW, int NWM = 2>
 __device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a,
                                                   f32x4 (&acc)[TH * TW / 16 / NWM][2],
@@ -1659,14 +1662,29 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
         if (++cc == nchunk) {
             // (explicit calls: a loop around the inlined epilogue cost the allocator ~240
             // spilled registers)
-            CS_WAIT(cs_epi, (x6_epilogue_wave<TH, TW, MT, WM, NT == 1>(
-                                a, acc[0], cp.tile, cp.b, cp.ty0, cp.tx0, cp.nb * BNI + wn * NT * 32,
-                                wm, ostg + wave * NT * X6_STG_WAVE)));
-            if constexpr (NT > 1)
+#ifdef X6R_NO_FW  // A/B build: the per-pixel column guards everywhere
+            if (false) {
+#else
+            if (cp.tx0 + TW <= a.W) {  // (uniform) the common case: a full-width tile
+#endif
+                CS_WAIT(cs_epi, (x6_epilogue_wave<TH, TW, MT, WM, NT == 1, true>(
+                                    a, acc[0], cp.tile, cp.b, cp.ty0, cp.tx0, cp.nb * BNI + wn * NT * 32,
+                                    wm, ostg + wave * NT * X6_STG_WAVE)));
+                if constexpr (NT > 1)
+                    CS_WAIT(cs_epi, (x6_epilogue_wave<TH, TW, MT, WM, NT == 1, true>(
+                                        a, acc[1], cp.tile, cp.b, cp.ty0, cp.tx0,
+                                        cp.nb * BNI + (wn * NT + 1) * 32, wm,
+                                        ostg + (wave * NT + 1) * X6_STG_WAVE)));
+            } else {
                 CS_WAIT(cs_epi, (x6_epilogue_wave<TH, TW, MT, WM, NT == 1>(
-                                    a, acc[1], cp.tile, cp.b, cp.ty0, cp.tx0,
-                                    cp.nb * BNI + (wn * NT + 1) * 32, wm,
-                                    ostg + (wave * NT + 1) * X6_STG_WAVE)));
+                                    a, acc[0], cp.tile, cp.b, cp.ty0, cp.tx0, cp.nb * BNI + wn * NT * 32,
+                                    wm, ostg + wave * NT * X6_STG_WAVE)));
+                if constexpr (NT > 1)
+                    CS_WAIT(cs_epi, (x6_epilogue_wave<TH, TW, MT, WM, NT == 1>(
+                                        a, acc[1], cp.tile, cp.b, cp.ty0, cp.tx0,
+                                        cp.nb * BNI + (wn * NT + 1) * 32, wm,
+                                        ostg + (wave * NT + 1) * X6_STG_WAVE)));
+            }
             static_assert(NT <= 2, "two n-tiles at most");
             if constexpr (NP == 1 && NT > 1) {
                 // the next step's first taps, not held in registers across the epilogue
