@@ -166,7 +166,30 @@ typedef struct {
     int math;              /* UGPG_WFMT_X6 (split-bf16) or UGPG_WFMT_BF16 (bf16) MFMA
                               where the shape allows (db == NULL, 64-channel
                               sources); else fp32 MFMA */
+    /* Optional: dy formed while loading from the BatchNorm(+ReLU) backward of the layer
+     * that follows (dy == dy_bf16 == NULL): dy = ugpg_bn_relu_bwd's apply of (da, y) with
+     * the coefficients ugpg_bn_relu_bwd_partials left in its workspace when called with
+     * dy == dy_bf16 == NULL, bit-identical to it; dy_out (nullable) receives that dy, the
+     * operand of the data gradient, written once per pixel -- the BatchNorm-backward apply
+     * pass folded into the weight gradient.  Cout % 64 == 0, 64-channel sources,
+     * db == NULL, and either UGPG_WFMT_X6 math with fp32 sources, da, y and dy_out, or
+     * UGPG_WFMT_BF16 math with bf16-stored sources and y, da fp32 or bf16, and dy_out_bf16
+     * (dy rounded to bf16, as the apply writes it).  NULL: off. */
+    const struct ugpg_bn_lazy* dy_bn;
 } ugpg_wgrad_t;
+typedef struct ugpg_bn_lazy {
+    const float* da;       /* NHWC [B][H][W][Cout]: dL/d(relu(bn(y))) (fp32) ... */
+    const void* da_bf16;   /* ... or stored in bf16 (da == NULL) */
+    const float* y;        /* NHWC [B][H][W][Cout]: the BatchNorm input (fp32) ... */
+    const void* y_bf16;    /* ... or stored in bf16 (y == NULL) */
+    const float* mean;
+    const float* invstd;
+    const float* scale;
+    const float* shift;
+    const float* coef;     /* [2][Cout]: the first 2*Cout floats of that workspace */
+    float* dy_out;         /* NHWC [B][H][W][Cout] (fp32 math) or NULL ... */
+    void* dy_out_bf16;     /* ... (bf16 math) or NULL; neither may alias da or y */
+} ugpg_bn_lazy_t;
 size_t ugpg_conv3x3_wgrad_workspace(const ugpg_wgrad_t* p);
 int ugpg_conv3x3_wgrad(const ugpg_wgrad_t* p, void* ws, size_t ws_bytes, void* stream);
 
@@ -192,7 +215,9 @@ int ugpg_bn_eval_params(const float* gamma, const float* beta, const float* runn
  * sum in fp32; both are ~0 because train-mode BN cancels a preceding bias). */
 size_t ugpg_bn_relu_bwd_workspace(int64_t npix, int C);
 /* The same from partials a data gradient wrote (ugpg_conv_t.bnb_part, nslots slots):
- * finalize + apply only; workspace ugpg_bn_relu_bwd_partials_workspace(C). */
+ * finalize + apply only; workspace ugpg_bn_relu_bwd_partials_workspace(C).  With
+ * dy == dy_bf16 == NULL the finalize only (dgamma, dbeta, dconv_bias, and the apply's
+ * coefficients in the first 2*C floats of ws, for ugpg_wgrad_t.dy_bn). */
 size_t ugpg_bn_relu_bwd_partials_workspace(int C);
 /* BatchNorm-backward partials folded into the kernel that last writes da (the pooling,
  * upsampling and head backward entries *_bnb): same partial layout, nslots from

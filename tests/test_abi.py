@@ -51,6 +51,27 @@ def test_invalid_arguments_fail_loudly_without_gpu():
     assert b"pack_conv3x3" in _C.lib.ugpg_last_error()
 
 
+def test_lazy_bn_dy_wgrad_validation_without_gpu():
+    """ugpg_wgrad_t.dy_bn: refused (workspace query 0, an error naming it) outside the
+    split-bf16 arithmetic or with a dy beside it; checked before any launch."""
+    import ctypes as C
+    from ugpg import _C
+    p = C.cast(C.c_void_p(0x1000), C.c_void_p)
+    lz = _C.BnLazy(p, None, p, None, p, p, p, p, p, None, None)
+    d = _C.WgradDesc()
+    d.B, d.H, d.W = 1, 8, 16
+    d.src[0] = _C.Src(p, None, None, 64, None)
+    d.Cout, d.dw, d.Cin_real, d.math = 64, p, 64, 2  # UGPG_WFMT_BF16
+    d.dy_bn = C.pointer(lz)
+    assert _C.lib.ugpg_conv3x3_wgrad_workspace(C.byref(d)) == 0
+    assert b"dy_bn" in _C.lib.ugpg_last_error()
+    d.math = 1  # UGPG_WFMT_X6, but a dy as well
+    d.dy = p
+    assert _C.lib.ugpg_conv3x3_wgrad_workspace(C.byref(d)) == 0
+    d.dy = None
+    assert _C.lib.ugpg_conv3x3_wgrad_workspace(C.byref(d)) > 0
+
+
 def test_ops_refuse_cpu_tensors():
     import pytest
     import torch

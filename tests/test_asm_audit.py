@@ -26,11 +26,14 @@ KERNELS = [
     X6R.format("i1ELb0ELi32ELi8ELb1ELi2"),
     X6R.format("i1ELb0ELi32ELi16ELb0ELi1"),   # single-piece 512 x 64 items
     X6R.format("i1ELb0ELi32ELi16ELb1ELi1"),
-    "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi3ELi0EEEvNS_9WgradArgsE",
-    "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi1ELi0EEEvNS_9WgradArgsE",
-    "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi1ELi1EEEvNS_9WgradArgsE",
-    "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi1ELi2EEEvNS_9WgradArgsE",
-    "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi1ELi3EEEvNS_9WgradArgsE",
+    "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi3ELi0ELb0EEEvNS_9WgradArgsE",
+    "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi3ELi0ELb1EEEvNS_9WgradArgsE",  # lazy BN dy
+    "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi1ELi0ELb0EEEvNS_9WgradArgsE",
+    "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi1ELi1ELb0EEEvNS_9WgradArgsE",
+    "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi1ELi2ELb0EEEvNS_9WgradArgsE",
+    "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi1ELi3ELb0EEEvNS_9WgradArgsE",
+    "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi1ELi1ELb1EEEvNS_9WgradArgsE",  # lazy, bf16
+    "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi1ELi3ELb1EEEvNS_9WgradArgsE",
 ]
 
 

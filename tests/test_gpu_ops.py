@@ -945,3 +945,62 @@ def test_resize_bilinear_backward(dev, hi, wi, ho, wo):
     got = ops.resize_nchw_bwd(g.to(dev), hi, wi).cpu().double()
     ref = x.grad.double()
     assert (got - ref).abs().max().item() <= 1e-5 * max(1.0, ref.abs().max().item())
+
+
+LAZY_CASES = [  # B, H, W, C0, C1, Cout: one / two sources, partial tiles, 2 ci and 2 co blocks
+    (2, 20, 36, 64, 0, 64),
+    (2, 33, 40, 64, 64, 128),
+    (1, 64, 64, 128, 0, 64),
+    (3, 16, 16, 64, 0, 192),
+]
+
+
+@pytest.mark.parametrize("case", LAZY_CASES)
+@pytest.mark.parametrize("form", ["x6", "bf16", "bf16-da16"])
+def test_wgrad_lazy_bn_dy_is_the_apply(dev, case, form):
+    """The BatchNorm-backward apply folded into the weight gradient (ugpg_wgrad_t.dy_bn,
+    ops.BnLazyDy): dy formed while loading (da, y) and written once per pixel equals the
+    apply pass's dy bit for bit (in bf16 under the bf16 arithmetic, as the apply rounds it),
+    and so do dW and the finalize's dgamma, dbeta and conv bias gradient."""
+    from ugpg import ops
+    old = ops.conv_math()
+    b16 = form != "x6"
+    ops.set_conv_math("bf16" if b16 else "x6")
+    q = (lambda t: t.to(torch.bfloat16)) if b16 else (lambda t: t)
+    try:
+        B, H, W, C0, C1, Cout = case
+        cin = C0 + C1
+        x0 = q(nhwc(rnd((B, C0, H, W), 201, "x0")).to(dev))
+        x1 = q(nhwc(rnd((B, C1, H, W), 202, "x1")).to(dev)) if C1 else None
+        sc0, sh0 = (rnd((C0,), 203, "s", 0.5) + 1).to(dev), rnd((C0,), 204, "h", 0.2).to(dev)
+        srcs = [ops.Act(x0, sc0, sh0)] + ([ops.Act(x1)] if C1 else [])
+        y = q(nhwc(rnd((B, Cout, H, W), 205, "y") + 0.2).to(dev))
+        da = nhwc(rnd((B, Cout, H, W), 206, "da")).to(dev)
+        if form == "bf16-da16":
+            da = da.to(torch.bfloat16)
+        mean, invstd = rnd((Cout,), 207, "m", 0.1).to(dev), (rnd((Cout,), 208, "i").abs() + 0.5).to(dev)
+        scale, shift = (rnd((Cout,), 209, "s", 0.5) + 1).to(dev), rnd((Cout,), 210, "h", 0.3).to(dev)
+        # one partial slot: (sum g, sum g*xhat, sum xhat) per channel
+        yd, dd = y.double(), da.double()
+        g = torch.where(yd * scale.double() + shift.double() > 0, dd, torch.zeros_like(dd))
+        xh = (yd - mean.double()) * invstd.double()
+        part = torch.stack([g.sum((0, 1, 2)), (g * xh).sum((0, 1, 2)), xh.sum((0, 1, 2))]).float()
+        part = part.reshape(3 * Cout, 1).contiguous()
+        outs = []
+        for lazy in (False, True):
+            dg, dbt, dcb = (torch.zeros(Cout, device=dev) for _ in range(3))
+            dw = torch.empty(Cout, cin, 3, 3, device=dev)
+            dy = torch.empty(da.shape, device=dev, dtype=torch.bfloat16 if b16 else torch.float32)
+            if lazy:
+                coef = ops.bn_relu_bwd(da, y, mean, invstd, scale, shift, None, dg, dbt, dcb,
+                                       part=part)
+                ops.conv3x3_wgrad(srcs, ops.BnLazyDy(da, y, mean, invstd, scale, shift, coef, dy),
+                                  dw, None, cin)
+            else:
+                ops.bn_relu_bwd(da, y, mean, invstd, scale, shift, dy, dg, dbt, dcb, part=part)
+                ops.conv3x3_wgrad(srcs, dy, dw, None, cin)
+            outs.append((dy, dw, dg, dbt, dcb))
+        for name, a_, b_ in zip(("dy", "dW", "dgamma", "dbeta", "dbias"), *outs):
+            assert torch.equal(a_, b_), name
+    finally:
+        ops.set_conv_math(old)

@@ -325,11 +325,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const TD* da, const T
     auto one = [&](f32x4 d, f32x4 v) {
         f32x4 o;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const float g = fmaf(v[k], sc[k], sh[k]) > 0.f ? d[k] : 0.f;
-            const float xh = (v[k] - mu[k]) * is[k];
-            o[k] = (g - k0[k] - xh * k1[k]) * sc[k];
-        }
+        for (int k = 0; k < 4; ++k) o[k] = bn_bwd_dy(d[k], v[k], sc[k], sh[k], mu[k], is[k], k0[k], k1[k]);
         return o;
     };
     static_assert(std::is_same<TD, float>::value || ROUTE == ROUTE_NONE, "bf16 da: no route");
@@ -582,13 +578,16 @@ static int bn_relu_bwd_partials(int kind, const Route& rt, const float* part, in
                                 float* dgamma, float* dbeta, float* dbias, int acc, void* ws,
                                 size_t ws_bytes, void* stream, const void* da_bf16 = nullptr) {
     const YRef y = yref(y_f32, y_bf16);
-    if (!part || nslots <= 0 || (!da && !da_bf16 && kind == ROUTE_NONE) || (da && da_bf16) ||
-        (!y.f && !y.h) || !dy == !dy_bf16 || !mean || !invstd || !scale || !shift || C % 4 ||
-        C <= 0 || C > 1024 || npix <= 0) {
+    // dy == dy_bf16 == NULL: the finalize only (the apply's coefficients stay in ws for a
+    // weight gradient that forms dy while loading, ugpg_wgrad_t.dy_bn)
+    const bool fin_only = !dy && !dy_bf16 && kind == ROUTE_NONE;
+    if (!part || nslots <= 0 || (!da && !da_bf16 && kind == ROUTE_NONE && !fin_only) ||
+        (da && da_bf16) || (!y.f && !y.h) || (dy && dy_bf16) || (!dy && !dy_bf16 && !fin_only) ||
+        !mean || !invstd || !scale || !shift || C % 4 || C <= 0 || C > 1024 || npix <= 0) {
         set_error("bn_relu_bwd_partials: bad arguments (C=%d nslots=%d)", C, nslots);
         return UGPG_ERR_INVALID;
     }
-    if (da_bf16 && (kind != ROUTE_NONE || y.f || dy)) {
+    if (da_bf16 && !fin_only && (kind != ROUTE_NONE || y.f || dy)) {
         set_error("bn_relu_bwd_partials: a bf16 da needs a bf16 y and a bf16 dy");
         return UGPG_ERR_INVALID;
     }
@@ -602,6 +601,7 @@ static int bn_relu_bwd_partials(int kind, const Route& rt, const float* part, in
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(bwd_fin_threads(nslots)), 0, st,
                        part, nslots, C, npix, scale, dgamma, dbeta, dbias, acc, coef);
     if (int e = check_launch("bn_bwd_finalize")) return e;
+    if (fin_only) return UGPG_OK;
     const unsigned q = (unsigned)(C / std::gcd(1024, C));
     const unsigned ga = (apply_grid(npix * C / 4) + q - 1) / q * q;
     launch_bn_apply(ga, st, da, y, npix, C, mean, invstd, scale, shift, coef, dy,

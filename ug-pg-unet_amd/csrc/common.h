@@ -105,6 +105,19 @@ __device__ __forceinline__ f32x4 act_reg4(f32x4 v, const Act4& a, bool on) {
     return v;
 }
 
+// BatchNorm(+ReLU) backward of one element: g = da*[scale*y + shift > 0], xhat =
+// (y - mean)*invstd, dy = (g - mean(g) - xhat*mean(g*xhat))*scale (k0 = mean(g), k1 =
+// mean(g*xhat) from bn_bwd_finalize).  One definition with contraction off for every
+// kernel that forms dy -- the BatchNorm-backward apply and the weight gradient that forms
+// it while loading (WgradArgs.bn_*) -- so both give bit-identical dy.
+__device__ __forceinline__ float bn_bwd_dy(float d, float v, float sc, float sh, float mu,
+                                           float is, float k0, float k1) {
+#pragma clang fp contract(off)
+    const float g = fmaf(v, sc, sh) > 0.f ? d : 0.f;
+    const float xh = (v - mu) * is;
+    return fmaf(-xh, k1, g - k0) * sc;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -1775,17 +1775,25 @@ constexpr int wrec() { return NP == 3 ? WX_REC : 192; }
 // XB bit 1: the activation operand is stored in bf16 (a.src*_16), bit 2: dy is (a.dy16) --
 // the bf16 arithmetic's storage, NP = 1: 8-byte loads of 4 channels instead of 16-byte
 // ones, same load count per step
-template <int TH, int TW, int NP, int XB = 0>
+// BN: dy is formed while loading from the following BatchNorm(+ReLU) backward (a.bn_*:
+// da, y and the apply's coefficients; bn_bwd_dy, bit-identical to the apply pass) and, by
+// the items of the first input-channel block, written to a.bn_dy_out for the data gradient
+// -- the BatchNorm-backward apply pass folded into the loader waves, which wait at
+// barriers 15-29 % of the loop in this form (profiles/r4n_x6w_stamps_x6.txt)
+template <int TH, int TW, int NP, int XB = 0, bool BN = false>
 __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) {
     constexpr bool XB16 = (XB & 1) != 0, DB16 = (XB & 2) != 0;
     static_assert(XB == 0 || NP == 1, "bf16 storage: single-piece arithmetic");
+    // BN: split-bf16 on fp32 tensors (XB 0), or single-piece on bf16-stored sources and y
+    // (XB bit 1), with da fp32 or (XB bit 2 -- in place of a bf16 dy) bf16
+    static_assert(!BN || (NP == 3 && XB == 0) || (NP == 1 && XB16), "lazy dy forms");
     constexpr int REC = wrec<NP>();
     static_assert(TW == 16, "one 16-pixel row per MFMA k-step");
     constexpr int P = TH * TW, HWD = TW + 2, NHALO = (TH + 2) * HWD;
     constexpr int DY_Q = P * 16, X_Q = NHALO * 16;  // float4 quads per tile
     constexpr int DY_PER = (DY_Q + 255) / 256, X_PER = (X_Q + 255) / 256;
     constexpr int RECS = P + NHALO;                  // records per buffer
-    constexpr int LOADS = DY_PER + X_PER + 2;        // loader VMEM instructions per step
+    constexpr int LOADS = DY_PER + X_PER + 2 + (BN ? DY_PER + 6 : 0);  // loader VMEM per step
     __shared__ __attribute__((aligned(16))) char smem[(2 * RECS + 1) * REC];
     char* const dummy = smem + 2 * RECS * REC;    // record for idle lanes' writes
 
@@ -1839,6 +1847,13 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
         Act4 xa[NSET];
         float xlo[NSET];
         unsigned dvalid[NSET], xvalid[NSET];
+        // BN: y beside da, the lane's 4 channels' (scale, shift, mean, invstd, k0, k1), and
+        // where (and whether: first ci block) the formed dy goes
+        typename std::conditional<NP == 1, u32x2v, f32x4>::type rby[BN ? NSET : 1][BN ? DY_PER : 1];
+        f32x4 bco[BN ? NSET : 1][6];
+        bool bwr[NSET];
+        size_t bbase[NSET];
+        int bof[BN ? NSET : 1][BN ? DY_PER : 1];
         // the loader's cursor also carries the item's co / ci blocks and the tile's
         // image position, updated without divisions inside an item
         struct LCur {
@@ -1941,10 +1956,30 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
             }
             const size_t dyo0 = ((size_t)(b * a.H + ty0) * a.W + tx0) * a.Cout + co0 + q4;
             const size_t xb = ((size_t)(b * a.H + ty0) * a.W + tx0) * Cs + cbase + q4;
+            if constexpr (BN) {
+                const int cq = co0 + q4;
+                bco[st][0] = gld16(a.bn_scale + cq);
+                bco[st][1] = gld16(a.bn_shift + cq);
+                bco[st][2] = gld16(a.bn_mean + cq);
+                bco[st][3] = gld16(a.bn_invstd + cq);
+                bco[st][4] = gld16(a.bn_coef + cq);
+                bco[st][5] = gld16(a.bn_coef + a.Cout + cq);
+                bwr[st] = (NP == 1 ? a.bn_dy16_out != nullptr : a.bn_dy_out != nullptr) && c.cb == 0;
+                bbase[st] = dyo0;
+            }
 #pragma unroll
             for (int v = 0; v < DY_PER; ++v) {
-                if constexpr (DB16) rdy[st][v] = gld8(a.dy16 + dyo0 + dof[v]);
-                else rdy[st][v] = gld16(a.dy + dyo0 + dof[v]);
+                if constexpr (BN) {
+                    if constexpr (DB16) rdy[st][v] = gld8(a.bn_da16 + dyo0 + dof[v]);
+                    else rdy[st][v] = gld16(a.bn_da + dyo0 + dof[v]);
+                    if constexpr (NP == 1) rby[st][v] = gld8(a.bn_y16 + dyo0 + dof[v]);
+                    else rby[st][v] = gld16(a.bn_y + dyo0 + dof[v]);
+                    bof[st][v] = dof[v];
+                } else if constexpr (DB16) {
+                    rdy[st][v] = gld8(a.dy16 + dyo0 + dof[v]);
+                } else {
+                    rdy[st][v] = gld16(a.dy + dyo0 + dof[v]);
+                }
             }
 #pragma unroll
             for (int v = 0; v < X_PER; ++v) {
@@ -1974,7 +2009,27 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
                               __uint_as_float(rdy[st][v].y << 16), __uint_as_float(rdy[st][v].y & 0xffff0000u)};
                 else
                     d = rdy[st][v];
-                put(dys + (idx >> 4) * REC, idx & 15, ((dvalid[st] >> v) & 1u) ? d : z);
+                const bool ok = (dvalid[st] >> v) & 1u;
+                if constexpr (BN) {
+                    f32x4 yv;
+                    if constexpr (NP == 1)  // 4 bf16 widened (exact)
+                        yv = f32x4{__uint_as_float(rby[st][v].x << 16), __uint_as_float(rby[st][v].x & 0xffff0000u),
+                                   __uint_as_float(rby[st][v].y << 16), __uint_as_float(rby[st][v].y & 0xffff0000u)};
+                    else
+                        yv = rby[st][v];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        d[i] = bn_bwd_dy(d[i], yv[i], bco[st][0][i], bco[st][1][i], bco[st][2][i],
+                                         bco[st][3][i], bco[st][4][i], bco[st][5][i]);
+                    if (bwr[st] && ok) {  // (uniform bwr)
+                        if constexpr (NP == 1)  // rounded to bf16 as the apply writes it
+                            *reinterpret_cast<u32x2*>(a.bn_dy16_out + bbase[st] + bof[st][v]) =
+                                __builtin_bit_cast(u32x2, __builtin_convertvector(d, bf16x4));
+                        else
+                            *reinterpret_cast<f32x4*>(a.bn_dy_out + bbase[st] + bof[st][v]) = d;
+                    }
+                }
+                put(dys + (idx >> 4) * REC, idx & 15, ok ? d : z);
             }
 #pragma unroll
             for (int v = 0; v < X_PER; ++v) {
@@ -2160,10 +2215,19 @@ void launch_wgrad_x6(const WgradArgs& a, int np, hipStream_t st) {
     const int64_t items = (int64_t)(a.Cout / 64) * (a.Cin / 64) * a.nsplit;
     int64_t g = std::min<int64_t>(cu_count(st), (items + 7) / 8 * 8);
     g = std::max<int64_t>(8, g / 8 * 8);
-    if (np == 3)
+    if (np == 3 && a.bn_da)
+        hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW, 3, 0, true>),
+                           dim3((unsigned)g), dim3(512), 0, st, a);
+    else if (np == 3)
         hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW, 3>), dim3((unsigned)g),
                            dim3(512), 0, st, a);
     // bf16 storage of the activations (the host checked both sources alike) and of dy
+    else if (a.bn_y16 && a.bn_da16)  // lazy dy from bf16 da and y (bf16-stored sources)
+        hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW, 1, 3, true>),
+                           dim3((unsigned)g), dim3(512), 0, st, a);
+    else if (a.bn_y16)  // ... from fp32 da
+        hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW, 1, 1, true>),
+                           dim3((unsigned)g), dim3(512), 0, st, a);
     else if (a.src0 == nullptr && a.dy == nullptr)
         hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW, 1, 3>),
                            dim3((unsigned)g), dim3(512), 0, st, a);

@@ -47,10 +47,18 @@ class PackItem(C.Structure):
     _fields_ = [("w", _p), ("wpk", _p), ("Cout", _i), ("Cin", _i), ("Cin_pad", _i), ("mode", _i)]
 
 
+class BnLazy(C.Structure):
+    """ugpg_bn_lazy_t."""
+    _fields_ = [("da", _p), ("da_bf16", _p), ("y", _p), ("y_bf16", _p), ("mean", _p),
+                ("invstd", _p), ("scale", _p), ("shift", _p), ("coef", _p), ("dy_out", _p),
+                ("dy_out_bf16", _p)]
+
+
 class WgradDesc(C.Structure):
     """ugpg_wgrad_t."""
     _fields_ = [("B", _i), ("H", _i), ("W", _i), ("src", Src * 2), ("dy", _p), ("dy_bf16", _p),
-                ("Cout", _i), ("dw", _p), ("Cin_real", _i), ("db", _p), ("accumulate", _i), ("math", _i)]
+                ("Cout", _i), ("dw", _p), ("Cin_real", _i), ("db", _p), ("accumulate", _i), ("math", _i),
+                ("dy_bn", C.POINTER(BnLazy))]
 
 
 # name -> (restype, argtypes); must match include/ugpg.h exactly

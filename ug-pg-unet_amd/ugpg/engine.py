@@ -123,6 +123,9 @@ def double_conv_forward(mod, srcs, ctx: BlockCtx, save: bool):
     return cur[0]
 
 
+_LAZY_BN_DY = 1  # (in-process A/B of the folded apply: tools/ab_step.py engine._LAZY_BN_DY=0)
+
+
 def _bn_relu_wgrad(conv, bn, y, st, in_srcs, da, grads, part=None, route=None):
     """dy = dL/d(conv output) from da = dL/d(relu(bn(y))) -- in place, or, where the bf16
     arithmetic stores the activations in bf16 (y is bf16), into a bf16 tensor: exactly the
@@ -135,6 +138,26 @@ def _bn_relu_wgrad(conv, bn, y, st, in_srcs, da, grads, part=None, route=None):
         raise RuntimeError("backward through an eval-mode BatchNorm is not supported")
     # the conv bias gradient (sum of dy) comes out of the BN-backward reduction
     db = grads.get(conv.bias) if conv.bias is not None else None
+    dw = grads.get(conv.weight)
+    co = conv.weight.shape[0]
+    # the apply pass folded into the weight gradient (the plain apply, from the partials of
+    # da's producer): the finalize here, then x6w forms dy while loading (da, y) and writes
+    # it once for the data gradient, bit-identical to the apply -- split-bf16 on fp32
+    # tensors, or the bf16 arithmetic on bf16-stored sources and y (dy then in bf16)
+    fold = _LAZY_BN_DY and route is None and part is not None and dw is not None and \
+        co % 64 == 0 and all(s.C % 64 == 0 for s in in_srcs)
+    x6 = fold and ops.conv_math() == "x6" and y.dtype == torch.float32 and \
+        da.dtype == torch.float32 and all(s.y.dtype == torch.float32 for s in in_srcs)
+    b16 = fold and ops.conv_math() == "bf16" and y.dtype == torch.bfloat16 and \
+        all(s.y.dtype == torch.bfloat16 for s in in_srcs)
+    if x6 or b16:
+        coef = ops.bn_relu_bwd(da, y, mean, invstd, scale, shift, None, grads.get(bn.weight),
+                               grads.get(bn.bias), db, part=part)
+        dy = ops.empty(*da.shape, like=da, dtype=torch.bfloat16 if b16 else torch.float32)
+        ci = conv.weight.shape[1]
+        ops.conv3x3_wgrad(in_srcs, ops.BnLazyDy(da, y, mean, invstd, scale, shift, coef, dy), dw,
+                          None, ci, flops=2.0 * dy.numel() / co * co * 9 * ci)
+        return dy
     dy = da
     if y.dtype == torch.bfloat16 and all(s.C % 64 == 0 for s in in_srcs) and \
             da.dtype != torch.bfloat16:
@@ -142,9 +165,8 @@ def _bn_relu_wgrad(conv, bn, y, st, in_srcs, da, grads, part=None, route=None):
     base = da if route is None or route[1] else None
     ops.bn_relu_bwd(base, y, mean, invstd, scale, shift, dy, grads.get(bn.weight),
                     grads.get(bn.bias), db, part=part, route=None if route is None else route[0])
-    dw = grads.get(conv.weight)
     if dw is not None:
-        co, ci = conv.weight.shape[0], conv.weight.shape[1]
+        ci = conv.weight.shape[1]
         ops.conv3x3_wgrad(in_srcs, dy, dw, None, ci, flops=2.0 * dy.numel() / co * co * 9 * ci)
     return dy
 

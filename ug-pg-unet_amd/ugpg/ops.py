@@ -11,7 +11,7 @@ import os
 
 import torch
 
-from ._C import Bnb, BwdRoute, ConvDesc, PackItem, Src, WgradDesc, check, lib
+from ._C import Bnb, BnLazy, BwdRoute, ConvDesc, PackItem, Src, WgradDesc, check, lib
 
 F32 = torch.float32
 
@@ -294,13 +294,37 @@ def conv3x3_fwd(srcs, wpk, bias, cout, outs, split=None, accumulate=(0, 0), stat
            lambda: check(lib.ugpg_conv3x3_fwd(C.byref(d), stream()), "conv3x3_fwd"))
 
 
+class BnLazyDy:
+    """dy of a weight gradient formed while loading from the following BatchNorm(+ReLU)
+    backward (ugpg_wgrad_t.dy_bn): da, the BN input y and its statistics, `coef` the
+    workspace bn_relu_bwd(..., dy=None, part=...) returned (its finalize only), and dy_out
+    receiving dy for the data gradient (bit-identical to the apply pass)."""
+    __slots__ = ("da", "y", "mean", "invstd", "scale", "shift", "coef", "dy_out")
+
+    def __init__(self, da, y, mean, invstd, scale, shift, coef, dy_out):
+        self.da, self.y, self.mean, self.invstd = da, y, mean, invstd
+        self.scale, self.shift, self.coef, self.dy_out = scale, shift, coef, dy_out
+
+    @property
+    def shape(self):
+        return tuple(self.da.shape)
+
+
 def conv3x3_wgrad(srcs, dy, dw, db, cin_real, accumulate=0, flops=None):
+    """dy: fp32, bf16 (the bf16 arithmetic's storage) or a BnLazyDy."""
     B, H, W, _ = srcs[0].shape
     d = WgradDesc()
     d.B, d.H, d.W = B, H, W
     d.src[0] = srcs[0].src()
     d.src[1] = srcs[1].src() if len(srcs) > 1 else NULL_SRC
-    d.dy, d.dy_bf16 = _yargs(dy)  # dy fp32, or bf16 (the bf16 arithmetic's storage)
+    lazy = None
+    if isinstance(dy, BnLazyDy):
+        lazy = BnLazy(*_yargs(dy.da), *_yargs(dy.y), ptr(dy.mean), ptr(dy.invstd),
+                      ptr(dy.scale), ptr(dy.shift), ptr(dy.coef), *_yargs(dy.dy_out))
+        d.dy_bn = C.pointer(lazy)
+        dy = dy.da
+    else:
+        d.dy, d.dy_bf16 = _yargs(dy)  # dy fp32, or bf16 (the bf16 arithmetic's storage)
     d.Cout = dy.shape[-1]
     d.dw, d.Cin_real, d.db, d.accumulate = ptr(dw), cin_real, ptr(db), int(accumulate)
     d.math = _MATH_FMT[_conv_math]
@@ -373,12 +397,15 @@ def bn_relu_bwd(da, y, mean, invstd, scale, shift, dy, dgamma, dbeta, dconv_bias
             "bn_relu_bwd_partials_routed")
         return
     if part is not None:
+        # dy None: the finalize only; the returned workspace holds the apply's coefficients
+        # (its first 2*C floats) for conv3x3_wgrad(dy=BnLazyDy(..., coef=ws, ...))
         ws = workspace(lib.ugpg_bn_relu_bwd_partials_workspace(c), y.device)
         check(lib.ugpg_bn_relu_bwd_partials(
             ptr(part), part.numel() // (3 * c), *_yargs(da), *_yargs(y), npix, c, ptr(mean), ptr(invstd),
-            ptr(scale), ptr(shift), *_yargs(dy), ptr(dgamma), ptr(dbeta), ptr(dconv_bias),
-            int(accumulate), ptr(ws), ws.numel(), stream()), "bn_relu_bwd_partials")
-        return
+            ptr(scale), ptr(shift), *(_yargs(dy) if dy is not None else (None, None)), ptr(dgamma),
+            ptr(dbeta), ptr(dconv_bias), int(accumulate), ptr(ws), ws.numel(), stream()),
+            "bn_relu_bwd_partials")
+        return ws
     ws = workspace(lib.ugpg_bn_relu_bwd_workspace(npix, c), y.device)
     check(lib.ugpg_bn_relu_bwd(ptr(da), *_yargs(y), npix, c, ptr(mean), ptr(invstd), ptr(scale),
                                ptr(shift), *_yargs(dy), ptr(dgamma), ptr(dbeta), ptr(dconv_bias),
