@@ -171,24 +171,19 @@ typedef struct {
      * the coefficients ugpg_bn_relu_bwd_partials left in its workspace when called with
      * dy == dy_bf16 == NULL, bit-identical to it; dy_out (nullable) receives that dy, the
      * operand of the data gradient, written once per pixel -- the BatchNorm-backward apply
-     * pass folded into the weight gradient.  Cout % 64 == 0, 64-channel sources,
-     * db == NULL, and either UGPG_WFMT_X6 math with fp32 sources, da, y and dy_out, or
-     * UGPG_WFMT_BF16 math with bf16-stored sources and y, da fp32 or bf16, and dy_out_bf16
-     * (dy rounded to bf16, as the apply writes it).  NULL: off. */
+     * pass folded into the weight gradient.  UGPG_WFMT_X6 math, fp32 sources, da, y and
+     * dy_out, Cout % 64 == 0, 64-channel sources, db == NULL.  NULL: off. */
     const struct ugpg_bn_lazy* dy_bn;
 } ugpg_wgrad_t;
 typedef struct ugpg_bn_lazy {
-    const float* da;       /* NHWC [B][H][W][Cout]: dL/d(relu(bn(y))) (fp32) ... */
-    const void* da_bf16;   /* ... or stored in bf16 (da == NULL) */
-    const float* y;        /* NHWC [B][H][W][Cout]: the BatchNorm input (fp32) ... */
-    const void* y_bf16;    /* ... or stored in bf16 (y == NULL) */
+    const float* da;       /* NHWC [B][H][W][Cout]: dL/d(relu(bn(y))) */
+    const float* y;        /* NHWC [B][H][W][Cout]: the BatchNorm input */
     const float* mean;
     const float* invstd;
     const float* scale;
     const float* shift;
     const float* coef;     /* [2][Cout]: the first 2*Cout floats of that workspace */
-    float* dy_out;         /* NHWC [B][H][W][Cout] (fp32 math) or NULL ... */
-    void* dy_out_bf16;     /* ... (bf16 math) or NULL; neither may alias da or y */
+    float* dy_out;         /* NHWC [B][H][W][Cout] or NULL; must not alias da or y */
 } ugpg_bn_lazy_t;
 size_t ugpg_conv3x3_wgrad_workspace(const ugpg_wgrad_t* p);
 int ugpg_conv3x3_wgrad(const ugpg_wgrad_t* p, void* ws, size_t ws_bytes, void* stream);

@@ -32,8 +32,6 @@ KERNELS = [
     "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi1ELi1ELb0EEEvNS_9WgradArgsE",
     "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi1ELi2ELb0EEEvNS_9WgradArgsE",
     "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi1ELi3ELb0EEEvNS_9WgradArgsE",
-    "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi1ELi1ELb1EEEvNS_9WgradArgsE",  # lazy, bf16
-    "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi1ELi3ELb1EEEvNS_9WgradArgsE",
 ]
 
 

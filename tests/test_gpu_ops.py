@@ -956,28 +956,23 @@ LAZY_CASES = [  # B, H, W, C0, C1, Cout: one / two sources, partial tiles, 2 ci 
 
 
 @pytest.mark.parametrize("case", LAZY_CASES)
-@pytest.mark.parametrize("form", ["x6", "bf16", "bf16-da16"])
-def test_wgrad_lazy_bn_dy_is_the_apply(dev, case, form):
-    """The BatchNorm-backward apply folded into the weight gradient (ugpg_wgrad_t.dy_bn,
-    ops.BnLazyDy): dy formed while loading (da, y) and written once per pixel equals the
-    apply pass's dy bit for bit (in bf16 under the bf16 arithmetic, as the apply rounds it),
-    and so do dW and the finalize's dgamma, dbeta and conv bias gradient."""
+def test_wgrad_lazy_bn_dy_is_the_apply(dev, case):
+    """The BatchNorm-backward apply folded into the split-bf16 weight gradient
+    (ugpg_wgrad_t.dy_bn, ops.BnLazyDy): dy formed while loading (da, y) and written once per
+    pixel equals the apply pass's dy bit for bit, and so do dW and the finalize's dgamma,
+    dbeta and conv bias gradient."""
     from ugpg import ops
     old = ops.conv_math()
-    b16 = form != "x6"
-    ops.set_conv_math("bf16" if b16 else "x6")
-    q = (lambda t: t.to(torch.bfloat16)) if b16 else (lambda t: t)
+    ops.set_conv_math("x6")
     try:
         B, H, W, C0, C1, Cout = case
         cin = C0 + C1
-        x0 = q(nhwc(rnd((B, C0, H, W), 201, "x0")).to(dev))
-        x1 = q(nhwc(rnd((B, C1, H, W), 202, "x1")).to(dev)) if C1 else None
+        x0 = nhwc(rnd((B, C0, H, W), 201, "x0")).to(dev)
+        x1 = nhwc(rnd((B, C1, H, W), 202, "x1")).to(dev) if C1 else None
         sc0, sh0 = (rnd((C0,), 203, "s", 0.5) + 1).to(dev), rnd((C0,), 204, "h", 0.2).to(dev)
         srcs = [ops.Act(x0, sc0, sh0)] + ([ops.Act(x1)] if C1 else [])
-        y = q(nhwc(rnd((B, Cout, H, W), 205, "y") + 0.2).to(dev))
+        y = nhwc(rnd((B, Cout, H, W), 205, "y") + 0.2).to(dev)
         da = nhwc(rnd((B, Cout, H, W), 206, "da")).to(dev)
-        if form == "bf16-da16":
-            da = da.to(torch.bfloat16)
         mean, invstd = rnd((Cout,), 207, "m", 0.1).to(dev), (rnd((Cout,), 208, "i").abs() + 0.5).to(dev)
         scale, shift = (rnd((Cout,), 209, "s", 0.5) + 1).to(dev), rnd((Cout,), 210, "h", 0.3).to(dev)
         # one partial slot: (sum g, sum g*xhat, sum xhat) per channel
@@ -990,7 +985,7 @@ def test_wgrad_lazy_bn_dy_is_the_apply(dev, case, form):
         for lazy in (False, True):
             dg, dbt, dcb = (torch.zeros(Cout, device=dev) for _ in range(3))
             dw = torch.empty(Cout, cin, 3, 3, device=dev)
-            dy = torch.empty(da.shape, device=dev, dtype=torch.bfloat16 if b16 else torch.float32)
+            dy = torch.empty_like(da)
             if lazy:
                 coef = ops.bn_relu_bwd(da, y, mean, invstd, scale, shift, None, dg, dbt, dcb,
                                        part=part)

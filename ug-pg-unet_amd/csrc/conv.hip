@@ -1034,22 +1034,14 @@ static int wgrad_check(const ugpg_wgrad_t* p) {
         return UGPG_ERR_INVALID;
     }
     const int C0 = p->src[0].C, C1 = wgrad_c1(p);
-    if (const ugpg_bn_lazy_t* l = p->dy_bn) {  // dy formed while loading (x6w)
-        // split-bf16: fp32 everything; bf16 arithmetic: bf16-stored sources and y, a bf16 dy
-        const bool x6 = p->math == UGPG_WFMT_X6 && !wgrad_b16(p) && l->da && !l->da_bf16 &&
-                        l->y && !l->y_bf16 && !l->dy_out_bf16;
-        const bool b16 = p->math == UGPG_WFMT_BF16 && wgrad_b16(p) && !l->da != !l->da_bf16 &&
-                         !l->y && l->y_bf16 && !l->dy_out;
-        const void* out = l->dy_out ? static_cast<const void*>(l->dy_out) : l->dy_out_bf16;
-        const void* ins[4] = {l->da, l->da_bf16, l->y, l->y_bf16};
-        bool alias = false;
-        for (const void* q : ins) alias = alias || (out && q == out);
-        if (p->dy || p->dy_bf16 || (!x6 && !b16) || p->db || C0 % 64 || C1 % 64 ||
-            p->Cout % 64 || p->Cin_real > C0 + C1 || !l->mean || !l->invstd || !l->scale ||
-            !l->shift || !l->coef || alias) {
-            set_error("conv3x3_wgrad: dy_bn needs no dy, no bias gradient, 64-channel sources "
-                      "and either the split-bf16 arithmetic on fp32 tensors or the bf16 one on "
-                      "bf16-stored sources and y (C0=%d C1=%d Cout=%d)", C0, C1, p->Cout);
+    if (const ugpg_bn_lazy_t* l = p->dy_bn) {  // dy formed while loading (x6w, split-bf16)
+        if (p->dy || p->dy_bf16 || p->math != UGPG_WFMT_X6 || p->db || C0 % 64 || C1 % 64 ||
+            wgrad_b16(p) || p->Cout % 64 || p->Cin_real > C0 + C1 || !l->da || !l->y ||
+            !l->mean || !l->invstd || !l->scale || !l->shift || !l->coef ||
+            (l->dy_out && (l->dy_out == l->da || l->dy_out == l->y))) {
+            set_error("conv3x3_wgrad: dy_bn needs the split-bf16 arithmetic, fp32 sources of "
+                      "64-channel multiples, no dy, no bias gradient and every BatchNorm input "
+                      "(C0=%d C1=%d Cout=%d)", C0, C1, p->Cout);
             return UGPG_ERR_INVALID;
         }
         return UGPG_OK;
@@ -1144,16 +1136,13 @@ extern "C" int ugpg_conv3x3_wgrad(const ugpg_wgrad_t* p, void* ws, size_t ws_byt
     a.dy16 = p->dy ? nullptr : static_cast<const __bf16*>(p->dy_bf16);
     const ugpg_bn_lazy_t* bl = p->dy_bn;
     a.bn_da = bl ? bl->da : nullptr;
-    a.bn_da16 = bl ? static_cast<const __bf16*>(bl->da_bf16) : nullptr;
     a.bn_y = bl ? bl->y : nullptr;
-    a.bn_y16 = bl ? static_cast<const __bf16*>(bl->y_bf16) : nullptr;
     a.bn_mean = bl ? bl->mean : nullptr;
     a.bn_invstd = bl ? bl->invstd : nullptr;
     a.bn_scale = bl ? bl->scale : nullptr;
     a.bn_shift = bl ? bl->shift : nullptr;
     a.bn_coef = bl ? bl->coef : nullptr;
     a.bn_dy_out = bl ? bl->dy_out : nullptr;
-    a.bn_dy16_out = bl ? static_cast<__bf16*>(bl->dy_out_bf16) : nullptr;
     a.Cout = p->Cout;
     a.Cin = Cin;
     a.part = static_cast<float*>(ws);

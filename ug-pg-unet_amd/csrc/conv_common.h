@@ -172,16 +172,13 @@ struct WgradArgs {
     // dy formed while loading from the following BatchNorm(+ReLU) backward (ugpg_bn_lazy_t;
     // bn_da == nullptr: off; the split-bf16 x6w form): bn_dy_out receives it (nullable)
     const float* bn_da;
-    const __bf16* bn_da16;   // (bn_da == nullptr: da stored in bf16)
     const float* bn_y;
-    const __bf16* bn_y16;    // (bn_y == nullptr: y stored in bf16; the single-piece form)
     const float* bn_mean;
     const float* bn_invstd;
     const float* bn_scale;
     const float* bn_shift;
     const float* bn_coef;
     float* bn_dy_out;
-    __bf16* bn_dy16_out;     // (the single-piece form: dy rounded to bf16, as the apply)
     int Cout, Cin;
     float* part;
     float* dbpart;

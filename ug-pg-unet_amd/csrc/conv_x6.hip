@@ -1784,9 +1784,9 @@ template <int TH, int TW, int NP, int XB = 0, bool BN = false>
 __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) {
     constexpr bool XB16 = (XB & 1) != 0, DB16 = (XB & 2) != 0;
     static_assert(XB == 0 || NP == 1, "bf16 storage: single-piece arithmetic");
-    // BN: split-bf16 on fp32 tensors (XB 0), or single-piece on bf16-stored sources and y
-    // (XB bit 1), with da fp32 or (XB bit 2 -- in place of a bf16 dy) bf16
-    static_assert(!BN || (NP == 3 && XB == 0) || (NP == 1 && XB16), "lazy dy forms");
+    // (BN in the single-piece form: its loaders already wait on loads 11-22 % of the loop,
+    // and folding the apply there made the bf16 step 1.6 % slower, profiles/r5j_*)
+    static_assert(!BN || (NP == 3 && XB == 0), "lazy BatchNorm-backward dy: split-bf16 form");
     constexpr int REC = wrec<NP>();
     static_assert(TW == 16, "one 16-pixel row per MFMA k-step");
     constexpr int P = TH * TW, HWD = TW + 2, NHALO = (TH + 2) * HWD;
@@ -1849,8 +1849,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
         unsigned dvalid[NSET], xvalid[NSET];
         // BN: y beside da, the lane's 4 channels' (scale, shift, mean, invstd, k0, k1), and
         // where (and whether: first ci block) the formed dy goes
-        typename std::conditional<NP == 1, u32x2v, f32x4>::type rby[BN ? NSET : 1][BN ? DY_PER : 1];
-        f32x4 bco[BN ? NSET : 1][6];
+        f32x4 rby[BN ? NSET : 1][BN ? DY_PER : 1], bco[BN ? NSET : 1][6];
         bool bwr[NSET];
         size_t bbase[NSET];
         int bof[BN ? NSET : 1][BN ? DY_PER : 1];
@@ -1964,16 +1963,14 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
                 bco[st][3] = gld16(a.bn_invstd + cq);
                 bco[st][4] = gld16(a.bn_coef + cq);
                 bco[st][5] = gld16(a.bn_coef + a.Cout + cq);
-                bwr[st] = (NP == 1 ? a.bn_dy16_out != nullptr : a.bn_dy_out != nullptr) && c.cb == 0;
+                bwr[st] = a.bn_dy_out != nullptr && c.cb == 0;
                 bbase[st] = dyo0;
             }
 #pragma unroll
             for (int v = 0; v < DY_PER; ++v) {
                 if constexpr (BN) {
-                    if constexpr (DB16) rdy[st][v] = gld8(a.bn_da16 + dyo0 + dof[v]);
-                    else rdy[st][v] = gld16(a.bn_da + dyo0 + dof[v]);
-                    if constexpr (NP == 1) rby[st][v] = gld8(a.bn_y16 + dyo0 + dof[v]);
-                    else rby[st][v] = gld16(a.bn_y + dyo0 + dof[v]);
+                    rdy[st][v] = gld16(a.bn_da + dyo0 + dof[v]);
+                    rby[st][v] = gld16(a.bn_y + dyo0 + dof[v]);
                     bof[st][v] = dof[v];
                 } else if constexpr (DB16) {
                     rdy[st][v] = gld8(a.dy16 + dyo0 + dof[v]);
@@ -2011,23 +2008,13 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
                     d = rdy[st][v];
                 const bool ok = (dvalid[st] >> v) & 1u;
                 if constexpr (BN) {
-                    f32x4 yv;
-                    if constexpr (NP == 1)  // 4 bf16 widened (exact)
-                        yv = f32x4{__uint_as_float(rby[st][v].x << 16), __uint_as_float(rby[st][v].x & 0xffff0000u),
-                                   __uint_as_float(rby[st][v].y << 16), __uint_as_float(rby[st][v].y & 0xffff0000u)};
-                    else
-                        yv = rby[st][v];
+                    const f32x4 yv = rby[st][v];
 #pragma unroll
                     for (int i = 0; i < 4; ++i)
                         d[i] = bn_bwd_dy(d[i], yv[i], bco[st][0][i], bco[st][1][i], bco[st][2][i],
                                          bco[st][3][i], bco[st][4][i], bco[st][5][i]);
-                    if (bwr[st] && ok) {  // (uniform bwr)
-                        if constexpr (NP == 1)  // rounded to bf16 as the apply writes it
-                            *reinterpret_cast<u32x2*>(a.bn_dy16_out + bbase[st] + bof[st][v]) =
-                                __builtin_bit_cast(u32x2, __builtin_convertvector(d, bf16x4));
-                        else
-                            *reinterpret_cast<f32x4*>(a.bn_dy_out + bbase[st] + bof[st][v]) = d;
-                    }
+                    if (bwr[st] && ok)  // (uniform bwr: one store per vector, then the next)
+                        *reinterpret_cast<f32x4*>(a.bn_dy_out + bbase[st] + bof[st][v]) = d;
                 }
                 put(dys + (idx >> 4) * REC, idx & 15, ok ? d : z);
             }
@@ -2222,12 +2209,6 @@ void launch_wgrad_x6(const WgradArgs& a, int np, hipStream_t st) {
         hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW, 3>), dim3((unsigned)g),
                            dim3(512), 0, st, a);
     // bf16 storage of the activations (the host checked both sources alike) and of dy
-    else if (a.bn_y16 && a.bn_da16)  // lazy dy from bf16 da and y (bf16-stored sources)
-        hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW, 1, 3, true>),
-                           dim3((unsigned)g), dim3(512), 0, st, a);
-    else if (a.bn_y16)  // ... from fp32 da
-        hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW, 1, 1, true>),
-                           dim3((unsigned)g), dim3(512), 0, st, a);
     else if (a.src0 == nullptr && a.dy == nullptr)
         hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW, 1, 3>),
                            dim3((unsigned)g), dim3(512), 0, st, a);

@@ -123,9 +123,6 @@ def double_conv_forward(mod, srcs, ctx: BlockCtx, save: bool):
     return cur[0]
 
 
-_LAZY_BN_DY = 1  # (in-process A/B of the folded apply: tools/ab_step.py engine._LAZY_BN_DY=0)
-
-
 def _bn_relu_wgrad(conv, bn, y, st, in_srcs, da, grads, part=None, route=None):
     """dy = dL/d(conv output) from da = dL/d(relu(bn(y))) -- in place, or, where the bf16
     arithmetic stores the activations in bf16 (y is bf16), into a bf16 tensor: exactly the
@@ -141,19 +138,16 @@ def _bn_relu_wgrad(conv, bn, y, st, in_srcs, da, grads, part=None, route=None):
     dw = grads.get(conv.weight)
     co = conv.weight.shape[0]
     # the apply pass folded into the weight gradient (the plain apply, from the partials of
-    # da's producer): the finalize here, then x6w forms dy while loading (da, y) and writes
-    # it once for the data gradient, bit-identical to the apply -- split-bf16 on fp32
-    # tensors, or the bf16 arithmetic on bf16-stored sources and y (dy then in bf16)
-    fold = _LAZY_BN_DY and route is None and part is not None and dw is not None and \
-        co % 64 == 0 and all(s.C % 64 == 0 for s in in_srcs)
-    x6 = fold and ops.conv_math() == "x6" and y.dtype == torch.float32 and \
-        da.dtype == torch.float32 and all(s.y.dtype == torch.float32 for s in in_srcs)
-    b16 = fold and ops.conv_math() == "bf16" and y.dtype == torch.bfloat16 and \
-        all(s.y.dtype == torch.bfloat16 for s in in_srcs)
-    if x6 or b16:
+    # da's producer; the split-bf16 arithmetic): the finalize here, then x6w forms dy while
+    # loading (da, y) and writes it once for the data gradient, bit-identical to the apply
+    # (in-process A/B: fp32 step -1.0 %, profiles/r5j_ab_step_folded_bn_apply.txt; the
+    # single-piece form, whose loaders already wait on loads, was 1.6 % slower with it)
+    if (route is None and part is not None and dw is not None and co % 64 == 0
+            and ops.conv_math() == "x6" and y.dtype == torch.float32 and da.dtype == torch.float32
+            and all(s.C % 64 == 0 and s.y.dtype == torch.float32 for s in in_srcs)):
         coef = ops.bn_relu_bwd(da, y, mean, invstd, scale, shift, None, grads.get(bn.weight),
                                grads.get(bn.bias), db, part=part)
-        dy = ops.empty(*da.shape, like=da, dtype=torch.bfloat16 if b16 else torch.float32)
+        dy = ops.empty(*da.shape, like=da)
         ci = conv.weight.shape[1]
         ops.conv3x3_wgrad(in_srcs, ops.BnLazyDy(da, y, mean, invstd, scale, shift, coef, dy), dw,
                           None, ci, flops=2.0 * dy.numel() / co * co * 9 * ci)

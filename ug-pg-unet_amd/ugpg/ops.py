@@ -319,8 +319,8 @@ def conv3x3_wgrad(srcs, dy, dw, db, cin_real, accumulate=0, flops=None):
     d.src[1] = srcs[1].src() if len(srcs) > 1 else NULL_SRC
     lazy = None
     if isinstance(dy, BnLazyDy):
-        lazy = BnLazy(*_yargs(dy.da), *_yargs(dy.y), ptr(dy.mean), ptr(dy.invstd),
-                      ptr(dy.scale), ptr(dy.shift), ptr(dy.coef), *_yargs(dy.dy_out))
+        lazy = BnLazy(ptr(dy.da), ptr(dy.y), ptr(dy.mean), ptr(dy.invstd), ptr(dy.scale),
+                      ptr(dy.shift), ptr(dy.coef), ptr(dy.dy_out))
         d.dy_bn = C.pointer(lazy)
         dy = dy.da
     else:
