@@ -1793,7 +1793,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
     constexpr int DY_Q = P * 16, X_Q = NHALO * 16;  // float4 quads per tile
     constexpr int DY_PER = (DY_Q + 255) / 256, X_PER = (X_Q + 255) / 256;
     constexpr int RECS = P + NHALO;                  // records per buffer
-    constexpr int LOADS = DY_PER + X_PER + 2 + (BN ? DY_PER + 6 : 0);  // loader VMEM per step
+    constexpr int LOADS = DY_PER + X_PER + 2 + (BN ? DY_PER : 0);  // loader untracked VMEM per step
     __shared__ __attribute__((aligned(16))) char smem[(2 * RECS + 1) * REC];
     char* const dummy = smem + 2 * RECS * REC;    // record for idle lanes' writes
 
@@ -1850,6 +1850,8 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
         // BN: y beside da, the lane's 4 channels' (scale, shift, mean, invstd, k0, k1), and
         // where (and whether: first ci block) the formed dy goes
         f32x4 rby[BN ? NSET : 1][BN ? DY_PER : 1], bco[BN ? NSET : 1][6];
+        int bco_nb = -1;  // output-channel block whose coefficients bco holds
+        static_assert(!BN || NSET == 1, "one coefficient set");
         bool bwr[NSET];
         size_t bbase[NSET];
         int bof[BN ? NSET : 1][BN ? DY_PER : 1];
@@ -1956,13 +1958,22 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
             const size_t dyo0 = ((size_t)(b * a.H + ty0) * a.W + tx0) * a.Cout + co0 + q4;
             const size_t xb = ((size_t)(b * a.H + ty0) * a.W + tx0) * Cs + cbase + q4;
             if constexpr (BN) {
-                const int cq = co0 + q4;
-                bco[st][0] = gld16(a.bn_scale + cq);
-                bco[st][1] = gld16(a.bn_shift + cq);
-                bco[st][2] = gld16(a.bn_mean + cq);
-                bco[st][3] = gld16(a.bn_invstd + cq);
-                bco[st][4] = gld16(a.bn_coef + cq);
-                bco[st][5] = gld16(a.bn_coef + a.Cout + cq);
+                // the lane's coefficients change with the output-channel block only: plain
+                // (tracked) loads at an item's first step (NSET = 1: consumed by this set)
+#ifndef X6W_BN_COEF_PER_STEP
+                if (c.nb != bco_nb)
+#endif
+                {
+                    bco_nb = c.nb;
+                    const int cq = co0 + q4;
+                    auto ld = [](const float* q) { return *reinterpret_cast<const f32x4*>(q); };
+                    bco[st][0] = ld(a.bn_scale + cq);
+                    bco[st][1] = ld(a.bn_shift + cq);
+                    bco[st][2] = ld(a.bn_mean + cq);
+                    bco[st][3] = ld(a.bn_invstd + cq);
+                    bco[st][4] = ld(a.bn_coef + cq);
+                    bco[st][5] = ld(a.bn_coef + a.Cout + cq);
+                }
                 bwr[st] = a.bn_dy_out != nullptr && c.cb == 0;
                 bbase[st] = dyo0;
             }
