@@ -1841,7 +1841,10 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
         // NSET register sets: the single-piece form (NP = 1) keeps two steps' loads in
         // flight (its steps are a third as long, and one step of flight left the loaders
         // waiting 11-22 % of the loop in vmcnt: tools/clock_probe.py --stamps --wgrad)
-        constexpr int NSET = NP == 1 ? 2 : 1;
+#ifndef X6W_NSET1  // (A/B builds: 3 sets measured neutral, profiles/r5l_ab_x6w_three_sets_bf16.txt)
+#define X6W_NSET1 2
+#endif
+        constexpr int NSET = NP == 1 ? X6W_NSET1 : 1;
         typename std::conditional<DB16, u32x2v, f32x4>::type rdy[NSET][DY_PER];
         typename std::conditional<XB16, u32x2v, f32x4>::type rx[NSET][X_PER];
         Act4 xa[NSET];
@@ -2044,7 +2047,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
             }
         };
         using Set0 = std::integral_constant<int, 0>;
-        using SetL = std::integral_constant<int, NSET - 1>;  // set of odd steps
+        // step s's loads go to register set s % NSET
         LCur lc;
         item_range(item0, lc.c);
         lderive(lc);
@@ -2052,11 +2055,16 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
         vm_wait<0>();
         lstore(0, Set0{});
         ladvance(lc);
-        gload(lc, SetL{});  // step 1
-        if constexpr (NSET == 2) {
+        gload(lc, std::integral_constant<int, 1 % NSET>{});  // step 1
+        if constexpr (NSET >= 2) {
             ladvance(lc);
-            gload(lc, Set0{});  // step 2 (set 0 was stored above)
+            gload(lc, std::integral_constant<int, 2 % NSET>{});  // step 2
         }
+        if constexpr (NSET >= 3) {
+            ladvance(lc);
+            gload(lc, Set0{});  // step 3 (set 0 was stored above)
+        }
+        static_assert(NSET <= 3, "at most three register sets");
         lds_barrier();
 #ifdef X6W_STAMP
         // diagnostic build: loader cycles waiting for global loads / at the barrier
@@ -2074,8 +2082,8 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
         // step k: write step k+1 (its loads retired: with two sets, step k+2's stay in
         // flight -- loads retire in issue order), then issue step k+1+NSET into the freed set
         auto lstep = [&](int k, auto S) {
-            if constexpr (NSET == 2) {
-                ST_WAIT(st_vm, vm_wait<LOADS>());
+            if constexpr (NSET >= 2) {  // steps k+2 .. k+NSET stay in flight
+                ST_WAIT(st_vm, vm_wait<(NSET - 1) * LOADS>());
             } else {
                 ST_WAIT(st_vm, vm_wait<0>());
             }
@@ -2084,13 +2092,12 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
             gload(lc, S);            // step k+1+NSET, in flight across the barrier
             ST_WAIT(st_bar, lds_barrier());
         };
-        if constexpr (NSET == 2) {
-            for (int k = 0; k < total; k += 2) {
-                lstep(k, SetL{});                         // step k+1 (odd): set 1
-                if (k + 1 < total) lstep(k + 1, Set0{});  // step k+2 (even): set 0
-            }
-        } else {
-            for (int k = 0; k < total; ++k) lstep(k, Set0{});
+        for (int k = 0; k < total; k += NSET) {  // lstep(k) stores step k+1: set (k+1) % NSET
+            lstep(k, std::integral_constant<int, 1 % NSET>{});
+            if constexpr (NSET >= 2)
+                if (k + 1 < total) lstep(k + 1, std::integral_constant<int, 2 % NSET>{});
+            if constexpr (NSET >= 3)
+                if (k + 2 < total) lstep(k + 2, Set0{});
         }
 #undef ST_WAIT
         vm_wait<0>();  // no load outlives the workgroup (nothing may run before this wait:
