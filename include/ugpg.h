@@ -172,7 +172,9 @@ typedef struct {
      * dy == dy_bf16 == NULL, bit-identical to it; dy_out (nullable) receives that dy, the
      * operand of the data gradient, written once per pixel -- the BatchNorm-backward apply
      * pass folded into the weight gradient.  UGPG_WFMT_X6 math, fp32 sources, da, y and
-     * dy_out, Cout % 64 == 0, 64-channel sources, db == NULL.  NULL: off. */
+     * dy_out, Cout % 64 == 0, 64-channel sources, db == NULL; or the image layer's form
+     * (one 8-channel source without activation, Cout == 64, Cin_real <= 3, dy_out == NULL:
+     * its dy has no other reader).  NULL: off. */
     const struct ugpg_bn_lazy* dy_bn;
 } ugpg_wgrad_t;
 typedef struct ugpg_bn_lazy {

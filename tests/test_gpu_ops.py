@@ -999,3 +999,42 @@ def test_wgrad_lazy_bn_dy_is_the_apply(dev, case):
             assert torch.equal(a_, b_), name
     finally:
         ops.set_conv_math(old)
+
+
+@pytest.mark.parametrize("shape", [(2, 36, 70), (1, 256, 256)])
+def test_wgrad_img_lazy_bn_dy_is_the_apply(dev, shape):
+    """The image layer's weight gradient (3 real channels of an 8-channel image, 64 outputs)
+    forming dy from the following BatchNorm backward (dy_out NULL: no other reader): dW and
+    the finalize's outputs bit-identical to the apply pass + the same kernel."""
+    from ugpg import ops
+    old = ops.conv_math()
+    ops.set_conv_math("x6")
+    try:
+        B, H, W = shape
+        C = 64
+        img = torch.zeros(B, H, W, 8)
+        img[..., :3] = nhwc(rnd((B, 3, H, W), 301, "img"))
+        srcs = [ops.Act(img.to(dev))]
+        y = nhwc(rnd((B, C, H, W), 302, "y") + 0.2).to(dev)
+        da = nhwc(rnd((B, C, H, W), 303, "da")).to(dev)
+        mean, invstd = rnd((C,), 304, "m", 0.1).to(dev), (rnd((C,), 305, "i").abs() + 0.5).to(dev)
+        scale, shift = (rnd((C,), 306, "s", 0.5) + 1).to(dev), rnd((C,), 307, "h", 0.3).to(dev)
+        part = torch.randn(3 * C, 1, generator=torch.Generator().manual_seed(308)).to(dev)
+        outs = []
+        for lazy in (False, True):
+            dg, dbt, dcb = (torch.zeros(C, device=dev) for _ in range(3))
+            dw = torch.empty(C, 3, 3, 3, device=dev)
+            if lazy:
+                coef = ops.bn_relu_bwd(da, y, mean, invstd, scale, shift, None, dg, dbt, dcb,
+                                       part=part)
+                ops.conv3x3_wgrad(srcs, ops.BnLazyDy(da, y, mean, invstd, scale, shift, coef, None),
+                                  dw, None, 3)
+            else:
+                dy = torch.empty_like(da)
+                ops.bn_relu_bwd(da, y, mean, invstd, scale, shift, dy, dg, dbt, dcb, part=part)
+                ops.conv3x3_wgrad(srcs, dy, dw, None, 3)
+            outs.append((dw, dg, dbt, dcb))
+        for name, a_, b_ in zip(("dW", "dgamma", "dbeta", "dbias"), *outs):
+            assert torch.equal(a_, b_), name
+    finally:
+        ops.set_conv_math(old)

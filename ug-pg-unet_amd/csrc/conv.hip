@@ -452,7 +452,11 @@ __global__ void __launch_bounds__(192) conv3x3_wgrad_c8_kernel(WgradArgs a) {
 // is a fixed count, so the summation order is device-independent.
 // ---------------------------------------------------------------------------
 constexpr int WGI_TH = 2, WGI_TW = 32, WGI_PX = 8, WGI_GRID = 1024, WGI_NCI = 3;
-
+// BN: dy formed from the following BatchNorm(+ReLU) backward while loading (a.bn_*: da, y
+// and the apply's coefficients; bn_bwd_dy, bit-identical to the apply pass) -- the image
+// layer's dy has no other reader (the input image needs no gradient), so the apply pass
+// over the largest activation of the network is dropped
+template <bool BN>
 __global__ void __launch_bounds__(256)
 conv3x3_wgrad_img_kernel(WgradArgs a) {
     typedef float f2 __attribute__((ext_vector_type(2)));
@@ -483,15 +487,33 @@ conv3x3_wgrad_img_kernel(WgradArgs a) {
     };
     // thread: channels 2*cp, 2*cp+1 of the 8-pixel segment (row, c0..c0+7)
     const int cp = lane & 31, seg = tid >> 5, row = seg / (TW / PX), c0 = (seg % (TW / PX)) * PX;
+    // BN: this thread's two channels' (scale, shift, mean, invstd, k0, k1)
+    f2 bc[BN ? 6 : 1];
+    if constexpr (BN) {
+        const float* src[6] = {a.bn_scale, a.bn_shift, a.bn_mean, a.bn_invstd, a.bn_coef,
+                               a.bn_coef + 64};
+#pragma unroll
+        for (int i = 0; i < 6; ++i) bc[i] = *reinterpret_cast<const f2*>(src[i] + 2 * cp);
+    }
     auto dy_fetch = [&](int tile, f2* d) {
         const int b = tile / tpi, trem = tile % tpi;
         const int gy = (trem / a.tiles_x) * TH + row, gx0 = (trem % a.tiles_x) * TW + c0;
-        const float* dyp = a.dy + ((size_t)(b * a.H + gy) * a.W + gx0) * 64 + 2 * cp;
+        const size_t o = ((size_t)(b * a.H + gy) * a.W + gx0) * 64 + 2 * cp;
 #pragma unroll
         for (int p = 0; p < PX; ++p) {
             d[p] = f2{0.f, 0.f};
-            if (tile < a.ntiles && gy < a.H && gx0 + p < a.W)
-                d[p] = *reinterpret_cast<const f2*>(dyp + (size_t)p * 64);
+            if (tile < a.ntiles && gy < a.H && gx0 + p < a.W) {
+                if constexpr (BN) {
+                    const f2 g = *reinterpret_cast<const f2*>(a.bn_da + o + (size_t)p * 64);
+                    const f2 v = *reinterpret_cast<const f2*>(a.bn_y + o + (size_t)p * 64);
+#pragma unroll
+                    for (int c = 0; c < 2; ++c)
+                        d[p][c] = bn_bwd_dy(g[c], v[c], bc[0][c], bc[1][c], bc[2][c], bc[3][c],
+                                            bc[4][c], bc[5][c]);
+                } else {
+                    d[p] = *reinterpret_cast<const f2*>(a.dy + o + (size_t)p * 64);
+                }
+            }
         }
     };
     float acc[NACC];
@@ -1034,7 +1056,14 @@ static int wgrad_check(const ugpg_wgrad_t* p) {
         return UGPG_ERR_INVALID;
     }
     const int C0 = p->src[0].C, C1 = wgrad_c1(p);
-    if (const ugpg_bn_lazy_t* l = p->dy_bn) {  // dy formed while loading (x6w, split-bf16)
+    if (const ugpg_bn_lazy_t* l = p->dy_bn) {  // dy formed while loading
+        // the image layer's kernel (8-channel image, no activation, 64 outputs: wgrad_kind's
+        // WG_IMG) forms it too, with no other reader of dy (dy_out == NULL)
+        const bool img = C1 == 0 && C0 == 8 && !p->db && !p->src[0].scale && p->Cout == 64 &&
+                         p->Cin_real > 0 && p->Cin_real <= WGI_NCI && !p->dy && !p->dy_bf16 &&
+                         !wgrad_b16(p) && l->da && l->y && l->mean && l->invstd && l->scale &&
+                         l->shift && l->coef && !l->dy_out;
+        if (img) return UGPG_OK;
         if (p->dy || p->dy_bf16 || p->math != UGPG_WFMT_X6 || p->db || C0 % 64 || C1 % 64 ||
             wgrad_b16(p) || p->Cout % 64 || p->Cin_real > C0 + C1 || !l->da || !l->y ||
             !l->mean || !l->invstd || !l->scale || !l->shift || !l->coef ||
@@ -1159,7 +1188,10 @@ extern "C" int ugpg_conv3x3_wgrad(const ugpg_wgrad_t* p, void* ws, size_t ws_byt
     if (kind == WG_X6) {
         launch_wgrad_x6(a, p->math == UGPG_WFMT_BF16 ? 1 : 3, st);
     } else if (kind == WG_IMG) {
-        hipLaunchKernelGGL(conv3x3_wgrad_img_kernel, dim3((unsigned)w.nsplit), dim3(256), 0, st, a);
+        if (a.bn_da)
+            hipLaunchKernelGGL(conv3x3_wgrad_img_kernel<true>, dim3((unsigned)w.nsplit), dim3(256), 0, st, a);
+        else
+            hipLaunchKernelGGL(conv3x3_wgrad_img_kernel<false>, dim3((unsigned)w.nsplit), dim3(256), 0, st, a);
     } else if (kind == WG_C8) {
         const unsigned grid = (unsigned)((p->Cout / 64) * w.nsplit);
         hipLaunchKernelGGL((conv3x3_wgrad_c8_kernel<WG8_TH, WG8_TW>), dim3(grid), dim3(192), 0, st,

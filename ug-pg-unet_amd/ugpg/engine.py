@@ -123,13 +123,14 @@ def double_conv_forward(mod, srcs, ctx: BlockCtx, save: bool):
     return cur[0]
 
 
-def _bn_relu_wgrad(conv, bn, y, st, in_srcs, da, grads, part=None, route=None):
+def _bn_relu_wgrad(conv, bn, y, st, in_srcs, da, grads, part=None, route=None, need_dy=True):
     """dy = dL/d(conv output) from da = dL/d(relu(bn(y))) -- in place, or, where the bf16
     arithmetic stores the activations in bf16 (y is bf16), into a bf16 tensor: exactly the
     operand its weight and data gradients read -- then dW, db.  Returns dy.
     part: BatchNorm-backward partials written by the data gradient that produced da.
     route: the deferred last producer of da (BlockCtx.route2): da holds only the base
-    gradient (nothing when route[1] is false) and the apply adds the producer's gradient."""
+    gradient (nothing when route[1] is false) and the apply adds the producer's gradient.
+    need_dy: the caller reads the returned dy (the data gradient); else None may return."""
     mean, invstd, scale, shift = st
     if mean is None:
         raise RuntimeError("backward through an eval-mode BatchNorm is not supported")
@@ -142,15 +143,20 @@ def _bn_relu_wgrad(conv, bn, y, st, in_srcs, da, grads, part=None, route=None):
     # loading (da, y) and writes it once for the data gradient, bit-identical to the apply
     # (in-process A/B: fp32 step -1.0 %, profiles/r5j_ab_step_folded_bn_apply.txt; the
     # single-piece form, whose loaders already wait on loads, was 1.6 % slower with it)
-    if (route is None and part is not None and dw is not None and co % 64 == 0
-            and ops.conv_math() == "x6" and y.dtype == torch.float32 and da.dtype == torch.float32
-            and all(s.C % 64 == 0 and s.y.dtype == torch.float32 for s in in_srcs)):
+    fold = route is None and part is not None and dw is not None and co % 64 == 0 and \
+        ops.conv_math() == "x6" and y.dtype == torch.float32 and da.dtype == torch.float32
+    x6w = fold and all(s.C % 64 == 0 and s.y.dtype == torch.float32 for s in in_srcs)
+    # the image layer's weight gradient (conv3x3_wgrad_img_kernel) forms it as well; its dy
+    # has no other reader (in-process A/B -0.2 %, profiles/r5m_ab_step_folded_apply_img.txt)
+    img = fold and not need_dy and co == 64 and len(in_srcs) == 1 and in_srcs[0].C == 8 and \
+        in_srcs[0].scale is None and in_srcs[0].y.dtype == torch.float32
+    if x6w or img:
         coef = ops.bn_relu_bwd(da, y, mean, invstd, scale, shift, None, grads.get(bn.weight),
                                grads.get(bn.bias), db, part=part)
-        dy = ops.empty(*da.shape, like=da)
+        dy = ops.empty(*da.shape, like=da) if x6w else None
         ci = conv.weight.shape[1]
         ops.conv3x3_wgrad(in_srcs, ops.BnLazyDy(da, y, mean, invstd, scale, shift, coef, dy), dw,
-                          None, ci, flops=2.0 * dy.numel() / co * co * 9 * ci)
+                          None, ci, flops=2.0 * da.numel() / co * co * 9 * ci)
         return dy
     dy = da
     if y.dtype == torch.bfloat16 and all(s.C % 64 == 0 for s in in_srcs) and \
@@ -196,7 +202,8 @@ def double_conv_backward(mod, ctx: BlockCtx, da2, targets, acc_flags, grads, pad
     ops.conv3x3_fwd([Act(dy2)], wpk2, None, cmid, [da1], flops=2.0 * npix * cmid * 9 * cout,
                     bnb=bnb)
     # stage 1: BN1/ReLU backward, wgrad(conv1), dgrad(conv1) -> source targets
-    dy1 = _bn_relu_wgrad(c1, b1, ctx.y1, ctx.st1, ctx.srcs, da1, grads, part=part)
+    dy1 = _bn_relu_wgrad(c1, b1, ctx.y1, ctx.st1, ctx.srcs, da1, grads, part=part,
+                         need_dy=any(t is not None for t in targets))
     if not any(t is not None for t in targets):
         return
     cin = c1.weight.shape[1]
