@@ -57,7 +57,7 @@ def test_lazy_bn_dy_wgrad_validation_without_gpu():
     import ctypes as C
     from ugpg import _C
     p = C.cast(C.c_void_p(0x1000), C.c_void_p)
-    lz = _C.BnLazy(p, p, p, p, p, p, p, None)
+    lz = _C.BnLazy(p, p, p, p, p, p, p, None, None, None)
     d = _C.WgradDesc()
     d.B, d.H, d.W = 1, 8, 16
     d.src[0] = _C.Src(p, None, None, 64, None)

@@ -1038,3 +1038,49 @@ def test_wgrad_img_lazy_bn_dy_is_the_apply(dev, shape):
             assert torch.equal(a_, b_), name
     finally:
         ops.set_conv_math(old)
+
+
+@pytest.mark.parametrize("case", [(2, 20, 36, 64, 0, 64), (2, 33, 41, 64, 64, 128), (1, 64, 64, 128, 0, 64)])
+@pytest.mark.parametrize("base", [True, False])
+def test_wgrad_lazy_bn_dy_pool_route_is_the_apply(dev, case, base):
+    """The folded apply with a deferred MaxPool2d backward routed into da (BlockCtx.route2
+    "pool"): the x6w loader adds the routed pooled gradient (argmax window match) to the
+    base gradient, as the routed apply does -- dy, dW and the finalize's outputs bit-identical
+    to bn_relu_bwd(route=("pool", ...)) + the weight gradient; odd sizes leave the last
+    row / column outside the pooled area."""
+    from ugpg import ops
+    old = ops.conv_math()
+    ops.set_conv_math("x6")
+    try:
+        B, H, W, C0, C1, Cout = case
+        cin = C0 + C1
+        x0 = nhwc(rnd((B, C0, H, W), 401, "x0")).to(dev)
+        x1 = nhwc(rnd((B, C1, H, W), 402, "x1")).to(dev) if C1 else None
+        sc0, sh0 = (rnd((C0,), 403, "s", 0.5) + 1).to(dev), rnd((C0,), 404, "h", 0.2).to(dev)
+        srcs = [ops.Act(x0, sc0, sh0)] + ([ops.Act(x1)] if C1 else [])
+        y = nhwc(rnd((B, Cout, H, W), 405, "y") + 0.2).to(dev)
+        mean, invstd = rnd((Cout,), 407, "m", 0.1).to(dev), (rnd((Cout,), 408, "i").abs() + 0.5).to(dev)
+        scale, shift = (rnd((Cout,), 409, "s", 0.5) + 1).to(dev), rnd((Cout,), 410, "h", 0.3).to(dev)
+        _, am = ops.maxpool2_fwd(ops.Act(y, scale, shift))
+        dout = nhwc(rnd((B, Cout, H // 2, W // 2), 411, "dp")).to(dev)
+        da = nhwc(rnd((B, Cout, H, W), 406, "da")).to(dev) if base else None
+        part = torch.randn(3 * Cout, 1, generator=torch.Generator().manual_seed(412)).to(dev)
+        outs = []
+        for lazy in (False, True):
+            dg, dbt, dcb = (torch.zeros(Cout, device=dev) for _ in range(3))
+            dw = torch.empty(Cout, cin, 3, 3, device=dev)
+            dy = torch.empty_like(y)
+            if lazy:
+                coef = ops.bn_relu_bwd(da, y, mean, invstd, scale, shift, None, dg, dbt, dcb,
+                                       part=part)
+                ops.conv3x3_wgrad(srcs, ops.BnLazyDy(da, y, mean, invstd, scale, shift, coef, dy,
+                                                     pool=(dout, am)), dw, None, cin)
+            else:
+                ops.bn_relu_bwd(da, y, mean, invstd, scale, shift, dy, dg, dbt, dcb, part=part,
+                                route=("pool", dout, am, H, W))
+                ops.conv3x3_wgrad(srcs, dy, dw, None, cin)
+            outs.append((dy, dw, dg, dbt, dcb))
+        for name, a_, b_ in zip(("dy", "dW", "dgamma", "dbeta", "dbias"), *outs):
+            assert torch.equal(a_, b_), name
+    finally:
+        ops.set_conv_math(old)

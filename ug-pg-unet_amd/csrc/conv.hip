@@ -1062,10 +1062,11 @@ static int wgrad_check(const ugpg_wgrad_t* p) {
         const bool img = C1 == 0 && C0 == 8 && !p->db && !p->src[0].scale && p->Cout == 64 &&
                          p->Cin_real > 0 && p->Cin_real <= WGI_NCI && !p->dy && !p->dy_bf16 &&
                          !wgrad_b16(p) && l->da && l->y && l->mean && l->invstd && l->scale &&
-                         l->shift && l->coef && !l->dy_out;
+                         l->shift && l->coef && !l->dy_out && !l->route_src && !l->route_argmax;
         if (img) return UGPG_OK;
         if (p->dy || p->dy_bf16 || p->math != UGPG_WFMT_X6 || p->db || C0 % 64 || C1 % 64 ||
-            wgrad_b16(p) || p->Cout % 64 || p->Cin_real > C0 + C1 || !l->da || !l->y ||
+            wgrad_b16(p) || p->Cout % 64 || p->Cin_real > C0 + C1 ||
+            (!l->da && !l->route_src) || !l->route_src != !l->route_argmax || !l->y ||
             !l->mean || !l->invstd || !l->scale || !l->shift || !l->coef ||
             (l->dy_out && (l->dy_out == l->da || l->dy_out == l->y))) {
             set_error("conv3x3_wgrad: dy_bn needs the split-bf16 arithmetic, fp32 sources of "
@@ -1172,6 +1173,8 @@ extern "C" int ugpg_conv3x3_wgrad(const ugpg_wgrad_t* p, void* ws, size_t ws_byt
     a.bn_shift = bl ? bl->shift : nullptr;
     a.bn_coef = bl ? bl->coef : nullptr;
     a.bn_dy_out = bl ? bl->dy_out : nullptr;
+    a.bn_rsrc = bl ? bl->route_src : nullptr;
+    a.bn_ram = bl ? bl->route_argmax : nullptr;
     a.Cout = p->Cout;
     a.Cin = Cin;
     a.part = static_cast<float*>(ws);
@@ -1188,7 +1191,7 @@ extern "C" int ugpg_conv3x3_wgrad(const ugpg_wgrad_t* p, void* ws, size_t ws_byt
     if (kind == WG_X6) {
         launch_wgrad_x6(a, p->math == UGPG_WFMT_BF16 ? 1 : 3, st);
     } else if (kind == WG_IMG) {
-        if (a.bn_da)
+        if (a.bn_y)
             hipLaunchKernelGGL(conv3x3_wgrad_img_kernel<true>, dim3((unsigned)w.nsplit), dim3(256), 0, st, a);
         else
             hipLaunchKernelGGL(conv3x3_wgrad_img_kernel<false>, dim3((unsigned)w.nsplit), dim3(256), 0, st, a);

@@ -179,6 +179,8 @@ struct WgradArgs {
     const float* bn_shift;
     const float* bn_coef;
     float* bn_dy_out;
+    const float* bn_rsrc;    // MaxPool2d route of da (nullable): pooled gradient, argmax
+    const uint8_t* bn_ram;
     int Cout, Cin;
     float* part;
     float* dbpart;

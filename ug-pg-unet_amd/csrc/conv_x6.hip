@@ -344,6 +344,12 @@ __device__ __forceinline__ u32x2v gld8(const void* p) {
     asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(r) : "v"(p));
     return r;
 }
+// ... and 4 bytes
+__device__ __forceinline__ unsigned gld4(const void* p) {
+    unsigned r;
+    asm volatile("global_load_dword %0, %1, off" : "=v"(r) : "v"(p));
+    return r;
+}
 // LDS-DMA: 16 bytes per lane from g (per-lane address) to lds_wave + 16*lane (lds_wave
 // wave-uniform), counted by vmcnt like a load; no VGPR destination
 __device__ __forceinline__ void glds16(const void* g, void* lds_wave) {
@@ -1853,6 +1859,10 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
         // BN: y beside da, the lane's 4 channels' (scale, shift, mean, invstd, k0, k1), and
         // where (and whether: first ci block) the formed dy goes
         f32x4 rby[BN ? NSET : 1][BN ? DY_PER : 1], bco[BN ? NSET : 1][6];
+        // BN with a MaxPool2d route: the pooled gradient and argmax bytes of each vector's
+        // pixel, and the pixel's window position (255: outside the pooled area)
+        f32x4 rrs[BN ? NSET : 1][BN ? DY_PER : 1];
+        unsigned ram[BN ? NSET : 1][BN ? DY_PER : 1], rkk[BN ? NSET : 1][BN ? DY_PER : 1];
         int bco_nb = -1;  // output-channel block whose coefficients bco holds
         static_assert(!BN || NSET == 1, "one coefficient set");
         bool bwr[NSET];
@@ -1983,9 +1993,21 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
 #pragma unroll
             for (int v = 0; v < DY_PER; ++v) {
                 if constexpr (BN) {
-                    rdy[st][v] = gld16(a.bn_da + dyo0 + dof[v]);
+                    // (no base gradient with a route: y's address stands in, the value unused --
+                    // the loads stay one straight sequence)
+                    rdy[st][v] = gld16((a.bn_da ? a.bn_da : a.bn_y) + dyo0 + dof[v]);
                     rby[st][v] = gld16(a.bn_y + dyo0 + dof[v]);
                     bof[st][v] = dof[v];
+                    if (a.bn_rsrc) {  // (uniform)
+                        const int p = (lt + v * 256) >> 4;
+                        const int gy = ty0 + p / TW, gx = tx0 + p % TW, Ho = a.H >> 1, Wo = a.W >> 1;
+                        const bool rok = gy < a.H && gx < a.W && (gy >> 1) < Ho && (gx >> 1) < Wo;
+                        const size_t ro = (rok ? ((size_t)(b * Ho + (gy >> 1)) * Wo + (gx >> 1)) * a.Cout : 0) +
+                                          co0 + q4;
+                        rrs[st][v] = gld16(a.bn_rsrc + ro);
+                        ram[st][v] = gld4(a.bn_ram + ro);
+                        rkk[st][v] = rok ? (unsigned)((gy & 1) * 2 + (gx & 1)) : 255u;
+                    }
                 } else if constexpr (DB16) {
                     rdy[st][v] = gld8(a.dy16 + dyo0 + dof[v]);
                 } else {
@@ -2022,6 +2044,17 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
                     d = rdy[st][v];
                 const bool ok = (dvalid[st] >> v) & 1u;
                 if constexpr (BN) {
+                    if (a.bn_rsrc) {  // (uniform) da = routed + base, in the apply's order
+                        f32x4 g;
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            g[i] = ((ram[st][v] >> (8 * i)) & 0xffu) == rkk[st][v] ? rrs[st][v][i] : 0.f;
+                        if (a.bn_da) {
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) g[i] += d[i];
+                        }
+                        d = g;
+                    }
                     const f32x4 yv = rby[st][v];
 #pragma unroll
                     for (int i = 0; i < 4; ++i)
@@ -2220,7 +2253,7 @@ void launch_wgrad_x6(const WgradArgs& a, int np, hipStream_t st) {
     const int64_t items = (int64_t)(a.Cout / 64) * (a.Cin / 64) * a.nsplit;
     int64_t g = std::min<int64_t>(cu_count(st), (items + 7) / 8 * 8);
     g = std::max<int64_t>(8, g / 8 * 8);
-    if (np == 3 && a.bn_da)
+    if (np == 3 && a.bn_y)  // (dy formed while loading; da may be absent with a route)
         hipLaunchKernelGGL((conv3x3_wgrad_x6w_kernel<WGX6W_TH, WGX6_TW, 3, 0, true>),
                            dim3((unsigned)g), dim3(512), 0, st, a);
     else if (np == 3)

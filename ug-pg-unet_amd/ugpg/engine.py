@@ -143,20 +143,25 @@ def _bn_relu_wgrad(conv, bn, y, st, in_srcs, da, grads, part=None, route=None, n
     # loading (da, y) and writes it once for the data gradient, bit-identical to the apply
     # (in-process A/B: fp32 step -1.0 %, profiles/r5j_ab_step_folded_bn_apply.txt; the
     # single-piece form, whose loaders already wait on loads, was 1.6 % slower with it)
-    fold = route is None and part is not None and dw is not None and co % 64 == 0 and \
-        ops.conv_math() == "x6" and y.dtype == torch.float32 and da.dtype == torch.float32
+    # (a deferred max-pool backward is routed into da by the x6w loader too, -0.3 %,
+    # profiles/r5o_ab_step_folded_apply_pool_route.txt; the head route keeps the apply pass)
+    pool = route is not None and route[0][0] == "pool"
+    fold = (route is None or pool) and part is not None and dw is not None and co % 64 == 0 \
+        and ops.conv_math() == "x6" and y.dtype == torch.float32 and da.dtype == torch.float32
     x6w = fold and all(s.C % 64 == 0 and s.y.dtype == torch.float32 for s in in_srcs)
     # the image layer's weight gradient (conv3x3_wgrad_img_kernel) forms it as well; its dy
     # has no other reader (in-process A/B -0.2 %, profiles/r5m_ab_step_folded_apply_img.txt)
-    img = fold and not need_dy and co == 64 and len(in_srcs) == 1 and in_srcs[0].C == 8 and \
+    img = fold and not pool and not need_dy and co == 64 and len(in_srcs) == 1 and in_srcs[0].C == 8 and \
         in_srcs[0].scale is None and in_srcs[0].y.dtype == torch.float32
     if x6w or img:
-        coef = ops.bn_relu_bwd(da, y, mean, invstd, scale, shift, None, grads.get(bn.weight),
+        base = da if not pool or route[1] else None
+        coef = ops.bn_relu_bwd(base, y, mean, invstd, scale, shift, None, grads.get(bn.weight),
                                grads.get(bn.bias), db, part=part)
-        dy = ops.empty(*da.shape, like=da) if x6w else None
+        dy = ops.empty(*y.shape, like=y) if x6w else None
         ci = conv.weight.shape[1]
-        ops.conv3x3_wgrad(in_srcs, ops.BnLazyDy(da, y, mean, invstd, scale, shift, coef, dy), dw,
-                          None, ci, flops=2.0 * da.numel() / co * co * 9 * ci)
+        ops.conv3x3_wgrad(in_srcs, ops.BnLazyDy(base, y, mean, invstd, scale, shift, coef, dy,
+                                                pool=route[0][1:3] if pool else None),
+                          dw, None, ci, flops=2.0 * y.numel() / co * co * 9 * ci)
         return dy
     dy = da
     if y.dtype == torch.bfloat16 and all(s.C % 64 == 0 for s in in_srcs) and \

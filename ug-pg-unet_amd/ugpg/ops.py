@@ -298,16 +298,20 @@ class BnLazyDy:
     """dy of a weight gradient formed while loading from the following BatchNorm(+ReLU)
     backward (ugpg_wgrad_t.dy_bn): da, the BN input y and its statistics, `coef` the
     workspace bn_relu_bwd(..., dy=None, part=...) returned (its finalize only), and dy_out
-    receiving dy for the data gradient (bit-identical to the apply pass)."""
-    __slots__ = ("da", "y", "mean", "invstd", "scale", "shift", "coef", "dy_out")
+    receiving dy for the data gradient (bit-identical to the apply pass).  pool: (dout,
+    argmax) of a deferred MaxPool2d backward routed into da (bn_relu_bwd's "pool" route;
+    da then holds only the base gradient, or None)."""
+    __slots__ = ("da", "y", "mean", "invstd", "scale", "shift", "coef", "dy_out", "pool")
 
-    def __init__(self, da, y, mean, invstd, scale, shift, coef, dy_out):
+    def __init__(self, da, y, mean, invstd, scale, shift, coef, dy_out, pool=None):
         self.da, self.y, self.mean, self.invstd = da, y, mean, invstd
         self.scale, self.shift, self.coef, self.dy_out = scale, shift, coef, dy_out
+        self.pool = pool
 
     @property
     def shape(self):
-        return tuple(self.da.shape)
+        return tuple(self.y.shape)
+
 
 
 def conv3x3_wgrad(srcs, dy, dw, db, cin_real, accumulate=0, flops=None):
@@ -319,10 +323,11 @@ def conv3x3_wgrad(srcs, dy, dw, db, cin_real, accumulate=0, flops=None):
     d.src[1] = srcs[1].src() if len(srcs) > 1 else NULL_SRC
     lazy = None
     if isinstance(dy, BnLazyDy):
+        pool = dy.pool or (None, None)
         lazy = BnLazy(ptr(dy.da), ptr(dy.y), ptr(dy.mean), ptr(dy.invstd), ptr(dy.scale),
-                      ptr(dy.shift), ptr(dy.coef), ptr(dy.dy_out))
+                      ptr(dy.shift), ptr(dy.coef), ptr(dy.dy_out), ptr(pool[0]), ptr(pool[1]))
         d.dy_bn = C.pointer(lazy)
-        dy = dy.da
+        dy = dy.y
     else:
         d.dy, d.dy_bf16 = _yargs(dy)  # dy fp32, or bf16 (the bf16 arithmetic's storage)
     d.Cout = dy.shape[-1]
@@ -401,7 +406,8 @@ def bn_relu_bwd(da, y, mean, invstd, scale, shift, dy, dgamma, dbeta, dconv_bias
         # (its first 2*C floats) for conv3x3_wgrad(dy=BnLazyDy(..., coef=ws, ...))
         ws = workspace(lib.ugpg_bn_relu_bwd_partials_workspace(c), y.device)
         check(lib.ugpg_bn_relu_bwd_partials(
-            ptr(part), part.numel() // (3 * c), *_yargs(da), *_yargs(y), npix, c, ptr(mean), ptr(invstd),
+            ptr(part), part.numel() // (3 * c), *(_yargs(da) if da is not None else (None, None)),
+            *_yargs(y), npix, c, ptr(mean), ptr(invstd),
             ptr(scale), ptr(shift), *(_yargs(dy) if dy is not None else (None, None)), ptr(dgamma),
             ptr(dbeta), ptr(dconv_bias), int(accumulate), ptr(ws), ws.numel(), stream()),
             "bn_relu_bwd_partials")
