@@ -34,6 +34,9 @@ extern "C" {
 #define UGPG_ERR_COMM (-4)        /* RCCL / device error in a ugpg_comm_* call */
 
 const char* ugpg_version(void);
+/* Content hash of the sources and flags this library was built from (build.py
+ * source_id()); the Python layer refuses a library whose id differs from its tree. */
+const char* ugpg_build_id(void);
 const char* ugpg_last_error(void);
 
 /* A lazily-activated NHWC operand: value = relu(scale[c]*x + shift[c]) when

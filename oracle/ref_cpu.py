@@ -183,16 +183,20 @@ class _Bf16GradRound(torch.autograd.Function):
 # The build's bf16 arithmetic also stores the data gradient of each DoubleConv's second
 # conv -- dL/d(its input), the first BatchNorm+ReLU's output gradient -- in bf16 for images
 # >= 32 wide (the x6r single-piece epilogue writes da1 in bf16 with the BatchNorm-backward
-# partials of the rounded values; the BN1 backward reads it).  Off only for experiments.
+# partials of the rounded values; the BN1 backward reads it).  Not in a block whose input
+# is the image (inc: the 3-channel source, zero-padded to 8, is not a 64-channel multiple,
+# so BN1's backward there writes an fp32 dy and the build keeps da1 fp32 too --
+# ugpg.engine.double_conv_backward `da16`).  Off only for experiments.
 BF16_DGRAD_STORE = True
 
 
 def double_conv(P, prefix, x, training):
     """Two conv -> BN -> ReLU.  Under CONV_MATH "bf16" a conv output of an image >= 32
     wide is stored in bf16 before its BatchNorm (see _bf16_store), and so is the data
-    gradient of the second conv (BF16_DGRAD_STORE)."""
+    gradient of the second conv (BF16_DGRAD_STORE) unless the block reads the image."""
+    src64 = x.shape[1] % 64 == 0
     for conv_i, bn_i in ((0, 1), (3, 4)):
-        if conv_i == 3 and BF16_DGRAD_STORE and _bf16_store(x):
+        if conv_i == 3 and BF16_DGRAD_STORE and src64 and _bf16_store(x):
             x = _Bf16GradRound.apply(x)
         y = conv3x3(x, P[f"{prefix}.{conv_i}.weight"], P[f"{prefix}.{conv_i}.bias"])
         if _bf16_store(y):

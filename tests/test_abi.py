@@ -20,6 +20,28 @@ def test_library_loads_and_reports_version():
     assert _C.lib.ugpg_last_error() is not None
 
 
+def test_library_is_built_from_these_sources():
+    """The in-tree library's embedded build id is the content hash of csrc/ + include/ +
+    flags (a stale prebuilt .so travels with the tree to the GPU box),
+    and the loader refuses a library whose id differs."""
+    import importlib.util
+    import pytest
+    from ugpg import _C
+    spec = importlib.util.spec_from_file_location("_b", ROOT / "ug-pg-unet_amd" / "build.py")
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    assert _C.lib.ugpg_build_id().decode() == b.source_id() == b.lib_id(_C.LIB_PATH)
+
+    class Fn:  # a ctypes function stand-in returning another id
+        def __call__(self):
+            return b"0" * 32
+
+    class Stale:
+        ugpg_build_id = Fn()
+    with pytest.raises(ImportError, match="stale"):
+        _C._check_fresh(Stale())
+
+
 def test_every_declared_symbol_is_exported_and_bound():
     from ugpg import _C
     names = declared()

@@ -255,7 +255,11 @@ def _replica_worker(rank, port, outdir):
     # the same rows in a different order on rank 1 (the shards would overlap), and the same
     # inputs with different targets: both refused
     perm = torch.tensor([1, 0, 2, 3, 4]) if rank == 1 else torch.arange(5)
-    for xa, ya in ((x[perm], y[perm]), (x, y + rank)):
+    # rows of equal sums swapped on rank 1 (a position-weighted sum of row sums
+    # cannot see it), e.g. binary masks with the same foreground count
+    z = torch.tensor([[1., 0., 0.], [0., 1., 0.], [0., 0., 1.], [1., 1., 0.]])
+    zp = z[torch.tensor([1, 0, 2, 3])] if rank == 1 else z
+    for xa, ya in ((x[perm], y[perm]), (x, y + rank), (zp, zp)):
         try:
             shard_batch(plain, xa, ya, check=True)
             refused.append(False)
@@ -277,7 +281,7 @@ def test_trainers_start_from_rank0_weights_and_shard_batches():
     assert r[0]["through"] and r[1]["through"]
     assert r[0]["checked"] == [0.0, 1.0] and r[1]["checked"] == [2.0, 3.0]
     assert all("different global batches" in (x["mismatch"] or "") for x in r)
-    assert all(x["refused"] == [True, True] for x in r), [x["refused"] for x in r]
+    assert all(x["refused"] == [True, True, True] for x in r), [x["refused"] for x in r]
 
 
 def _mixed_worker(rank, port, outdir):

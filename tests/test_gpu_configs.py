@@ -43,7 +43,10 @@ def _hip_step(dev, state, prev, x, t):
     out = m(xd)
     crit = nn.BCEWithLogitsLoss(pos_weight=torch.tensor([5.0], device=dev), reduction="none")
     final, base = L.apply_uncertainty_weighted_loss(crit, out, td, u, 1.0)
+    lg_fwd = out.detach().clone()
     final.backward()
+    # the backward must leave the forward's logits alone
+    assert torch.equal(out.detach(), lg_fwd), "the backward pass modified the forward's logits"
     grads = {k: p.grad.detach().cpu().clone() for k, p in m.named_parameters()}
     opt = ugpg.RMSprop(m.parameters(), lr=1e-4, weight_decay=1e-4)
     opt.step()

@@ -947,6 +947,31 @@ def test_resize_bilinear_backward(dev, hi, wi, ho, wo):
     assert (got - ref).abs().max().item() <= 1e-5 * max(1.0, ref.abs().max().item())
 
 
+class _Guards:
+    """Device tensors placed inside NaN-canary guard bands (tests/_guard.py); check() asserts
+    that no kernel of the test wrote past either end of any of them."""
+
+    def __init__(self, dev):
+        self.dev, self.all = dev, []
+
+    def __call__(self, host, name):
+        from tests._guard import guarded
+        g = guarded(tuple(host.shape), self.dev, host.dtype, fill=host.to(self.dev))
+        self.all.append((g, name))
+        return g.t
+
+    def empty(self, shape, name, dtype=torch.float32):
+        from tests._guard import guarded
+        g = guarded(shape, self.dev, dtype)
+        self.all.append((g, name))
+        return g.t
+
+    def check(self):
+        torch.cuda.synchronize()
+        for g, name in self.all:
+            g.check(name)
+
+
 LAZY_CASES = [  # B, H, W, C0, C1, Cout: one / two sources, partial tiles, 2 ci and 2 co blocks
     (2, 20, 36, 64, 0, 64),
     (2, 33, 40, 64, 64, 128),
@@ -971,8 +996,9 @@ def test_wgrad_lazy_bn_dy_is_the_apply(dev, case):
         x1 = nhwc(rnd((B, C1, H, W), 202, "x1")).to(dev) if C1 else None
         sc0, sh0 = (rnd((C0,), 203, "s", 0.5) + 1).to(dev), rnd((C0,), 204, "h", 0.2).to(dev)
         srcs = [ops.Act(x0, sc0, sh0)] + ([ops.Act(x1)] if C1 else [])
-        y = nhwc(rnd((B, Cout, H, W), 205, "y") + 0.2).to(dev)
-        da = nhwc(rnd((B, Cout, H, W), 206, "da")).to(dev)
+        gd = _Guards(dev)
+        y = gd(nhwc(rnd((B, Cout, H, W), 205, "y") + 0.2), "y")
+        da = gd(nhwc(rnd((B, Cout, H, W), 206, "da")), "da")
         mean, invstd = rnd((Cout,), 207, "m", 0.1).to(dev), (rnd((Cout,), 208, "i").abs() + 0.5).to(dev)
         scale, shift = (rnd((Cout,), 209, "s", 0.5) + 1).to(dev), rnd((Cout,), 210, "h", 0.3).to(dev)
         # one partial slot: (sum g, sum g*xhat, sum xhat) per channel
@@ -980,12 +1006,12 @@ def test_wgrad_lazy_bn_dy_is_the_apply(dev, case):
         g = torch.where(yd * scale.double() + shift.double() > 0, dd, torch.zeros_like(dd))
         xh = (yd - mean.double()) * invstd.double()
         part = torch.stack([g.sum((0, 1, 2)), (g * xh).sum((0, 1, 2)), xh.sum((0, 1, 2))]).float()
-        part = part.reshape(3 * Cout, 1).contiguous()
+        part = gd(part.reshape(3 * Cout, 1).cpu(), "part")
         outs = []
         for lazy in (False, True):
-            dg, dbt, dcb = (torch.zeros(Cout, device=dev) for _ in range(3))
-            dw = torch.empty(Cout, cin, 3, 3, device=dev)
-            dy = torch.empty_like(da)
+            dg, dbt, dcb = (gd(torch.zeros(Cout), n) for n in ("dgamma", "dbeta", "dbias"))
+            dw = gd.empty((Cout, cin, 3, 3), "dW")
+            dy = gd.empty(tuple(da.shape), "dy")
             if lazy:
                 coef = ops.bn_relu_bwd(da, y, mean, invstd, scale, shift, None, dg, dbt, dcb,
                                        part=part)
@@ -995,6 +1021,7 @@ def test_wgrad_lazy_bn_dy_is_the_apply(dev, case):
                 ops.bn_relu_bwd(da, y, mean, invstd, scale, shift, dy, dg, dbt, dcb, part=part)
                 ops.conv3x3_wgrad(srcs, dy, dw, None, cin)
             outs.append((dy, dw, dg, dbt, dcb))
+        gd.check()
         for name, a_, b_ in zip(("dy", "dW", "dgamma", "dbeta", "dbias"), *outs):
             assert torch.equal(a_, b_), name
     finally:
@@ -1015,25 +1042,27 @@ def test_wgrad_img_lazy_bn_dy_is_the_apply(dev, shape):
         img = torch.zeros(B, H, W, 8)
         img[..., :3] = nhwc(rnd((B, 3, H, W), 301, "img"))
         srcs = [ops.Act(img.to(dev))]
-        y = nhwc(rnd((B, C, H, W), 302, "y") + 0.2).to(dev)
-        da = nhwc(rnd((B, C, H, W), 303, "da")).to(dev)
+        gd = _Guards(dev)
+        y = gd(nhwc(rnd((B, C, H, W), 302, "y") + 0.2), "y")
+        da = gd(nhwc(rnd((B, C, H, W), 303, "da")), "da")
         mean, invstd = rnd((C,), 304, "m", 0.1).to(dev), (rnd((C,), 305, "i").abs() + 0.5).to(dev)
         scale, shift = (rnd((C,), 306, "s", 0.5) + 1).to(dev), rnd((C,), 307, "h", 0.3).to(dev)
-        part = torch.randn(3 * C, 1, generator=torch.Generator().manual_seed(308)).to(dev)
+        part = gd(torch.randn(3 * C, 1, generator=torch.Generator().manual_seed(308)), "part")
         outs = []
         for lazy in (False, True):
-            dg, dbt, dcb = (torch.zeros(C, device=dev) for _ in range(3))
-            dw = torch.empty(C, 3, 3, 3, device=dev)
+            dg, dbt, dcb = (gd(torch.zeros(C), n) for n in ("dgamma", "dbeta", "dbias"))
+            dw = gd.empty((C, 3, 3, 3), "dW")
             if lazy:
                 coef = ops.bn_relu_bwd(da, y, mean, invstd, scale, shift, None, dg, dbt, dcb,
                                        part=part)
                 ops.conv3x3_wgrad(srcs, ops.BnLazyDy(da, y, mean, invstd, scale, shift, coef, None),
                                   dw, None, 3)
             else:
-                dy = torch.empty_like(da)
+                dy = gd.empty(tuple(da.shape), "dy")
                 ops.bn_relu_bwd(da, y, mean, invstd, scale, shift, dy, dg, dbt, dcb, part=part)
                 ops.conv3x3_wgrad(srcs, dy, dw, None, 3)
             outs.append((dw, dg, dbt, dcb))
+        gd.check()
         for name, a_, b_ in zip(("dW", "dgamma", "dbeta", "dbias"), *outs):
             assert torch.equal(a_, b_), name
     finally:
@@ -1058,18 +1087,20 @@ def test_wgrad_lazy_bn_dy_pool_route_is_the_apply(dev, case, base):
         x1 = nhwc(rnd((B, C1, H, W), 402, "x1")).to(dev) if C1 else None
         sc0, sh0 = (rnd((C0,), 403, "s", 0.5) + 1).to(dev), rnd((C0,), 404, "h", 0.2).to(dev)
         srcs = [ops.Act(x0, sc0, sh0)] + ([ops.Act(x1)] if C1 else [])
-        y = nhwc(rnd((B, Cout, H, W), 405, "y") + 0.2).to(dev)
+        gd = _Guards(dev)
+        y = gd(nhwc(rnd((B, Cout, H, W), 405, "y") + 0.2), "y")
         mean, invstd = rnd((Cout,), 407, "m", 0.1).to(dev), (rnd((Cout,), 408, "i").abs() + 0.5).to(dev)
         scale, shift = (rnd((Cout,), 409, "s", 0.5) + 1).to(dev), rnd((Cout,), 410, "h", 0.3).to(dev)
         _, am = ops.maxpool2_fwd(ops.Act(y, scale, shift))
-        dout = nhwc(rnd((B, Cout, H // 2, W // 2), 411, "dp")).to(dev)
-        da = nhwc(rnd((B, Cout, H, W), 406, "da")).to(dev) if base else None
-        part = torch.randn(3 * Cout, 1, generator=torch.Generator().manual_seed(412)).to(dev)
+        am = gd(am.cpu(), "argmax")
+        dout = gd(nhwc(rnd((B, Cout, H // 2, W // 2), 411, "dp")), "dout")
+        da = gd(nhwc(rnd((B, Cout, H, W), 406, "da")), "da") if base else None
+        part = gd(torch.randn(3 * Cout, 1, generator=torch.Generator().manual_seed(412)), "part")
         outs = []
         for lazy in (False, True):
-            dg, dbt, dcb = (torch.zeros(Cout, device=dev) for _ in range(3))
-            dw = torch.empty(Cout, cin, 3, 3, device=dev)
-            dy = torch.empty_like(y)
+            dg, dbt, dcb = (gd(torch.zeros(Cout), n) for n in ("dgamma", "dbeta", "dbias"))
+            dw = gd.empty((Cout, cin, 3, 3), "dW")
+            dy = gd.empty(tuple(y.shape), "dy")
             if lazy:
                 coef = ops.bn_relu_bwd(da, y, mean, invstd, scale, shift, None, dg, dbt, dcb,
                                        part=part)
@@ -1080,6 +1111,7 @@ def test_wgrad_lazy_bn_dy_pool_route_is_the_apply(dev, case, base):
                                 route=("pool", dout, am, H, W))
                 ops.conv3x3_wgrad(srcs, dy, dw, None, cin)
             outs.append((dy, dw, dg, dbt, dcb))
+        gd.check()
         for name, a_, b_ in zip(("dy", "dW", "dgamma", "dbeta", "dbias"), *outs):
             assert torch.equal(a_, b_), name
     finally:

@@ -1799,7 +1799,11 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
     constexpr int DY_Q = P * 16, X_Q = NHALO * 16;  // float4 quads per tile
     constexpr int DY_PER = (DY_Q + 255) / 256, X_PER = (X_Q + 255) / 256;
     constexpr int RECS = P + NHALO;                  // records per buffer
-    constexpr int LOADS = DY_PER + X_PER + 2 + (BN ? DY_PER : 0);  // loader untracked VMEM per step
+    // loader untracked VMEM per step: dY, X, the two coefficient loads and, with the lazy
+    // BatchNorm-backward dy, the y loads plus the max-pool route's pooled-gradient and argmax
+    // loads (2 * DY_PER, an upper bound: issued only on routed launches).  Only counted waits
+    // of earlier register sets use it (NSET > 1), which BN excludes today (static_assert below)
+    constexpr int LOADS = DY_PER + X_PER + 2 + (BN ? 3 * DY_PER : 0);
     __shared__ __attribute__((aligned(16))) char smem[(2 * RECS + 1) * REC];
     char* const dummy = smem + 2 * RECS * REC;    // record for idle lanes' writes
 

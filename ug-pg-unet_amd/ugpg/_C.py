@@ -63,6 +63,7 @@ class WgradDesc(C.Structure):
 # name -> (restype, argtypes); must match include/ugpg.h exactly
 SIGNATURES = {
     "ugpg_version": (C.c_char_p, []),
+    "ugpg_build_id": (C.c_char_p, []),
     "ugpg_last_error": (C.c_char_p, []),
     "ugpg_conv3x3_fwd": (_i, [C.POINTER(ConvDesc), _p]),
     "ugpg_conv3x3_fwd_ntiles": (_i, [_i, _i, _i, _i, _i, _i]),
@@ -144,6 +145,32 @@ SIGNATURES = {
 }
 
 
+def _check_fresh(lib) -> None:
+    """Refuse an in-tree libugpg.so built from other sources than the ones beside it (a
+    stale prebuilt library travelling with the tree): its embedded
+    ugpg_build_id() must equal build.source_id() of csrc/ + include/.  Skipped for an
+    explicit UGPG_LIB (A/B variants are built from other defines on purpose)."""
+    if "UGPG_LIB" in os.environ:
+        return
+    bpy = Path(__file__).resolve().parent.parent / "build.py"
+    if not bpy.exists():
+        return
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("_ugpg_build", bpy)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    want = mod.source_id()
+    fn = getattr(lib, "ugpg_build_id", None)
+    got = None
+    if fn is not None:
+        fn.restype, fn.argtypes = C.c_char_p, []
+        got = fn().decode()
+    if got != want:
+        raise ImportError(
+            f"ugpg: {LIB_PATH} is stale (built from sources {got}, tree has {want}) -- "
+            "rebuild it with `python ug-pg-unet_amd/build.py`. There is no CPU fallback.")
+
+
 class _Lib:
     def __init__(self):
         self._lib = None
@@ -155,6 +182,7 @@ class _Lib:
                     f"ugpg: native library {LIB_PATH} not found -- build it with "
                     "`python ug-pg-unet_amd/build.py` (hipcc, gfx950). There is no CPU fallback.")
             lib = C.CDLL(str(LIB_PATH))
+            _check_fresh(lib)
             for name, (res, args) in SIGNATURES.items():
                 fn = getattr(lib, name)
                 fn.restype = res

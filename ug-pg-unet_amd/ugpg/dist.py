@@ -409,39 +409,47 @@ def _has_distributed_sampler(loader) -> bool:
     return False
 
 
-def _batch_checksum(t: torch.Tensor) -> float:
-    """Order-sensitive float64 checksum of a batch: each row's sum weighted by its position
-    (1..n), so two ranks holding the same rows in a different order -- which shard_batch
-    would split into different, overlapping shards -- disagree."""
-    if t.dim() == 0 or t.shape[0] == 0:
-        return float(t.detach().double().sum().item())
-    rows = t.detach().double().reshape(t.shape[0], -1).sum(1)
-    w = torch.arange(1, t.shape[0] + 1, dtype=torch.float64, device=rows.device)
-    return float((rows * w).sum().item())
+def _batch_fingerprint(t: torch.Tensor) -> torch.Tensor:
+    """Per-row float64 fingerprint of a batch, shape (rows, 2): each row's sum and its dot
+    product with fixed non-constant weights.  Compared row by row across ranks, so rows in
+    a different order -- which shard_batch would split into different, overlapping shards
+    -- and rows with equal sums but different content both disagree (one
+    position-weighted scalar let swapped rows of near-equal sums through)."""
+    r = t.detach().double().reshape(t.shape[0] if t.dim() else 1, -1)
+    m = r.shape[1]
+    w = torch.sin(torch.arange(1, m + 1, dtype=torch.float64, device=r.device) * 0.7548776662466927) + 1.5
+    return torch.stack([r.sum(1), r @ w], 1).reshape(-1)
 
 
 def check_same_batch(*tensors: torch.Tensor):
-    """Raise unless every rank holds the same global batch (inputs and targets: an
-    order-sensitive float64 checksum per tensor, all-reduced MAX of (s, -s)).  Without a
+    """Raise unless every rank holds the same global batch (inputs and targets): the
+    per-row fingerprints of every tensor, all-reduced as MAX of (v, -v), must agree
+    element by element (after one tiny all-reduce that checks the sizes agree).  Without a
     DistributedSampler the ranks must draw identical batches (same shuffle seed and
     augmentation RNG); a per-rank seed would otherwise train silently on overlapping
-    shards.  One tiny collective per call."""
+    shards.  Two tiny collectives per call."""
     _, ws = world()
     if ws <= 1:
         return
-    sums = [_batch_checksum(t) for t in tensors]
     dev = torch.device("cuda", torch.cuda.current_device()) \
         if dist.get_backend() == "nccl" else torch.device("cpu")
-    v = torch.tensor(sums + [-s for s in sums], dtype=torch.float64, device=dev)
+    fp = torch.cat([_batch_fingerprint(t).to(dev) for t in tensors])
+    n = torch.tensor([fp.numel(), -fp.numel()], dtype=torch.float64, device=dev)
+    dist.all_reduce(n, op=dist.ReduceOp.MAX)
+    if int(n[0]) != -int(n[1]):
+        raise RuntimeError(
+            f"ugpg data parallel: ranks drew batches of different sizes ({-int(n[1])} .. "
+            f"{int(n[0])} fingerprint values)")
+    v = torch.cat([fp, -fp])
     dist.all_reduce(v, op=dist.ReduceOp.MAX)
-    n = len(sums)
-    for i in range(n):
-        hi, lo = float(v[i]), -float(v[n + i])
-        if hi - lo > 1e-6 * max(1.0, abs(hi)):
-            raise RuntimeError(
-                "ugpg data parallel: ranks drew different global batches (checksums "
-                f"{lo!r} .. {hi!r}); seed the DataLoader / augmentation identically on every "
-                "rank or use a DistributedSampler")
+    hi, lo = v[:fp.numel()], -v[fp.numel():]
+    bad = (hi - lo) > 1e-9 * hi.abs().clamp_min(1.0)
+    if bool(bad.any()):
+        i = int(bad.nonzero()[0])
+        raise RuntimeError(
+            "ugpg data parallel: ranks drew different global batches (fingerprint value "
+            f"{i}: {float(lo[i])!r} .. {float(hi[i])!r}); seed the DataLoader / augmentation "
+            "identically on every rank or use a DistributedSampler")
 
 
 def shard_batch(loader, *tensors, check=False):

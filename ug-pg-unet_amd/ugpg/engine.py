@@ -151,13 +151,16 @@ def _bn_relu_wgrad(conv, bn, y, st, in_srcs, da, grads, part=None, route=None, n
     x6w = fold and all(s.C % 64 == 0 and s.y.dtype == torch.float32 for s in in_srcs)
     # the image layer's weight gradient (conv3x3_wgrad_img_kernel) forms it as well; its dy
     # has no other reader (in-process A/B -0.2 %, profiles/r5m_ab_step_folded_apply_img.txt)
+    # (only up to 3 real input channels: conv.hip's image-layer form, WGI_NCI; a 4-8 channel
+    # image padded to 8 takes the apply pass and the narrow-input weight gradient)
     img = fold and not pool and not need_dy and co == 64 and len(in_srcs) == 1 and in_srcs[0].C == 8 and \
-        in_srcs[0].scale is None and in_srcs[0].y.dtype == torch.float32
+        conv.weight.shape[1] <= 3 and in_srcs[0].scale is None and in_srcs[0].y.dtype == torch.float32
     if x6w or img:
         base = da if not pool or route[1] else None
         coef = ops.bn_relu_bwd(base, y, mean, invstd, scale, shift, None, grads.get(bn.weight),
                                grads.get(bn.bias), db, part=part)
-        dy = ops.empty(*y.shape, like=y) if x6w else None
+        # dy_out only when the data gradient reads it (no dead full-size write)
+        dy = ops.empty(*y.shape, like=y) if x6w and need_dy else None
         ci = conv.weight.shape[1]
         ops.conv3x3_wgrad(in_srcs, ops.BnLazyDy(base, y, mean, invstd, scale, shift, coef, dy,
                                                 pool=route[0][1:3] if pool else None),
