@@ -207,6 +207,19 @@ int ugpg_bn_finalize(const float* stats, int ntiles, int C, const float* gamma,
                      const float* beta, float* running_mean, float* running_var,
                      int64_t* num_batches_tracked, float momentum, float eps,
                      float* mean, float* invstd, float* scale, float* shift, void* stream);
+/* Synchronised BatchNorm across data-parallel ranks (SURVEY.md §8e's optional policy: the
+ * reference's train-mode BN normalises over the whole batch, UG_unet_parts.py:11,14, which
+ * a sharded batch only reproduces with a cross-rank exchange).  Forward:
+ * ugpg_bn_stats_pack merges this rank's tile partials into fp64 (N, mean, M2) per channel,
+ * out[3][C] (the caller places it in its rank's row of a zeroed [nranks][3][C] buffer and
+ * SUM-all-reduces it); ugpg_bn_finalize_merged merges the rows in rank order (Chan) and
+ * finalizes from the global statistics exactly as ugpg_bn_finalize does from tiles. */
+int ugpg_bn_stats_pack(const float* stats, int ntiles, int C, double* out, void* stream);
+int ugpg_bn_finalize_merged(const double* merged, int nranks, int C, const float* gamma,
+                            const float* beta, float* running_mean, float* running_var,
+                            int64_t* num_batches_tracked, float momentum, float eps,
+                            float* mean, float* invstd, float* scale, float* shift,
+                            void* stream);
 /* Eval: (scale, shift) from running stats (K5). */
 int ugpg_bn_eval_params(const float* gamma, const float* beta, const float* running_mean,
                         const float* running_var, float eps, int C, float* scale,
@@ -224,6 +237,19 @@ size_t ugpg_bn_relu_bwd_workspace(int64_t npix, int C);
  * dy == dy_bf16 == NULL the finalize only (dgamma, dbeta, dconv_bias, and the apply's
  * coefficients in the first 2*C floats of ws, for ugpg_wgrad_t.dy_bn). */
 size_t ugpg_bn_relu_bwd_partials_workspace(int C);
+/* Backward partials as a pass (when no producer wrote them): part [3][C][nslots]. */
+int ugpg_bn_relu_bwd_reduce(const float* da, const float* y_f32, const void* y_bf16,
+                            int64_t npix, int C, const float* mean, const float* invstd,
+                            const float* scale, const float* shift, float* part, int nslots,
+                            void* stream);
+/* Synchronised BatchNorm backward: ugpg_bn_bwd_partials_pack sums the slots per channel
+ * in fp64, out[3][C] = (sum g, sum g*xhat, sum xhat); after a SUM all-reduce,
+ * ugpg_bn_bwd_partials_unpack writes sums*scale (scale = 1/nranks) into slot 0 and zeroes
+ * the others, so the finalize above sees the global means (torch SyncBatchNorm's backward)
+ * and dgamma / dbeta / dconv_bias average to the global-batch gradient. */
+int ugpg_bn_bwd_partials_pack(const float* part, int nslots, int C, double* out, void* stream);
+int ugpg_bn_bwd_partials_unpack(const double* sums, double scale, float* part, int nslots,
+                                int C, void* stream);
 /* BatchNorm-backward partials folded into the kernel that last writes da (the pooling,
  * upsampling and head backward entries *_bnb): same partial layout, nslots from
  * ugpg_bnb_slots(npix, C) (0 for unsupported shapes). */

@@ -97,10 +97,70 @@ def state_spec(stage: int, in_channels: int, num_classes: int, key_prefix: str =
 # Forward building blocks
 # ---------------------------------------------------------------------------
 
+# Synchronised BatchNorm over data-parallel ranks (tests only: the CPU restatement of the
+# build's optional SyncBN, ugpg.dist.enable_sync_batchnorm): None, or an exchange object
+# with rank, nranks and all_reduce(t) (SUM, in place).
+BN_SYNC = None
+
+
+class _SyncBatchNorm(torch.autograd.Function):
+    """Train-mode BatchNorm2d over the GLOBAL batch of all ranks (torch SyncBatchNorm's
+    semantics; the reference's single-process BatchNorm2d over its whole batch,
+    UG_unet_parts.py:11,14).  Forward: per-rank fp64 (n, mean, M2), gathered by a SUM
+    all-reduce into rank rows, merged in rank order (Chan); biased variance for the
+    normalisation, unbiased for the running variance.  Backward: the local (sum g,
+    sum g*xhat) all-reduced, dy = w*invstd*(g - mean_all(g) - xhat*mean_all(g*xhat));
+    dgamma / dbeta are local sums (the gradient all-reduce averages them)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, rm, rv, sync):
+        C = x.shape[1]
+        xd = x.double()
+        n = xd.numel() // C
+        mu = xd.mean((0, 2, 3))
+        q = ((xd - mu.view(1, -1, 1, 1)) ** 2).sum((0, 2, 3))
+        g = torch.zeros(sync.nranks, 3, C, dtype=torch.float64)
+        g[sync.rank] = torch.stack([torch.full((C,), float(n), dtype=torch.float64), mu, q])
+        sync.all_reduce(g)
+        N = torch.zeros(C, dtype=torch.float64)
+        m = torch.zeros(C, dtype=torch.float64)
+        M2 = torch.zeros(C, dtype=torch.float64)
+        for r in range(sync.nranks):
+            nr, mr, qr = g[r]
+            Nt = N + nr
+            d = mr - m
+            m = m + d * (nr / Nt)
+            M2 = M2 + qr + d * d * (N * nr / Nt)
+            N = Nt
+        var = M2 / N
+        invstd = 1.0 / torch.sqrt(var + BN_EPS)
+        with torch.no_grad():
+            rm.mul_(1 - BN_MOMENTUM).add_((BN_MOMENTUM * m).to(rm.dtype))
+            rv.mul_(1 - BN_MOMENTUM).add_((BN_MOMENTUM * M2 / (N - 1)).to(rv.dtype))
+        xhat = ((xd - m.view(1, -1, 1, 1)) * invstd.view(1, -1, 1, 1)).to(x.dtype)
+        ctx.save_for_backward(xhat, invstd.to(x.dtype), w)
+        ctx.sync, ctx.N = sync, N
+        return xhat * w.view(1, -1, 1, 1) + b.view(1, -1, 1, 1)
+
+    @staticmethod
+    def backward(ctx, go):
+        xhat, invstd, w = ctx.saved_tensors
+        sg = go.double().sum((0, 2, 3))
+        sgx = (go.double() * xhat.double()).sum((0, 2, 3))
+        s = torch.stack([sg, sgx])
+        ctx.sync.all_reduce(s)
+        mg, mgx = (s[0] / ctx.N).to(go.dtype), (s[1] / ctx.N).to(go.dtype)
+        v = lambda t: t.view(1, -1, 1, 1)
+        dx = v(w * invstd) * (go - v(mg) - xhat * v(mgx))
+        return dx, sgx.to(go.dtype), sg.to(go.dtype), None, None, None
+
+
 def _bn(P, pre, x, training):
     rm, rv = P[pre + ".running_mean"], P[pre + ".running_var"]
     if training:
         P[pre + ".num_batches_tracked"].add_(1)
+        if BN_SYNC is not None:
+            return _SyncBatchNorm.apply(x, P[pre + ".weight"], P[pre + ".bias"], rm, rv, BN_SYNC)
     return F.batch_norm(x, rm, rv, P[pre + ".weight"], P[pre + ".bias"],
                         training, BN_MOMENTUM, BN_EPS)
 

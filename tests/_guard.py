@@ -55,14 +55,16 @@ def guarded(shape, dev, dtype=torch.float32, fill=None, pad=16384):
     return Guarded(tuple(shape), dev, dtype, pad, fill)
 
 
-def poison_cache(dev):
-    """NaN-fill what the caching allocator will hand out next: release the cache, then
-    allocate, fill and free one large block (later large allocations split it) and 256
-    small ones (the small pool's 2 MiB segments)."""
+def poison_cache(dev, value=float("nan")):
+    """Fill what the caching allocator will hand out next with `value`: release the cache,
+    then allocate, fill and free one large block (later large allocations split it) and 256
+    small ones (the small pool's 2 MiB segments).  NaN alone is not a complete poison --
+    fmaxf-based ReLU and max-pool drop it -- so tests run twice with two different fills
+    and require bit-identical results."""
     torch.cuda.synchronize(dev)
     torch.cuda.empty_cache()
     free, _ = torch.cuda.mem_get_info(dev)
-    big = torch.empty(int(min(free * 0.5, 16e9)) // 4, device=dev).fill_(float("nan"))
-    small = [torch.empty(1 << 17, device=dev).fill_(float("nan")) for _ in range(256)]
+    big = torch.empty(int(min(free * 0.5, 16e9)) // 4, device=dev).fill_(value)
+    small = [torch.empty(1 << 17, device=dev).fill_(value) for _ in range(256)]
     del big, small
     torch.cuda.synchronize(dev)

@@ -326,3 +326,69 @@ def test_allreduce_flat_run_plus_loose_tensors():
             got, want = torch.load(os.path.join(d, f"m{r}.pt"), weights_only=True)
             for a, b in zip(got, want):
                 assert torch.allclose(a, b, rtol=1e-6, atol=1e-6)
+
+
+def _syncbn_worker(rank, port, outdir):
+    """One rank of the synchronised-BatchNorm step: the oracle's Stage-1 train step on this
+    rank's bs2 shard with every BatchNorm synchronised through ugpg.dist's exchange (the
+    object ops._BN_SYNC holds when enable_sync_batchnorm is on), then the trainer's gradient
+    all-reduce (mean)."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "ug-pg-unet_amd")]
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    torch.set_num_threads(2)
+    from oracle import ref_cpu as O
+    from tests._parity import det_state, oracle_run, param_keys
+    from ugpg import ops
+    from ugpg.dist import allreduce_gradients, enable_sync_batchnorm, shard
+    enable_sync_batchnorm(True)
+    O.BN_SYNC = ops._BN_SYNC
+    assert (O.BN_SYNC.rank, O.BN_SYNC.nranks) == (rank, WORLD)
+    state = det_state(1, 3, 1)
+    x, t = _shards()
+    logits, final, _, g, P = oracle_run(1, state, shard(x, rank, WORLD), shard(t, rank, WORLD))
+    keys = param_keys(state)
+    params = [nn.Parameter(torch.zeros_like(g[k])) for k in keys]
+    for p, k in zip(params, keys):
+        p.grad = g[k].clone()
+    scale = allreduce_gradients(params, bucket_bytes=1 << 20)
+    bufs = {k: v for k, v in P.items() if k.endswith(("running_mean", "running_var"))}
+    torch.save({"logits": logits, "grads": {k: p.grad * scale for k, p in zip(keys, params)},
+                "bufs": bufs}, os.path.join(outdir, f"r{rank}.pt"))
+    enable_sync_batchnorm(False)
+    dist.destroy_process_group()
+
+
+def test_sync_batchnorm_step_equals_global_batch():
+    """SURVEY §8e's optional SyncBN: two gloo ranks on bs2 shards with
+    synchronised BatchNorm reproduce the single-process bs4 step of the reference (the
+    oracle, bit-identical to it): logits per shard, every averaged gradient within the §8d
+    rule (3x the reference's own fp32 noise floor + 1e-6 of scale), BN running statistics
+    1e-5 -- the exchange under test is ugpg.dist's own (_SyncBN.all_reduce)."""
+    from tests._parity import det_state, grad_check, noise_floor, oracle_run, param_keys
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_syncbn_worker, args=(_free_port(), d), nprocs=WORLD, join=True)
+        r = [torch.load(os.path.join(d, f"r{i}.pt"), weights_only=True) for i in range(WORLD)]
+    state = det_state(1, 3, 1)
+    x, t = _shards()
+    logits32, _, _, g32, P32 = oracle_run(1, state, x, t)
+    _, _, _, g64, _ = oracle_run(1, state, x, t, dtype=torch.float64)
+    floor = noise_floor(1, state, x, t, g32, g64)
+    lg = torch.cat([r[0]["logits"], r[1]["logits"]])
+    assert (lg - logits32).abs().max().item() <= 1e-4
+    bad = []
+    for k in param_keys(state):
+        assert torch.equal(r[0]["grads"][k], r[1]["grads"][k]), "replicas diverged"
+        ok, err, bound = grad_check(k, r[0]["grads"][k], g32[k], g64[k], floor[k])
+        if not ok:
+            bad.append(f"{k}: {err:.3e} > {bound:.3e}")
+    assert not bad, "synced gradients differ from the global-batch step:\n" + "\n".join(bad)
+    for k, v in r[0]["bufs"].items():
+        assert (v - P32[k]).abs().max().item() <= 1e-5 * max(1.0, P32[k].abs().max().item()), k
+        assert torch.equal(v, r[1]["bufs"][k]), k
+    # and local BatchNorm does NOT equal it (the test can tell the two policies apart)
+    la, _, _, _, _ = oracle_run(1, state, x[:B_PER], t[:B_PER])
+    assert (la - logits32[:B_PER]).abs().max().item() > 1e-3

@@ -158,3 +158,48 @@ def test_dp_two_ranks_bf16_exchange(tmp_path, exchange):
             assert not bad, "\n".join(bad[:20])
     finally:
         O.CONV_MATH = "f32"
+
+
+@pytest.mark.parametrize("stage,B,res", [(1, 4, 32), (4, 4, 64)])
+def test_sync_batchnorm_two_ranks_equal_global_batch(tmp_path, stage, B, res):
+    """SURVEY §8e's optional SyncBN on the HIP path: two GPU ranks on
+    bs B/2 shards with every BatchNorm synchronised (forward statistics gathered, backward
+    sums all-reduced: ugpg_bn_stats_pack / ugpg_bn_finalize_merged / ugpg_bn_bwd_partials_*)
+    reproduce the reference's single-process bs-B step: logits 1e-3, averaged gradients by
+    the §8d rule against the oracle's own noise floor, BN running statistics 1e-5."""
+    from tests._parity import noise_floor
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
+               WORLD_SIZE="2", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    procs = [subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "_syncbn_worker.py"),
+                               str(tmp_path), str(stage), str(B), str(res)],
+                              env=dict(env, RANK=str(r), LOCAL_RANK=str(r)), cwd=ROOT)
+             for r in range(2)]
+    try:
+        rcs = [p.wait(timeout=300) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert rcs == [0, 0], rcs
+    res_ = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(2)]
+    state = det_state(stage, 3, 1)
+    x = G.randn(1, (B, 3, res, res), "x")
+    t = G.bernoulli(2, (B, 1, res, res), 0.5, "t")
+    logits32, _, _, g32, P32 = oracle_run(stage, state, x, t)
+    _, _, _, g64, _ = oracle_run(stage, state, x, t, dtype=torch.float64)
+    floor = noise_floor(stage, state, x, t, g32, g64)
+    lg = torch.cat([res_[0]["logits"], res_[1]["logits"]])
+    assert (lg - logits32).abs().max().item() <= 1e-3
+    bad = []
+    for k in param_keys(state):
+        assert torch.equal(res_[0]["grads"][k], res_[1]["grads"][k]), f"replicas diverged: {k}"
+        ok, err, bound = grad_check(k, res_[0]["grads"][k], g32[k], g64[k], floor[k])
+        if not ok:
+            bad.append(f"{k}: {err:.3e} > {bound:.3e}")
+    assert not bad, "synced gradients differ from the global-batch step:\n" + "\n".join(bad[:20])
+    for k, v in res_[0]["bufs"].items():
+        assert torch.equal(v, res_[1]["bufs"][k]), k
+        if k.endswith("num_batches_tracked"):
+            assert int(v) == int(P32[k]), k
+        else:
+            assert (v - P32[k]).abs().max().item() <= 1e-5 * max(1.0, P32[k].abs().max().item()), k

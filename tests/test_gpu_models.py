@@ -35,11 +35,19 @@ def test_pgunet_train_step_parity(dev, stage, B, res, nc):
 @pytest.mark.parametrize("stage,B,res,nc", [(1, 4, 32, 2), (4, 2, 64, 1), (4, 2, 256, 1)])
 def test_train_step_reads_no_unwritten_memory(dev, stage, B, res, nc):
     """the same step with every allocation the caching allocator hands
-    out NaN-filled beforehand (tests/_guard.poison_cache), so a forward or backward kernel
-    that reads a workspace, partial slot or halo nobody wrote in this step fails
-    deterministically (NaN logits / gradients) instead of depending on what earlier work
-    left in that memory."""
-    _train_step_parity(dev, stage, B, res, nc, poison=True)
+    out pre-filled (tests/_guard.poison_cache), twice -- NaN, then -3e38 -- so a forward or
+    backward kernel that reads a workspace, partial slot or halo nobody wrote in this step
+    fails deterministically (the two runs differ, or NaN reaches the results) instead of
+    depending on what earlier work left in that memory; the first run also passes the full
+    parity checks."""
+    a = _train_step_parity(dev, stage, B, res, nc, poison=float("nan"))
+    b = _train_step_parity(dev, stage, B, res, nc, poison=-3e38, check=False)
+    for name, x, y in zip(("logits", "grads", "buffers"), a, b):
+        if isinstance(x, dict):
+            for k in x:
+                assert torch.equal(x[k], y[k]), f"{name} {k} depends on unwritten memory"
+        else:
+            assert torch.equal(x, y), f"{name} depend on unwritten memory"
 
 
 @pytest.mark.parametrize("cin", [4, 8])
@@ -51,7 +59,7 @@ def test_train_step_parity_image_channels_4_to_8(dev, cin):
     _train_step_parity(dev, 4, 2, 64, 1, cin=cin)
 
 
-def _train_step_parity(dev, stage, B, res, nc, poison=False, cin=3):
+def _train_step_parity(dev, stage, B, res, nc, poison=None, cin=3, check=True):
     from ugpg.loss import UncertaintyGuidedLoss
     import torch.nn as nn
     from tests._guard import poison_cache
@@ -62,8 +70,8 @@ def _train_step_parity(dev, stage, B, res, nc, poison=False, cin=3):
     _, final64, _, g64, _ = oracle_run(stage, state, x, t, dtype=torch.float64)
     floor = noise_floor(stage, state, x, t, g32, g64)
 
-    if poison:
-        poison_cache(dev)
+    if poison is not None:
+        poison_cache(dev, poison)
     m = build(stage, nc, state, dev, cin)
     out = m(x.to(dev))
     crit = nn.BCEWithLogitsLoss(pos_weight=torch.tensor([5.0], device=dev), reduction="none")
@@ -74,6 +82,10 @@ def _train_step_parity(dev, stage, B, res, nc, poison=False, cin=3):
     final.backward()
     assert torch.equal(out.detach(), lg_fwd), "the backward pass modified the forward's logits"
     assert all(torch.isfinite(p.grad).all() for p in m.parameters()), "non-finite gradient"
+    result = (out.detach().cpu(), {k: p.grad.cpu() for k, p in m.named_parameters()},
+              {k: v.cpu() for k, v in m.state_dict().items() if "running" in k})
+    if not check:
+        return result
     # forward logits and mask
     lg = out.detach().cpu()
     assert (lg - logits32).abs().max().item() <= LOGIT_TOL
@@ -97,6 +109,7 @@ def _train_step_parity(dev, stage, B, res, nc, poison=False, cin=3):
             assert (sd[k].cpu() - v).abs().max().item() <= 1e-5 * max(1.0, v.abs().max().item()), k
         if k.endswith("num_batches_tracked"):
             assert int(sd[k]) == int(v), k
+    return result
 
 
 def test_grads_are_one_flat_buffer(dev):
@@ -557,3 +570,35 @@ def test_progressive_unet_forward_with_input_gradient(dev):
         floor = max(floor, (gp.double() - g64).abs().max().item())
     err = (xd.grad.cpu().double() - g64).abs().max().item()
     assert err <= 3 * floor + 1e-6 * g64.abs().max().item(), (err, floor)
+
+
+def test_sync_batchnorm_kernels_at_world_size_one(dev):
+    """The synchronised-BatchNorm kernels in one process (the exchange is the identity):
+    the forward gather + rank-ordered merge reproduces the local finalize bit for bit
+    (logits, running statistics); the backward sums packed in fp64 and written back as one
+    slot change the gradients only by that slot's fp32 rounding."""
+    import torch.nn as nn
+    from ugpg.dist import enable_sync_batchnorm
+    from ugpg.loss import UncertaintyGuidedLoss
+    state = det_state(4, 3, 1)
+    x = G.randn(1, (2, 3, 64, 64), "x").to(dev)
+    t = G.bernoulli(2, (2, 1, 64, 64), 0.5, "t").to(dev)
+    res = []
+    for sync in (False, True):
+        enable_sync_batchnorm(sync)
+        try:
+            m = build(4, 1, state, dev)
+            out = m(x)
+            crit = nn.BCEWithLogitsLoss(pos_weight=torch.tensor([5.0], device=dev), reduction="none")
+            final, _ = UncertaintyGuidedLoss(dev).apply_uncertainty_weighted_loss(crit, out, t)
+            final.backward()
+            res.append((out.detach().clone(), {k: p.grad.clone() for k, p in m.named_parameters()},
+                        {k: v.clone() for k, v in m.state_dict().items() if "running" in k}))
+        finally:
+            enable_sync_batchnorm(False)
+    assert torch.equal(res[0][0], res[1][0])
+    for k, v in res[0][2].items():
+        assert torch.equal(v, res[1][2][k]), k
+    for k, g in res[0][1].items():
+        tol = 1e-5 if is_prebn_bias(k) else 1e-4 * max(g.abs().max().item(), 1e-30)
+        assert (g - res[1][1][k]).abs().max().item() <= tol, k

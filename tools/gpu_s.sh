@@ -1,0 +1,47 @@
+#!/bin/bash
+# One targeted GPU session (round 5): named steps, each under its own time limit, stopping
+# at the first crash / timeout / fault (exit > 1 for pytest; any nonzero otherwise).
+#   bash tools/gpu_s.sh TAG step [step ...]
+# steps:
+#   t:<file>[:<-k expr>]   pytest -m gpu on one test file (optionally -k)
+#   ab3v4                  same-box A/B: round-3 and round-4 final trees' bench, alternating
+#   bench[:args]           bench.py (default line, no CPU baseline) with extra args ('+' = space)
+#   prof[:args]            rocprofv3 --kernel-trace --stats of a short bench run
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=$1; shift
+mkdir -p gpurun_out
+run() {  # name seconds cmd...
+  local name=$1 sec=$2; shift 2
+  timeout -k 10 "$sec" "$@" > "gpurun_out/${TAG}_${name}.out" 2> "gpurun_out/${TAG}_${name}.err"
+  local rc=$?
+  echo "[$TAG] $name rc=$rc"; tail -4 "gpurun_out/${TAG}_${name}.out"
+  return $rc
+}
+for s in "$@"; do
+  case $s in
+    t:*)
+      IFS=: read -r _ f k <<< "$s"
+      n=$(basename "$f" .py)${k:+_k}
+      if [ -n "$k" ]; then
+        run "$n" 900 python -u -m pytest "tests/$f" -m gpu -x -q -rf -k "$k" --timeout 300 --timeout-method thread -p no:cacheprovider
+      else
+        run "$n" 900 python -u -m pytest "tests/$f" -m gpu -x -q -rf --timeout 300 --timeout-method thread -p no:cacheprovider
+      fi
+      rc=$?; [ $rc -gt 1 ] && exit $rc ;;
+    ab3v4)
+      for i in 1 2 3; do
+        for t in r3 r4; do
+          run "ab_${t}_$i" 300 python exp/${t}tree/bench.py --steps 20 --warmup 5 --no-cpu-baseline || exit $?
+        done
+      done ;;
+    bench*)
+      a=${s#bench}; a=${a#:}; a=${a//+/ }
+      run "bench${a// /}" 600 python bench.py --no-cpu-baseline $a || exit $? ;;
+    prof*)
+      a=${s#prof}; a=${a#:}; a=${a//+/ }
+      run "prof${a// /}" 600 rocprofv3 --kernel-trace --stats -d "gpurun_out/prof_${TAG}${a// /}" -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline $a || exit $? ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+exit 0

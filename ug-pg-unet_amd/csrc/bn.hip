@@ -15,16 +15,13 @@
 
 namespace ugpg {
 
-__global__ void bn_finalize_kernel(const float* __restrict__ stats, int ntiles, int C,
-                                   const float* gamma, const float* beta, float* rmean,
-                                   float* rvar, int64_t* nbt, float momentum, float eps,
-                                   float* mean_o, float* invstd_o, float* scale_o,
-                                   float* shift_o) {
-    // Parallel-variance combination of the per-tile partials (count, sum, M2) in ONE
-    // pass, shifted by K = the first non-empty tile's mean (close to the global mean, so
-    // no cancellation): with e_t = sum_t - n_t K,  m = K + sum e_t / N  and
-    // M2 = sum M2_t + sum e_t^2 / n_t - (sum e_t)^2 / N.  1024 threads per channel.
-    const int c = blockIdx.x;
+// Parallel-variance combination of one channel's per-tile partials (count, sum, M2) in ONE
+// pass, shifted by K = the first non-empty tile's mean (close to the global mean, so no
+// cancellation): with e_t = sum_t - n_t K,  m = K + sum e_t / N  and
+// M2 = sum M2_t + sum e_t^2 / n_t - (sum e_t)^2 / N.  Whole block per channel; the result
+// (N, mean, M2) is valid in thread 0.
+__device__ __forceinline__ void bn_merge_tiles(const float* __restrict__ stats, int ntiles, int C,
+                                               int c, double& N_o, double& mean_o, double& M2_o) {
     __shared__ double sn[16], se[16], sq[16];
     const float* cnt = stats + (size_t)c * ntiles;
     const float* sum = stats + ((size_t)C + c) * ntiles;
@@ -66,32 +63,91 @@ __global__ void bn_finalize_kernel(const float* __restrict__ stats, int ntiles, 
         sq[wv] = M;
     }
     __syncthreads();
-    if (threadIdx.x == 0)
+    if (threadIdx.x == 0) {
         for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
             sn[0] += sn[w];
             se[0] += se[w];
             sq[0] += sq[w];
         }
-    const double Ntot = sn[0];
-    const double mean = Ntot > 0 ? K + se[0] / Ntot : 0.0;
-    if (threadIdx.x == 0 && Ntot > 0) sq[0] -= se[0] * se[0] / Ntot;
-    if (threadIdx.x == 0) {
-        const double N = Ntot, m = mean;
-        const double var = sq[0] / N;
-        const float inv = (float)(1.0 / sqrt(var + (double)eps));
-        const float mf = (float)m;
-        const float sc = inv * gamma[c];
-        mean_o[c] = mf;
-        invstd_o[c] = inv;
-        scale_o[c] = sc;
-        shift_o[c] = beta[c] - mf * sc;
-        if (rmean) {
-            const double unbiased = N > 1 ? sq[0] / (N - 1) : sq[0];
-            rmean[c] = (float)(momentum * m + (1.0 - momentum) * (double)rmean[c]);
-            rvar[c] = (float)(momentum * unbiased + (1.0 - momentum) * (double)rvar[c]);
-        }
-        if (c == 0 && nbt) *nbt += 1;
+        const double Ntot = sn[0];
+        N_o = Ntot;
+        mean_o = Ntot > 0 ? K + se[0] / Ntot : 0.0;
+        M2_o = Ntot > 0 ? sq[0] - se[0] * se[0] / Ntot : sq[0];
     }
+}
+
+// mean/invstd/scale/shift and the running statistics (unbiased variance) of one channel
+// from its merged (N, mean, M2)
+__device__ __forceinline__ void bn_finalize_channel(int c, double N, double m, double M2,
+                                                    const float* gamma, const float* beta,
+                                                    float* rmean, float* rvar, int64_t* nbt,
+                                                    float momentum, float eps, float* mean_o,
+                                                    float* invstd_o, float* scale_o, float* shift_o) {
+    const double var = M2 / N;
+    const float inv = (float)(1.0 / sqrt(var + (double)eps));
+    const float mf = (float)m;
+    const float sc = inv * gamma[c];
+    mean_o[c] = mf;
+    invstd_o[c] = inv;
+    scale_o[c] = sc;
+    shift_o[c] = beta[c] - mf * sc;
+    if (rmean) {
+        const double unbiased = N > 1 ? M2 / (N - 1) : M2;
+        rmean[c] = (float)(momentum * m + (1.0 - momentum) * (double)rmean[c]);
+        rvar[c] = (float)(momentum * unbiased + (1.0 - momentum) * (double)rvar[c]);
+    }
+    if (c == 0 && nbt) *nbt += 1;
+}
+
+__global__ void bn_finalize_kernel(const float* __restrict__ stats, int ntiles, int C,
+                                   const float* gamma, const float* beta, float* rmean,
+                                   float* rvar, int64_t* nbt, float momentum, float eps,
+                                   float* mean_o, float* invstd_o, float* scale_o,
+                                   float* shift_o) {
+    const int c = blockIdx.x;
+    double N, m, M2;
+    bn_merge_tiles(stats, ntiles, C, c, N, m, M2);
+    if (threadIdx.x == 0)
+        bn_finalize_channel(c, N, m, M2, gamma, beta, rmean, rvar, nbt, momentum, eps, mean_o,
+                            invstd_o, scale_o, shift_o);
+}
+
+// ---- synchronised BatchNorm across data-parallel ranks (SURVEY §8e's optional policy) ----
+// Forward: each rank merges its tiles into (N, mean, M2) in fp64 and writes them into its own
+// row of a zeroed [nranks][3][C] buffer; a SUM all-reduce of that buffer is an exact gather
+// (every other row is zero); every rank then merges the rows in rank order (Chan) -- the
+// same bits on every rank -- and finalizes from the global statistics.
+__global__ void bn_stats_pack_kernel(const float* __restrict__ stats, int ntiles, int C,
+                                     double* out) {
+    const int c = blockIdx.x;
+    double N, m, M2;
+    bn_merge_tiles(stats, ntiles, C, c, N, m, M2);
+    if (threadIdx.x == 0) {
+        out[c] = N;
+        out[C + c] = m;
+        out[2 * C + c] = M2;
+    }
+}
+
+__global__ void bn_finalize_merged_kernel(const double* __restrict__ g, int nranks, int C,
+                                          const float* gamma, const float* beta, float* rmean,
+                                          float* rvar, int64_t* nbt, float momentum, float eps,
+                                          float* mean_o, float* invstd_o, float* scale_o,
+                                          float* shift_o) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double N = 0, m = 0, M2 = 0;
+    for (int r = 0; r < nranks; ++r) {
+        const double* row = g + (size_t)r * 3 * C;
+        const double nr = row[c], mr = row[C + c], qr = row[2 * C + c];
+        if (!(nr > 0)) continue;
+        const double Nt = N + nr, d = mr - m;
+        m += d * (nr / Nt);
+        M2 += qr + d * d * (N * nr / Nt);
+        N = Nt;
+    }
+    bn_finalize_channel(c, N, m, M2, gamma, beta, rmean, rvar, nbt, momentum, eps, mean_o, invstd_o,
+                        scale_o, shift_o);
 }
 
 __global__ void bn_eval_params_kernel(const float* gamma, const float* beta, const float* rm,
@@ -167,10 +223,10 @@ __global__ void __launch_bounds__(256)
     }
 }
 
-__global__ void bn_bwd_finalize_kernel(const float* part, int nblk, int C, int64_t npix,
-                                       const float* scale, float* dgamma, float* dbeta,
-                                       float* dbias, int acc, float* coef) {
-    const int c = blockIdx.x;
+// one channel's backward partials (sum g, sum g*xhat, sum xhat) over its slots in fp64,
+// fixed order; valid in thread 0
+__device__ __forceinline__ void bn_bwd_sum_slots(const float* part, int nblk, int C, int c,
+                                                 double& a_o, double& b_o, double& x_o) {
     __shared__ double s1[4], s2[4], s3[4];
     double a = 0, b = 0, x = 0;
     int i = threadIdx.x;
@@ -206,24 +262,63 @@ __global__ void bn_bwd_finalize_kernel(const float* part, int nblk, int C, int64
         s3[wv] = x;
     }
     __syncthreads();
-    if (threadIdx.x == 0)
+    if (threadIdx.x == 0) {
         for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
             s1[0] += s1[w];
             s2[0] += s2[w];
             s3[0] += s3[w];
         }
+        a_o = s1[0];
+        b_o = s2[0];
+        x_o = s3[0];
+    }
+}
+
+__global__ void bn_bwd_finalize_kernel(const float* part, int nblk, int C, int64_t npix,
+                                       const float* scale, float* dgamma, float* dbeta,
+                                       float* dbias, int acc, float* coef) {
+    const int c = blockIdx.x;
+    double A, Bs, X;
+    bn_bwd_sum_slots(part, nblk, C, c, A, Bs, X);
     if (threadIdx.x == 0) {
-        const float sg = (float)s1[0], sgx = (float)s2[0];
+        const float sg = (float)A, sgx = (float)Bs;
         if (dgamma) dgamma[c] = acc ? dgamma[c] + sgx : sgx;
         if (dbeta) dbeta[c] = acc ? dbeta[c] + sg : sg;
-        const double mg = s1[0] / (double)npix, mgx = s2[0] / (double)npix;
+        const double mg = A / (double)npix, mgx = Bs / (double)npix;
         coef[c] = (float)mg;         // mean(g)
         coef[C + c] = (float)mgx;    // mean(g*xhat)
         if (dbias) {
             // sum_p dy_p = scale*(sum g - N*mean(g) - mean(g*xhat)*sum xhat)
-            const float db = (float)((double)scale[c] * (s1[0] - (double)npix * mg - mgx * s3[0]));
+            const float db = (float)((double)scale[c] * (A - (double)npix * mg - mgx * X));
             dbias[c] = acc ? dbias[c] + db : db;
         }
+    }
+}
+
+// Backward of the synchronised BatchNorm: each rank's (sum g, sum g*xhat, sum xhat) in fp64
+// are SUM all-reduced, then written back as ONE slot holding sum/nranks (the other slots
+// zeroed), so the unchanged finalize computes mean(g) = sum_all / (nranks * npix_local) --
+// the global means, as torch's SyncBatchNorm backward -- while dgamma, dbeta and the conv
+// bias gradient become the global sums / nranks, whose average over ranks (the gradient
+// all-reduce) is the global-batch gradient of the local-loss average.
+__global__ void bn_bwd_pack_kernel(const float* part, int nblk, int C, double* out) {
+    const int c = blockIdx.x;
+    double A, Bs, X;
+    bn_bwd_sum_slots(part, nblk, C, c, A, Bs, X);
+    if (threadIdx.x == 0) {
+        out[c] = A;
+        out[C + c] = Bs;
+        out[2 * C + c] = X;
+    }
+}
+
+__global__ void bn_bwd_unpack_kernel(const double* __restrict__ sums, double scale, float* part,
+                                     int nblk, int C) {
+    const int64_t n = (int64_t)3 * C * nblk;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t row = i / nblk, slot = i - row * nblk;
+        part[i] = slot == 0 ? (float)(sums[row] * scale) : 0.f;
     }
 }
 
@@ -479,6 +574,13 @@ BwdPlan bwd_plan(int64_t npix, int C) {
 
 using namespace ugpg;
 
+// threads per channel of the forward merge: one per PF = 8 slots, 64..1024
+static int fwd_fin_threads(int ntiles) {
+    int nt = 64;
+    while (nt < 1024 && (int64_t)nt * 8 < ntiles) nt *= 2;
+    return nt;
+}
+
 extern "C" int ugpg_bn_finalize(const float* stats, int ntiles, int C, const float* gamma,
                                 const float* beta, float* running_mean, float* running_var,
                                 int64_t* nbt, float momentum, float eps, float* mean,
@@ -490,12 +592,37 @@ extern "C" int ugpg_bn_finalize(const float* stats, int ntiles, int C, const flo
     }
     // threads per channel: one per PF = 8 slots, 64..1024 -- the narrow-image layers have
     // 128-512 slots, and 1024-thread blocks of mostly idle lanes cost them ~4 us a launch
-    int nt = 64;
-    while (nt < 1024 && (int64_t)nt * 8 < ntiles) nt *= 2;
+    const int nt = fwd_fin_threads(ntiles);
     hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(nt), 0, as_stream(stream), stats,
                        ntiles, C, gamma, beta, running_mean, running_var, nbt, momentum, eps,
                        mean, invstd, scale, shift);
     return check_launch("bn_finalize");
+}
+
+extern "C" int ugpg_bn_stats_pack(const float* stats, int ntiles, int C, double* out,
+                                  void* stream) {
+    if (!stats || !out || C <= 0 || ntiles <= 0) {
+        set_error("bn_stats_pack: bad arguments");
+        return UGPG_ERR_INVALID;
+    }
+    hipLaunchKernelGGL(bn_stats_pack_kernel, dim3(C), dim3(fwd_fin_threads(ntiles)), 0,
+                       as_stream(stream), stats, ntiles, C, out);
+    return check_launch("bn_stats_pack");
+}
+
+extern "C" int ugpg_bn_finalize_merged(const double* merged, int nranks, int C, const float* gamma,
+                                       const float* beta, float* running_mean, float* running_var,
+                                       int64_t* nbt, float momentum, float eps, float* mean,
+                                       float* invstd, float* scale, float* shift, void* stream) {
+    if (!merged || nranks <= 0 || !gamma || !beta || !mean || !invstd || !scale || !shift ||
+        C <= 0 || (!running_mean != !running_var)) {
+        set_error("bn_finalize_merged: bad arguments");
+        return UGPG_ERR_INVALID;
+    }
+    hipLaunchKernelGGL(bn_finalize_merged_kernel, dim3(cdiv(C, 256)), dim3(256), 0,
+                       as_stream(stream), merged, nranks, C, gamma, beta, running_mean, running_var,
+                       nbt, momentum, eps, mean, invstd, scale, shift);
+    return check_launch("bn_finalize_merged");
 }
 
 extern "C" int ugpg_bn_eval_params(const float* gamma, const float* beta, const float* rm,
@@ -563,6 +690,44 @@ void launch_bn_bwd_reduce(const float* da, YRef y, int64_t npix, int C, const fl
 extern "C" int ugpg_bnb_slots(int64_t npix, int C) {
     if (npix <= 0 || C <= 0 || C % 4 || C > 1024) return 0;
     return bwd_plan(npix, C).nblk;
+}
+
+extern "C" int ugpg_bn_relu_bwd_reduce(const float* da, const float* y_f32, const void* y_bf16,
+                                       int64_t npix, int C, const float* mean, const float* invstd,
+                                       const float* scale, const float* shift, float* part,
+                                       int nslots, void* stream) {
+    const YRef y = yref(y_f32, y_bf16);
+    if (!da || (!y.f && !y.h) || !mean || !invstd || !scale || !shift || !part || nslots <= 0 ||
+        C % 4 || C <= 0 || C > 1024 || npix <= 0) {
+        set_error("bn_relu_bwd_reduce: bad arguments (C=%d nslots=%d)", C, nslots);
+        return UGPG_ERR_INVALID;
+    }
+    launch_bn_bwd_reduce(da, y, npix, C, mean, invstd, scale, shift, part, nslots,
+                         as_stream(stream));
+    return check_launch("bn_bwd_reduce");
+}
+
+extern "C" int ugpg_bn_bwd_partials_pack(const float* part, int nslots, int C, double* out,
+                                         void* stream) {
+    if (!part || !out || nslots <= 0 || C <= 0) {
+        set_error("bn_bwd_partials_pack: bad arguments");
+        return UGPG_ERR_INVALID;
+    }
+    hipLaunchKernelGGL(bn_bwd_pack_kernel, dim3(C), dim3(bwd_fin_threads(nslots)), 0,
+                       as_stream(stream), part, nslots, C, out);
+    return check_launch("bn_bwd_partials_pack");
+}
+
+extern "C" int ugpg_bn_bwd_partials_unpack(const double* sums, double scale, float* part,
+                                           int nslots, int C, void* stream) {
+    if (!sums || !part || nslots <= 0 || C <= 0) {
+        set_error("bn_bwd_partials_unpack: bad arguments");
+        return UGPG_ERR_INVALID;
+    }
+    const int64_t n = (int64_t)3 * C * nslots;
+    hipLaunchKernelGGL(bn_bwd_unpack_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 1024)),
+                       dim3(256), 0, as_stream(stream), sums, scale, part, nslots, C);
+    return check_launch("bn_bwd_partials_unpack");
 }
 
 extern "C" size_t ugpg_bn_relu_bwd_partials_workspace(int C) {

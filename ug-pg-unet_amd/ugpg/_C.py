@@ -73,6 +73,11 @@ SIGNATURES = {
     "ugpg_conv3x3_wgrad_workspace": (_sz, [C.POINTER(WgradDesc)]),
     "ugpg_conv3x3_wgrad": (_i, [C.POINTER(WgradDesc), _p, _sz, _p]),
     "ugpg_bn_finalize": (_i, [_p, _i, _i, _p, _p, _p, _p, _p, _f, _f, _p, _p, _p, _p, _p]),
+    "ugpg_bn_stats_pack": (_i, [_p, _i, _i, _p, _p]),
+    "ugpg_bn_finalize_merged": (_i, [_p, _i, _i, _p, _p, _p, _p, _p, _f, _f, _p, _p, _p, _p, _p]),
+    "ugpg_bn_relu_bwd_reduce": (_i, [_p, _p, _p, _i64, _i, _p, _p, _p, _p, _p, _i, _p]),
+    "ugpg_bn_bwd_partials_pack": (_i, [_p, _i, _i, _p, _p]),
+    "ugpg_bn_bwd_partials_unpack": (_i, [_p, C.c_double, _p, _i, _i, _p]),
     "ugpg_bn_eval_params": (_i, [_p, _p, _p, _p, _f, _i, _p, _p, _p]),
     "ugpg_bn_relu_bwd_workspace": (_sz, [_i64, _i]),
     "ugpg_bn_relu_bwd": (_i, [_p, _p, _p, _i64, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _p,

@@ -7,8 +7,9 @@ produces it back to front, so as soon as every gradient above an offset is final
 the bucket below the previous watermark is handed to RCCL (async, on its own
 stream) while the remaining backward kernels run (OverlapReducer).
 
-BatchNorm stays local to each rank (each rank's forward equals the reference's
-bs-16 forward on its shard); gradients are summed and the 1/world_size average
+BatchNorm stays local to each rank by default (each rank's forward equals the
+reference's bs-16 forward on its shard); enable_sync_batchnorm / UGPG_SYNC_BN=1 makes it
+normalise over the global batch instead (SURVEY §8e's optional SyncBN).  Gradients are summed and the 1/world_size average
 is folded into the RMSprop kernel (``RMSprop.grad_scale``).  Everything here is
 device-agnostic so the same code path is exercised with the ``gloo`` backend on
 CPU in the test-suite.
@@ -41,6 +42,49 @@ def init_from_env(backend: str | None = None):
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
     dist.init_process_group(backend=backend)
     return world()
+
+
+class _SyncBN:
+    """The exchange of synchronised BatchNorm (ops._BN_SYNC): SUM all-reduces, in place and
+    stream-ordered, through torch.distributed (RCCL under "nccl") or libugpg's communicator
+    (UGPG_COMM=native).  At world size 1 (forced) the exchange is the identity."""
+
+    def __init__(self):
+        self.rank, self.nranks = world()
+
+    def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+        if self.nranks > 1:
+            comm = native_comm() if t.is_cuda else None
+            if comm is not None:
+                comm.all_reduce(t)
+            else:
+                dist.all_reduce(t)
+        return t
+
+
+def enable_sync_batchnorm(flag: bool = True) -> None:
+    """Synchronised BatchNorm (SURVEY §8e's optional policy; default off = local BatchNorm):
+    every train-mode BatchNorm of every ugpg model normalises over the GLOBAL batch, as the
+    reference's single-process BatchNorm2d does over its whole batch (UG_unet_parts.py:11,
+    14), at the cost of two small collectives per BatchNorm per step (forward statistics,
+    backward sums).  COLLECTIVE: enable it on every rank (UGPG_SYNC_BN=1 makes the trainers
+    do so)."""
+    from . import ops
+    ops._BN_SYNC = _SyncBN() if flag else None
+
+
+def sync_batchnorm_enabled() -> bool:
+    from . import ops
+    return ops._BN_SYNC is not None
+
+
+def sync_batchnorm_from_env() -> None:
+    """UGPG_SYNC_BN=1: synchronised BatchNorm under data parallelism (the trainers call
+    this at construction); UGPG_SYNC_BN=force also at world size 1 (the kernels run, the
+    exchange is the identity: for measuring their cost on one GPU)."""
+    v = os.environ.get("UGPG_SYNC_BN", "0")
+    if v == "force" or (v == "1" and world()[1] > 1):
+        enable_sync_batchnorm(True)
 
 
 def shard(batch: torch.Tensor, rank: int, world_size: int) -> torch.Tensor:

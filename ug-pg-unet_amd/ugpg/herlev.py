@@ -33,7 +33,8 @@ from . import ops
 from .flat import ensure_flat
 from .loss import UncertaintyGuidedLoss
 from .dist import (allreduce_gradients, allreduce_metrics, broadcast_buffers,
-                   broadcast_parameters, overlapped_allreduce, shard_batch, world)
+                   broadcast_parameters, overlapped_allreduce, shard_batch,
+                   sync_batchnorm_from_env, world)
 from .optim import Adam
 from .unet import STAGE_CLASSES, STAGE_RESOLUTIONS, _LAYOUT
 
@@ -205,6 +206,7 @@ class HerlevTrainer:
         self.history = {k: [] for k in ("train_loss", "val_loss", "train_acc", "val_acc",
                                         "uncertainty_weights_mean", "uncertainty_weights_std",
                                         "base_loss", "stage_transitions")}
+        sync_batchnorm_from_env()
         if world()[1] > 1:  # data parallel: every replica starts from rank 0's weights
             for m in self.models.values():
                 broadcast_parameters(m)

@@ -343,12 +343,32 @@ def conv3x3_wgrad(srcs, dy, dw, db, cin_real, accumulate=0, flops=None):
 
 
 # ------------------------------------------------------------------ BN
+# Synchronised BatchNorm across data-parallel ranks (ugpg.dist.enable_sync_batchnorm): None
+# (local BatchNorm, the default), or an object with `rank`, `nranks` and `all_reduce(t)`
+# (SUM, in place, ordered on the current stream).  Every train-mode BatchNorm then
+# normalises over the global batch: its forward statistics are gathered before the
+# finalize, its backward sums all-reduced before the backward finalize.
+_BN_SYNC = None
+
+
 def bn_finalize(stats, ntiles, gamma, beta, rm, rv, nbt, momentum, eps):
     c = gamma.numel()
     mean, invstd, scale, shift = (empty(c, like=gamma) for _ in range(4))
-    check(lib.ugpg_bn_finalize(ptr(stats), ntiles, c, _f32(gamma), _f32(beta), ptr(rm), ptr(rv),
-                               ptr(nbt), momentum, eps, ptr(mean), ptr(invstd), ptr(scale),
-                               ptr(shift), stream()), "bn_finalize")
+    sync = _BN_SYNC
+    if sync is not None:
+        # this rank's (N, mean, M2) per channel in its row of a zeroed [nranks][3][C] fp64
+        # buffer; the SUM all-reduce is an exact gather; every rank merges the rows in order
+        g = torch.zeros(sync.nranks, 3, c, dtype=torch.float64, device=stats.device)
+        check(lib.ugpg_bn_stats_pack(ptr(stats), ntiles, c, ptr(g[sync.rank]), stream()),
+              "bn_stats_pack")
+        sync.all_reduce(g)
+        check(lib.ugpg_bn_finalize_merged(ptr(g), sync.nranks, c, _f32(gamma), _f32(beta), ptr(rm),
+                                          ptr(rv), ptr(nbt), momentum, eps, ptr(mean), ptr(invstd),
+                                          ptr(scale), ptr(shift), stream()), "bn_finalize_merged")
+    else:
+        check(lib.ugpg_bn_finalize(ptr(stats), ntiles, c, _f32(gamma), _f32(beta), ptr(rm), ptr(rv),
+                                   ptr(nbt), momentum, eps, ptr(mean), ptr(invstd), ptr(scale),
+                                   ptr(shift), stream()), "bn_finalize")
     if rm is not None:
         weights_written([rm, rv])  # running stats updated in place (eval-param cache keys)
     return mean, invstd, scale, shift
@@ -385,6 +405,21 @@ def bn_relu_bwd(da, y, mean, invstd, scale, shift, dy, dgamma, dbeta, dconv_bias
     head_bwd(defer=True); the apply adds its gradient to da (da None: nothing to add)."""
     c = y.shape[-1]
     npix = y.numel() // c
+    sync = _BN_SYNC
+    if sync is not None:
+        if part is None:  # no producer wrote the partials: the reduction as a pass
+            part = empty(3 * c * lib.ugpg_bnb_slots(npix, c), like=y, dtype=F32)
+            check(lib.ugpg_bn_relu_bwd_reduce(ptr(da), *_yargs(y), npix, c, ptr(mean), ptr(invstd),
+                                              ptr(scale), ptr(shift), ptr(part),
+                                              part.numel() // (3 * c), stream()), "bn_relu_bwd_reduce")
+        # (sum g, sum g*xhat, sum xhat) summed over ranks, written back as one slot / nranks
+        sums = empty(3 * c, like=y, dtype=torch.float64)
+        nslots = part.numel() // (3 * c)
+        check(lib.ugpg_bn_bwd_partials_pack(ptr(part), nslots, c, ptr(sums), stream()),
+              "bn_bwd_partials_pack")
+        sync.all_reduce(sums)
+        check(lib.ugpg_bn_bwd_partials_unpack(ptr(sums), 1.0 / sync.nranks, ptr(part), nslots, c,
+                                              stream()), "bn_bwd_partials_unpack")
     if route is not None:
         if route[0] == "pool":
             _, dout, am, H, W = route

@@ -20,7 +20,8 @@ import torch.nn as nn
 
 from . import ops
 from .dist import (allreduce_gradients, allreduce_metrics, broadcast_buffers,
-                   broadcast_parameters, overlapped_allreduce, shard_batch, world)
+                   broadcast_parameters, overlapped_allreduce, shard_batch,
+                   sync_batchnorm_from_env, world)
 from .loss import UncertaintyGuidedLoss, weighted_loss_tensors
 from .optim import RMSprop
 from .unet import PGUNet1, PGUNet2, PGUNet3, PGUNet4, ProgressiveUNet
@@ -79,6 +80,7 @@ class UncertaintyGuidedProgressiveTrainer:
         self.history = {k: [] for k in ("train_loss", "val_loss", "train_dice", "val_dice",
                                         "uncertainty_weights_mean", "uncertainty_weights_std",
                                         "base_loss", "stage_transitions")}
+        sync_batchnorm_from_env()
         self.sync_replicas()
 
     # ------------------------------------------------------------ data parallel
