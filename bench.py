@@ -220,7 +220,7 @@ def main():
     import torch.distributed as dist
     import ugpg
     from ugpg import ops
-    from ugpg.dist import init_from_env, max_over_ranks
+    from ugpg.dist import init_from_env, max_over_ranks, sync_batchnorm_enabled
     from ugpg.trainer import MetricsReadback
 
     ops.set_conv_math(args.conv_math)
@@ -327,6 +327,7 @@ def main():
                                "PGUNet3 eval fwd 128^2 (U-map) + weighted BCE + RMSprop",
                    "per_gpu_batch": B, "global_batch": B * world, "resolution": R,
                    "parallelism": f"dp{world}",
+                   "batchnorm": "sync (global batch)" if sync_batchnorm_enabled() else "local (per rank)",
                    "baseline_config": ("BASELINE.json configs[2] arithmetic (bf16 conv operands, "
                                        "fp32 accumulation, bf16 activation storage)" if args.conv_math == "bf16"
                                        else "BASELINE.json configs[1]")},

@@ -7,6 +7,8 @@
 #   ab3v4                  same-box A/B: round-3 and round-4 final trees' bench, alternating
 #   bench[:args]           bench.py (default line, no CPU baseline) with extra args ('+' = space)
 #   prof[:args]            rocprofv3 --kernel-trace --stats of a short bench run
+#   cb:<args>              tools/conv_bench.py with args ('+' = space)
+#   env:VAR=VAL / unenv:VAR   set / unset an environment variable for the following steps
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=$1; shift
@@ -37,10 +39,15 @@ for s in "$@"; do
       done ;;
     bench*)
       a=${s#bench}; a=${a#:}; a=${a//+/ }
-      run "bench${a// /}" 600 python bench.py --no-cpu-baseline $a || exit $? ;;
+      nb=$((nb+1)); run "bench${nb}" 600 python bench.py --no-cpu-baseline $a || exit $? ;;
     prof*)
       a=${s#prof}; a=${a#:}; a=${a//+/ }
       run "prof${a// /}" 600 rocprofv3 --kernel-trace --stats -d "gpurun_out/prof_${TAG}${a// /}" -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline $a || exit $? ;;
+    cb:*)
+      a=${s#cb:}; a=${a//+/ }
+      nc=$((nc+1)); run "convbench${nc}" 600 python tools/conv_bench.py $a || exit $? ;;
+    env:*) export "${s#env:}"; echo "[$TAG] export ${s#env:}" ;;
+    unenv:*) unset "${s#unenv:}" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
