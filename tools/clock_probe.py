@@ -64,7 +64,7 @@ def main():
                 torch.cuda.synchronize()
                 n += 20
             dt = (time.perf_counter() - t0) / n
-            v = (ctypes.c_double * 11)()
+            v = (ctypes.c_double * 14)()
             nwg = fn(v)
             if not a.stamps:
                 what = f"clock {v[0]:.0f} MHz"
@@ -74,7 +74,9 @@ def main():
                 what = ("loader vm_wait/barrier per phase " + " ".join(
                     f"p{q}:{v[q]:.1%}/{v[3 + q]:.1%}" for q in range(3)) +
                     f" | compute barrier {v[6]:.1%} epilogue {v[7]:.1%}, {v[8]:.0f} cyc/step;"
-                    f" last epilogue: stores {v[9]:.0f} stats {v[10]:.0f} cyc")
+                    f" last epilogue: stores {v[9]:.0f} stats {v[10]:.0f} cyc;"
+                    f" loader work: halo stores {v[11]:.1%} row DMAs {v[12]:.1%}"
+                    f" halo loads+cursors {v[13]:.1%}")
             print(f"{name}: {dt*1e3:.3f} ms/launch {flops/dt/1e12:.0f} TF  {what} "
                   f"(median of {nwg} workgroups)", flush=True)
 

@@ -7,6 +7,7 @@
 #   ab3v4                  same-box A/B: round-3 and round-4 final trees' bench, alternating
 #   bench[:args]           bench.py (default line, no CPU baseline) with extra args ('+' = space)
 #   prof[:args]            rocprofv3 --kernel-trace --stats of a short bench run
+#   stamps:<x6|bf16>       in-kernel stamps (exp/lib_stamp.so) of five layers
 #   cb:<args>              tools/conv_bench.py with args ('+' = space)
 #   env:VAR=VAL / unenv:VAR   set / unset an environment variable for the following steps
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -46,6 +47,9 @@ for s in "$@"; do
     cb:*)
       a=${s#cb:}; a=${a//+/ }
       nc=$((nc+1)); run "convbench${nc}" 600 python tools/conv_bench.py $a || exit $? ;;
+    stamps:*)  # in-kernel loader/compute stamps of exp/lib_stamp.so (-D X6R_STAMP=1), math x6 or bf16
+      m=${s#stamps:}; ns=$((ns+1))
+      run "stamps${ns}_$m" 300 env UGPG_LIB=exp/lib_stamp.so python tools/clock_probe.py --stamps --seconds 1 --math $m $( [ "$m" = bf16 ] && echo --out16 ) --layers inc.3,down1.3,down2.3,down3.3,up4.0 || exit $? ;;
     env:*) export "${s#env:}"; echo "[$TAG] export ${s#env:}" ;;
     unenv:*) unset "${s#unenv:}" ;;
     *) echo "unknown step $s"; exit 2 ;;

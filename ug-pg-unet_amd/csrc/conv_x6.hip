@@ -363,6 +363,39 @@ __device__ __forceinline__ void glds16(const void* g, void* lds_wave) {
         : "v"(g), "s"(m0)
         : "memory");
 }
+// N (<= 4) consecutive 1-KiB LDS-DMA blocks of one wave: global g + 1024 i -> LDS
+// lds_wave + 1024 i + 16 lane.  The instruction offset applies to both addresses, so M0 is
+// set once per run (the per-block M0 switches -- readfirstlane, s_mov, s_nop, restore --
+// were the bulk of the loaders' DMA issue)
+template <int N>
+__device__ __forceinline__ void glds16_run(const void* g, void* lds_wave) {
+    static_assert(N >= 1 && N <= 4, "13-bit instruction offsets: at most 4 blocks per run");
+    const unsigned m0 =
+        __builtin_amdgcn_readfirstlane((unsigned)reinterpret_cast<uintptr_t>(lds_wave));
+    unsigned keep;
+    if constexpr (N == 1)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                     "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(g), "s"(m0) : "memory");
+    else if constexpr (N == 2)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                     "global_load_lds_dwordx4 %1, off\n\t"
+                     "global_load_lds_dwordx4 %1, off offset:1024\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(g), "s"(m0) : "memory");
+    else if constexpr (N == 3)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                     "global_load_lds_dwordx4 %1, off\n\t"
+                     "global_load_lds_dwordx4 %1, off offset:1024\n\t"
+                     "global_load_lds_dwordx4 %1, off offset:2048\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(g), "s"(m0) : "memory");
+    else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                     "global_load_lds_dwordx4 %1, off\n\t"
+                     "global_load_lds_dwordx4 %1, off offset:1024\n\t"
+                     "global_load_lds_dwordx4 %1, off offset:2048\n\t"
+                     "global_load_lds_dwordx4 %1, off offset:3072\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(g), "s"(m0) : "memory");
+}
 template <int N>
 __device__ __forceinline__ void vm_wait() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -900,7 +933,9 @@ __device__ unsigned long long g_clk[8192];
 // fraction of the main loop spent in vm_wait (out[0..2], per phase) and at barriers
 // (out[3..5]); the first compute wave's fraction at barriers (out[6]) and in the
 // per-item epilogue (out[7]); loop cycles per step of the compute wave (out[8]); cycles of
-// the last epilogue's store phase (out[9]) and statistics phase (out[10])
+// the last epilogue's store phase (out[9]) and statistics phase (out[10]); the loader waves'
+// fractions of the loop in halo stores (out[11]), weight-row DMA issue (out[12]) and halo
+// loads + cursor advances (out[13])
 extern "C" int ugpg_debug_stamps(double* out) {
     static unsigned long long h[8192];
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_clk), sizeof(h)) != hipSuccess) return -1;
@@ -908,12 +943,13 @@ extern "C" int ugpg_debug_stamps(double* out) {
     static unsigned long long he[512 * 4];
     if (hipMemcpyFromSymbol(he, HIP_SYMBOL(g_epi), sizeof(he)) != hipSuccess) return -1;
 #endif
-    static double f[11][512];
+    static double f[14][512];
     int n = 0;
     for (int i = 0; i < 512; ++i)
         if (h[16 * i] > 0) {
             const unsigned long long* r = h + 16 * i;
             for (int q = 0; q < 6; ++q) f[q][n] = (double)r[1 + q] / r[0];
+            for (int q = 0; q < 3; ++q) f[11 + q][n] = (double)r[12 + q] / r[0];
             f[6][n] = r[8] ? (double)r[9] / r[8] : 0.0;
             f[7][n] = r[8] ? (double)r[10] / r[8] : 0.0;
             f[8][n] = r[11] ? (double)r[8] / r[11] : 0.0;
@@ -925,7 +961,7 @@ extern "C" int ugpg_debug_stamps(double* out) {
 #endif
             ++n;
         }
-    for (int q = 0; q < 11; ++q) {
+    for (int q = 0; q < 14; ++q) {
         std::sort(f[q], f[q] + n);
         out[q] = n ? f[q][n / 2] : 0.0;
     }
@@ -1217,11 +1253,21 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
                 const u32x4* ws = static_cast<const u32x4*>(a.wpk) +
                                   (((size_t)(q.nb * NSLAB + sb) * nchunk + q.c) * 3 + ky) * R_VEC;
                 u32x4* Bs = Bring + slot * R_STR + sb * R_VEC;
+#ifdef X6R_DMA_PERBLOCK  // A/B build: one M0 setting per block, blocks strided by wave
 #pragma unroll
                 for (int v = 0; v < R_PER; ++v) {
                     const int base = v * 256 + (v + 1 < R_PER ? lw : lw % R_LASTW) * 64;
                     glds16(ws + base + lane, Bs + base);
                 }
+#else
+                // wave lw copies R_PER consecutive blocks of the row (the last wave's run
+                // ends at the row's end, repeating blocks of the wave before it: identical
+                // bytes to the same place), in runs of at most four blocks per M0 setting
+                constexpr int NB = R_VEC / 64;
+                const int b0 = min(lw * R_PER, NB - R_PER) * 64;
+                glds16_run<(R_PER < 4 ? R_PER : 4)>(ws + b0 + lane, Bs + b0);
+                if constexpr (R_PER > 4) glds16_run<R_PER - 4>(ws + b0 + 256 + lane, Bs + b0 + 256);
+#endif
             }
         };
         // prologue: step 0 in LDS (halo buffer 0, rows 0-2), halos 1 and 2 in registers
@@ -1274,6 +1320,7 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
 #ifdef X6R_STAMP
         // diagnostic build: loader cycles spent waiting for global loads / at barriers
         unsigned long long st_vm[3] = {0, 0, 0}, st_bar[3] = {0, 0, 0};
+        unsigned long long st_sh = 0, st_dma = 0, st_lh = 0;  // halo stores, row DMAs, halo loads
         const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();
 #define ST_WAIT(acc, stmt)                                          \
     {                                                               \
@@ -1302,18 +1349,18 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
             // batches, and phase 0 first retires halo(k+1) (issued right after row 3k+2)
             // before writing it.
             // phase 0
-            dma_row(cw, 0, sl);
+            ST_WAIT(st_dma, dma_row(cw, 0, sl));
             if constexpr (LA == 3) {
-                store_halo(k + 1, S, 0, HA);
+                ST_WAIT(st_sh, store_halo(k + 1, S, 0, HA));
                 ST_WAIT(st_vm[0], vm_wait<H + R>());  // row j-1
             } else {
                 ST_WAIT(st_vm[0], vm_wait<4 * R + H>());  // halo(k+1), row 3k+2
-                store_halo(k + 1, S, 0, HA);
+                ST_WAIT(st_sh, store_halo(k + 1, S, 0, HA));
             }
             ST_WAIT(st_bar[0], lds_barrier());
             // phase 1
-            dma_row(cw, 1, (sl + 1) % NSLOT);
-            store_halo(k + 1, S, HA, A_PER);
+            ST_WAIT(st_dma, dma_row(cw, 1, (sl + 1) % NSLOT));
+            ST_WAIT(st_sh, store_halo(k + 1, S, HA, A_PER));
             if constexpr (LA == 3) {
                 ST_WAIT(st_vm[1], vm_wait<R>());  // row j (and halo(k+2))
             } else {
@@ -1321,10 +1368,8 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
             }
             ST_WAIT(st_bar[1], lds_barrier());
             // phase 2
-            dma_row(cw, 2, (sl + 2) % NSLOT);
-            load_halo(ch, S, TabOn{});
-            advance(cw, false);
-            advance(ch, true);
+            ST_WAIT(st_dma, dma_row(cw, 2, (sl + 2) % NSLOT));
+            ST_WAIT(st_lh, load_halo(ch, S, TabOn{}); advance(cw, false); advance(ch, true));
             sl = (sl + 3) % NSLOT;
             if constexpr (LA == 3) {
                 ST_WAIT(st_vm[2], vm_wait<R + H>());  // row j+1
@@ -1350,6 +1395,9 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
                 g_clk[16 * blockIdx.x + 1 + q] = st_vm[q];
                 g_clk[16 * blockIdx.x + 4 + q] = st_bar[q];
             }
+            g_clk[16 * blockIdx.x + 12] = st_sh;
+            g_clk[16 * blockIdx.x + 13] = st_dma;
+            g_clk[16 * blockIdx.x + 14] = st_lh;
         }
 #endif
         return;
