@@ -1376,7 +1376,10 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
             } else {
                 ST_WAIT(st_vm[2], vm_wait<4 * R + 2 * H>());  // row 3k+4
             }
-            ST_WAIT(st_bar[2], lds_barrier());
+            // phase 2 writes no LDS (its DMA completions are the vmcnt wait above): no
+            // lgkmcnt(0) before this barrier, so the coefficient-table reads of load_halo
+            // (consumed by the next phase-0 halo stores) stay in flight across it
+            ST_WAIT(st_bar[2], read_barrier());
         };
         static_assert((NSLOT & (NSLOT - 1)) == 0 && NSLOT >= LA + 1, "ring slot arithmetic");
         for (int k = 0; k < total; k += 2) {
