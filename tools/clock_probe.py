@@ -69,7 +69,8 @@ def main():
             if not a.stamps:
                 what = f"clock {v[0]:.0f} MHz"
             elif a.wgrad:
-                what = f"loader vm_wait {v[0]:.1%} barrier {v[3]:.1%}"
+                what = (f"loader vm_wait {v[0]:.1%} barrier {v[3]:.1%} LDS stores (incl. VALU)"
+                        f" {v[11]:.1%} loads+cursor {v[12]:.1%}")
             else:
                 what = ("loader vm_wait/barrier per phase " + " ".join(
                     f"p{q}:{v[q]:.1%}/{v[3 + q]:.1%}" for q in range(3)) +

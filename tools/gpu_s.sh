@@ -8,6 +8,7 @@
 #   bench[:args]           bench.py (default line, no CPU baseline) with extra args ('+' = space)
 #   prof[:args]            rocprofv3 --kernel-trace --stats of a short bench run
 #   stamps:<x6|bf16>       in-kernel stamps (exp/lib_stamp.so) of five layers
+#   abstep:<lib>:<math>   tools/ab_step.py in-tree vs exp/<lib>.so (x6 or bf16)
 #   cb:<args>              tools/conv_bench.py with args ('+' = space)
 #   env:VAR=VAL / unenv:VAR   set / unset an environment variable for the following steps
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -50,6 +51,12 @@ for s in "$@"; do
     stamps:*)  # in-kernel loader/compute stamps of exp/lib_stamp.so (-D X6R_STAMP=1), math x6 or bf16
       m=${s#stamps:}; ns=$((ns+1))
       run "stamps${ns}_$m" 300 env UGPG_LIB=exp/lib_stamp.so python tools/clock_probe.py --stamps --seconds 1 --math $m $( [ "$m" = bf16 ] && echo --out16 ) --layers inc.3,down1.3,down2.3,down3.3,up4.0 || exit $? ;;
+    wstamps:*)  # weight-gradient loader stamps of exp/lib_wstamp.so (-D X6W_STAMP=1)
+      m=${s#wstamps:}; ns=$((ns+1))
+      run "wstamps${ns}_$m" 300 env UGPG_LIB=exp/lib_wstamp.so python tools/clock_probe.py --stamps --wgrad --seconds 1 --math $m $( [ "$m" = bf16 ] && echo --out16 ) --layers inc.3,down1.3,down2.3,down3.3,up4.0 || exit $? ;;
+    abstep:*)  # in-process whole-step A/B: in-tree library vs exp/<lib>.so, arithmetic m
+      IFS=: read -r _ l m <<< "$s"; na=$((na+1))
+      run "abstep${na}_${l}_$m" 600 python tools/ab_step.py --a lib:ug-pg-unet_amd/ugpg/libugpg.so --b lib:exp/$l.so --conv-math $m --rounds 6 || exit $? ;;
     env:*) export "${s#env:}"; echo "[$TAG] export ${s#env:}" ;;
     unenv:*) unset "${s#unenv:}" ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -1954,6 +1954,25 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
                 lderive(l);
             }
         };
+        // the lane's element offsets from the tile origin for interior tiles (every dy and
+        // halo pixel inside the image): step-invariant, computed once (one set per source,
+        // whose channel counts differ) instead of two integer multiplies per vector per step
+        int dof_in[DY_PER], xof_in[2][X_PER];
+        unsigned xin_all = 0;
+#pragma unroll
+        for (int v = 0; v < DY_PER; ++v) {
+            const int p = (lt + v * 256) >> 4;
+            dof_in[v] = ((p / TW) * a.W + p % TW) * a.Cout;
+        }
+#pragma unroll
+        for (int v = 0; v < X_PER; ++v) {
+            const int idx = lt + v * 256;
+            const int hp = idx < X_Q ? idx >> 4 : 0;
+            const int o = (hp / HWD - 1) * a.W + hp % HWD - 1;
+            xof_in[0][v] = idx < X_Q ? o * a.C0 : 0;
+            xof_in[1][v] = idx < X_Q ? o * a.C1 : 0;
+            xin_all |= (idx < X_Q ? 1u : 0u) << v;
+        }
         auto gload = [&](const LCur& c, auto S) {
             constexpr int st = decltype(S)::value;
             const int co0 = c.nb * 64, ci0 = c.cb * 64;
@@ -1995,12 +2014,11 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
             if (ty0 >= 1 && tx0 >= 1 && ty0 + TH + 1 <= a.H && tx0 + TW + 1 <= a.W) {
                 // interior tile (uniform): every dy pixel and halo pixel is in the image
 #pragma unroll
-                for (int v = 0; v < DY_PER; ++v) dof[v] = dyo[v] * a.Cout;
+                for (int v = 0; v < DY_PER; ++v) dof[v] = dof_in[v];
 #pragma unroll
-                for (int v = 0; v < X_PER; ++v)
-                    xof[v] = ((xin >> v) & 1u) ? (xpy[v] * a.W + xpx[v]) * Cs : 0;
+                for (int v = 0; v < X_PER; ++v) xof[v] = second ? xof_in[1][v] : xof_in[0][v];
                 dvalid[st] = (1u << DY_PER) - 1;
-                xvalid[st] = xin;
+                xvalid[st] = xin_all;
             } else {
                 dvalid[st] = 0;
 #pragma unroll
@@ -2090,6 +2108,14 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
 #pragma unroll
             for (int v = 0; v < DY_PER; ++v) {
                 const int idx = lt + v * 256;
+                if constexpr (NP == 1 && DB16 && !BN) {
+                    // bf16 dy is already the single piece: its bits go to the record as they
+                    // are (the widen / round trip through fp32 was exact and cost 10 VALU)
+                    const bool ok = (dvalid[st] >> v) & 1u;
+                    const u32x2 w = {ok ? rdy[st][v].x : 0u, ok ? rdy[st][v].y : 0u};
+                    *reinterpret_cast<u32x2*>(dys + (idx >> 4) * REC + (idx & 15) * 8) = w;
+                    continue;
+                }
                 const f32x4 z = {0.f, 0.f, 0.f, 0.f};
                 f32x4 d;
                 if constexpr (DB16)  // 4 bf16 widened (exact)
@@ -2119,6 +2145,19 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
                         *reinterpret_cast<f32x4*>(a.bn_dy_out + bbase[st] + bof[st][v]) = d;
                 }
                 put(dys + (idx >> 4) * REC, idx & 15, ok ? d : z);
+            }
+            if constexpr (NP == 1 && XB16) {
+                if (!(xlo[st] > -INFINITY)) {  // (uniform) no activation: the bits as they are
+#pragma unroll
+                    for (int v = 0; v < X_PER; ++v) {
+                        const int idx = lt + v * 256;
+                        const bool ok = (xvalid[st] >> v) & 1u;
+                        const u32x2 w = {ok ? rx[st][v].x : 0u, ok ? rx[st][v].y : 0u};
+                        *reinterpret_cast<u32x2*>((idx < X_Q ? xs + (idx >> 4) * REC : dummy) +
+                                                  (idx & 15) * 8) = w;
+                    }
+                    return;
+                }
             }
 #pragma unroll
             for (int v = 0; v < X_PER; ++v) {
@@ -2156,7 +2195,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
         lds_barrier();
 #ifdef X6W_STAMP
         // diagnostic build: loader cycles waiting for global loads / at the barrier
-        unsigned long long st_vm = 0, st_bar = 0;
+        unsigned long long st_vm = 0, st_bar = 0, st_ls = 0, st_gl = 0;  // + LDS stores, loads
         const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();
 #define ST_WAIT(acc, stmt)                                          \
     {                                                               \
@@ -2175,9 +2214,8 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
             } else {
                 ST_WAIT(st_vm, vm_wait<0>());
             }
-            lstore((k + 1) & 1, S);  // step k+1
-            ladvance(lc);
-            gload(lc, S);            // step k+1+NSET, in flight across the barrier
+            ST_WAIT(st_ls, lstore((k + 1) & 1, S));  // step k+1
+            ST_WAIT(st_gl, ladvance(lc); gload(lc, S));  // step k+1+NSET, in flight across the barrier
             ST_WAIT(st_bar, lds_barrier());
         };
         for (int k = 0; k < total; k += NSET) {  // lstep(k) stores step k+1: set (k+1) % NSET
@@ -2195,6 +2233,8 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
             g_clk[16 * blockIdx.x] = __builtin_amdgcn_s_memtime() - st_t0;
             g_clk[16 * blockIdx.x + 1] = st_vm;
             g_clk[16 * blockIdx.x + 4] = st_bar;
+            g_clk[16 * blockIdx.x + 12] = st_ls;
+            g_clk[16 * blockIdx.x + 13] = st_gl;
         }
 #endif
         return;
