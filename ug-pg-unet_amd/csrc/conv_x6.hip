@@ -572,7 +572,13 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
 #else
                 if (fullw || p < vw)
 #endif
+#ifndef X6_PLAIN_STORES  // (A/B build: plain stores)
+                    // non-temporal bf16 output stores: forward launches 3-5 % faster, bf16 step
+                    // -0.6 % in-process (profiles/r6f_ab_nontemporal_epilogue_stores.txt)
+                    __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(a.out0_16 + rowb + (size_t)p * ostride + 8 * k));
+#else
                     *reinterpret_cast<u32x4*>(a.out0_16 + rowb + (size_t)p * ostride + 8 * k) = w;
+#endif
             }
             asm volatile("" ::: "memory");  // the next m-tile's staging writes after these reads
         }
@@ -781,6 +787,8 @@ __device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a,
 #pragma unroll
                         for (int i = 0; i < 4; ++i) v[i] += o[i];
                     }
+                    // (plain: non-temporal here made the fp32 step 1.4 % slower -- the next
+                    // layer reads this output -- profiles/r6f_ab_nontemporal_epilogue_stores.txt)
                     *q = v;
 #pragma unroll
                     for (int i = 0; i < 4; ++i) psum[nt][i] += acc[mt][nt][i];
