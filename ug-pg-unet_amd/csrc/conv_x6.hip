@@ -1212,6 +1212,24 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
         auto store_halo = [&](int k, auto S, int v0, int v1) {
             constexpr int st = decltype(S)::value;
             u32x4* As = smem + (k & 1) * A_VECS;
+            if constexpr (NP == 1) {
+                if (b16[st] && !(lo[st] > -INFINITY)) {
+                    // (uniform) a bf16 source without activation (a data gradient's dy, an Up
+                    // conv's upsampled half): its 8 bf16 are already the single piece -- the
+                    // bits go to LDS as they are (no widen / identity affine / round trip)
+#pragma unroll
+                    for (int v = v0; v < v1; ++v) {
+                        const int hp = item_px(lt + v * 256);
+                        const bool ok = (avalid[st] >> v) & 1u;
+                        u32x4 w = __builtin_bit_cast(u32x4, ra[st][v][0]);
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) w[i] = ok ? w[i] : 0u;
+                        const int hl = hp < NHALO ? (hp / HWD) * HS + hp % HWD : NHALO;
+                        As[hhl * NHP + hl] = w;
+                    }
+                    return;
+                }
+            }
 #pragma unroll
             for (int v = v0; v < v1; ++v) {
                 const int hp = item_px(lt + v * 256), hh = hhl;
