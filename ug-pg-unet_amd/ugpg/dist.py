@@ -51,6 +51,10 @@ class _SyncBN:
 
     def __init__(self):
         self.rank, self.nranks = world()
+        # a process group of its own (its own RCCL communicator and stream): the statistics
+        # exchange of a BatchNorm in the backward must not queue behind the overlapped
+        # gradient buckets in flight on the default group
+        self.group = dist.new_group(list(range(self.nranks))) if self.nranks > 1 else None
 
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         if self.nranks > 1:
@@ -58,7 +62,7 @@ class _SyncBN:
             if comm is not None:
                 comm.all_reduce(t)
             else:
-                dist.all_reduce(t)
+                dist.all_reduce(t, group=self.group)
         return t
 
 
