@@ -177,7 +177,7 @@ typedef struct {
      * pass folded into the weight gradient.  UGPG_WFMT_X6 math, fp32 sources, da, y and
      * dy_out, Cout % 64 == 0, 64-channel sources, db == NULL; or the image layer's form
      * (one 8-channel source without activation, Cout == 64, Cin_real <= 3, dy_out == NULL:
-     * its dy has no other reader).  With route_src / route_argmax (the split-bf16 form):
+     * its dy has no other reader; any math; y fp32 or stored in bf16, y_bf16).  With route_src / route_argmax (the split-bf16 form):
      * da = the MaxPool2d backward of route_src routed by route_argmax (as
      * ugpg_bn_relu_bwd_partials_routed's UGPG_ROUTE_MAXPOOL2) plus `da` when da != NULL.
      * NULL: off. */
@@ -194,6 +194,7 @@ typedef struct ugpg_bn_lazy {
     float* dy_out;         /* NHWC [B][H][W][Cout] or NULL; must not alias da or y */
     const float* route_src;       /* NHWC [B][H/2][W/2][Cout] pooled-output gradient or NULL */
     const uint8_t* route_argmax;  /* its window argmax (ugpg_maxpool2_fwd), or NULL */
+    const void* y_bf16;    /* y stored in bf16 (y == NULL): the image layer's weight gradient only */
 } ugpg_bn_lazy_t;
 size_t ugpg_conv3x3_wgrad_workspace(const ugpg_wgrad_t* p);
 int ugpg_conv3x3_wgrad(const ugpg_wgrad_t* p, void* ws, size_t ws_bytes, void* stream);

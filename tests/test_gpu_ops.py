@@ -1028,14 +1028,17 @@ def test_wgrad_lazy_bn_dy_is_the_apply(dev, case):
         ops.set_conv_math(old)
 
 
+@pytest.mark.parametrize("math", ["x6", "bf16"])
 @pytest.mark.parametrize("shape", [(2, 36, 70), (1, 256, 256)])
-def test_wgrad_img_lazy_bn_dy_is_the_apply(dev, shape):
+def test_wgrad_img_lazy_bn_dy_is_the_apply(dev, shape, math):
     """The image layer's weight gradient (3 real channels of an 8-channel image, 64 outputs)
     forming dy from the following BatchNorm backward (dy_out NULL: no other reader): dW and
-    the finalize's outputs bit-identical to the apply pass + the same kernel."""
+    the finalize's outputs bit-identical to the apply pass + the same kernel.  Under the
+    bf16 arithmetic y is stored in bf16 (the image layer's output) and the apply writes an
+    fp32 dy (the image layer's weight gradient is fp32)."""
     from ugpg import ops
     old = ops.conv_math()
-    ops.set_conv_math("x6")
+    ops.set_conv_math(math)
     try:
         B, H, W = shape
         C = 64
@@ -1043,7 +1046,8 @@ def test_wgrad_img_lazy_bn_dy_is_the_apply(dev, shape):
         img[..., :3] = nhwc(rnd((B, 3, H, W), 301, "img"))
         srcs = [ops.Act(img.to(dev))]
         gd = _Guards(dev)
-        y = gd(nhwc(rnd((B, C, H, W), 302, "y") + 0.2), "y")
+        yh = nhwc(rnd((B, C, H, W), 302, "y") + 0.2)
+        y = gd(yh.to(torch.bfloat16) if math == "bf16" else yh, "y")
         da = gd(nhwc(rnd((B, C, H, W), 303, "da")), "da")
         mean, invstd = rnd((C,), 304, "m", 0.1).to(dev), (rnd((C,), 305, "i").abs() + 0.5).to(dev)
         scale, shift = (rnd((C,), 306, "s", 0.5) + 1).to(dev), rnd((C,), 307, "h", 0.3).to(dev)

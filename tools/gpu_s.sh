@@ -9,6 +9,7 @@
 #   prof[:args]            rocprofv3 --kernel-trace --stats of a short bench run
 #   stamps:<x6|bf16>       in-kernel stamps (exp/lib_stamp.so) of five layers
 #   abstep:<lib>:<math>   tools/ab_step.py in-tree vs exp/<lib>.so (x6 or bf16)
+#   abx@<a>@<b>@<math>     tools/ab_step.py of two settings (lib:path / module._NAME=v)
 #   cb:<args>              tools/conv_bench.py with args ('+' = space)
 #   env:VAR=VAL / unenv:VAR   set / unset an environment variable for the following steps
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -57,6 +58,12 @@ for s in "$@"; do
     abstep:*)  # in-process whole-step A/B: in-tree library vs exp/<lib>.so, arithmetic m
       IFS=: read -r _ l m <<< "$s"; na=$((na+1))
       run "abstep${na}_${l}_$m" 600 python tools/ab_step.py --a lib:ug-pg-unet_amd/ugpg/libugpg.so --b lib:exp/$l.so --conv-math $m --rounds 6 || exit $? ;;
+    abx@*)  # in-process whole-step A/B of two settings: abx@<a>@<b>@<math> (tools/ab_step.py)
+      IFS=@ read -r _ sa sb m <<< "$s"; na=$((na+1))
+      run "abx${na}_$m" 600 python tools/ab_step.py --a "$sa" --b "$sb" --conv-math $m --rounds 6 || exit $? ;;
+    py:*)  # python <args> ('+' = space), e.g. py:tools/img_bench.py+--libs+a.so,b.so
+      a=${s#py:}; a=${a//+/ }; npy=$((npy+1))
+      run "py${npy}" 600 python $a || exit $? ;;
     env:*) export "${s#env:}"; echo "[$TAG] export ${s#env:}" ;;
     unenv:*) unset "${s#unenv:}" ;;
     *) echo "unknown step $s"; exit 2 ;;

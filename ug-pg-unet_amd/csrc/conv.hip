@@ -451,13 +451,22 @@ __global__ void __launch_bounds__(192) conv3x3_wgrad_c8_kernel(WgradArgs a) {
 // writes one split-K partial slab (ci 3..7 as zeros) for wgrad_reduce_kernel.  The grid
 // is a fixed count, so the summation order is device-independent.
 // ---------------------------------------------------------------------------
-constexpr int WGI_TH = 2, WGI_TW = 32, WGI_PX = 8, WGI_GRID = 1024, WGI_NCI = 3;
+#ifndef UGPG_WGI_GRID
+#define UGPG_WGI_GRID 1024
+#endif
+constexpr int WGI_TH = 2, WGI_TW = 32, WGI_PX = 8, WGI_GRID = UGPG_WGI_GRID, WGI_NCI = 3;
 // BN: dy formed from the following BatchNorm(+ReLU) backward while loading (a.bn_*: da, y
 // and the apply's coefficients; bn_bwd_dy, bit-identical to the apply pass) -- the image
 // layer's dy has no other reader (the input image needs no gradient), so the apply pass
 // over the largest activation of the network is dropped
-template <bool BN>
+// TY: the storage of y (float, or __bf16: the bf16 arithmetic stores the image layer's output
+// in bf16).  The next tile's (da, y) stay raw in registers while the current tile computes
+// and dy is formed after it: forming dy at the fetch made every tile wait for its loads
+// (the bf16-y form is held to 128 registers -- 2 workgroups per CU instead of 1, 8 B/lane of
+// spills: 126 -> 99 us; the fp32-y form spills 48 B/lane there and is faster at 138)
+template <bool BN, typename TY = float>
 __global__ void __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(std::is_same<TY, float>::value ? 1 : 4)))
 conv3x3_wgrad_img_kernel(WgradArgs a) {
     typedef float f2 __attribute__((ext_vector_type(2)));
     constexpr int TH = WGI_TH, TW = WGI_TW, PX = WGI_PX, NCI = WGI_NCI, CIN = 8, NT = 256;
@@ -495,24 +504,54 @@ conv3x3_wgrad_img_kernel(WgradArgs a) {
 #pragma unroll
         for (int i = 0; i < 6; ++i) bc[i] = *reinterpret_cast<const f2*>(src[i] + 2 * cp);
     }
-    auto dy_fetch = [&](int tile, f2* d) {
+    // raw operands of one tile's dy: da (or dy) and y of this thread's 8 pixels x 2 channels
+    // (pixels past the image / tiles past the end: zero dy, bit ok clear)
+    typedef typename std::conditional<std::is_same<TY, float>::value, f2, uint32_t>::type yv_t;
+    struct Raw {
+        f2 g[PX];
+        yv_t v[BN ? PX : 1];
+        uint32_t ok;
+    };
+    auto dy_fetch = [&](int tile, Raw& r) {
         const int b = tile / tpi, trem = tile % tpi;
         const int gy = (trem / a.tiles_x) * TH + row, gx0 = (trem % a.tiles_x) * TW + c0;
         const size_t o = ((size_t)(b * a.H + gy) * a.W + gx0) * 64 + 2 * cp;
+        r.ok = 0;
 #pragma unroll
         for (int p = 0; p < PX; ++p) {
-            d[p] = f2{0.f, 0.f};
+            r.g[p] = f2{0.f, 0.f};
+            if constexpr (BN) r.v[p] = yv_t{};
             if (tile < a.ntiles && gy < a.H && gx0 + p < a.W) {
+                r.ok |= 1u << p;
                 if constexpr (BN) {
-                    const f2 g = *reinterpret_cast<const f2*>(a.bn_da + o + (size_t)p * 64);
-                    const f2 v = *reinterpret_cast<const f2*>(a.bn_y + o + (size_t)p * 64);
-#pragma unroll
-                    for (int c = 0; c < 2; ++c)
-                        d[p][c] = bn_bwd_dy(g[c], v[c], bc[0][c], bc[1][c], bc[2][c], bc[3][c],
-                                            bc[4][c], bc[5][c]);
+                    r.g[p] = *reinterpret_cast<const f2*>(a.bn_da + o + (size_t)p * 64);
+                    if constexpr (std::is_same<TY, float>::value)
+                        r.v[p] = *reinterpret_cast<const f2*>(a.bn_y + o + (size_t)p * 64);
+                    else
+                        r.v[p] = *reinterpret_cast<const uint32_t*>(a.bn_y16 + o + (size_t)p * 64);
                 } else {
-                    d[p] = *reinterpret_cast<const f2*>(a.dy + o + (size_t)p * 64);
+                    r.g[p] = *reinterpret_cast<const f2*>(a.dy + o + (size_t)p * 64);
                 }
+            }
+        }
+    };
+    auto dy_form = [&](const Raw& r, f2* d) {
+#pragma unroll
+        for (int p = 0; p < PX; ++p) {
+            if constexpr (BN) {
+                f2 v;
+                if constexpr (std::is_same<TY, float>::value) {
+                    v = r.v[p];
+                } else {  // exact widening of the two bf16
+                    v = f2{__uint_as_float(r.v[p] << 16), __uint_as_float(r.v[p] & 0xffff0000u)};
+                }
+#pragma unroll
+                for (int c = 0; c < 2; ++c)
+                    d[p][c] = (r.ok >> p) & 1u ? bn_bwd_dy(r.g[p][c], v[c], bc[0][c], bc[1][c], bc[2][c],
+                                                           bc[3][c], bc[4][c], bc[5][c])
+                                               : 0.f;
+            } else {
+                d[p] = r.g[p];
             }
         }
     };
@@ -523,15 +562,17 @@ conv3x3_wgrad_img_kernel(WgradArgs a) {
     int buf = 0;
     if ((int)blockIdx.x < a.ntiles) {
         halo_put(0, halo_fetch(blockIdx.x));
-        dy_fetch(blockIdx.x, d);
+        Raw r0;
+        dy_fetch(blockIdx.x, r0);
+        dy_form(r0, d);
     }
     __syncthreads();
     for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x, buf ^= 1) {
         // next tile (zeros past the end: no branch for the compiler to sink the FMAs past)
         const int nxt = tile + gridDim.x;
         const f32x4 hn = halo_fetch(nxt);
-        f2 dn[PX];
-        dy_fetch(nxt, dn);
+        Raw rn;
+        dy_fetch(nxt, rn);
 #pragma unroll
         for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
@@ -564,8 +605,7 @@ conv3x3_wgrad_img_kernel(WgradArgs a) {
                     for (int kx = 0; kx < 3; ++kx) asm volatile("" : "+v"(acc[((c * 3 + ky) * 3 + kx) * NCI + ci]));
             }
         halo_put(buf ^ 1, hn);
-#pragma unroll
-        for (int p = 0; p < PX; ++p) d[p] = dn[p];
+        dy_form(rn, d);
         __syncthreads();
     }
     // the 2 segments of a wave that share cp (lane bit 5), then waves 4 -> 2 -> 1
@@ -1061,12 +1101,12 @@ static int wgrad_check(const ugpg_wgrad_t* p) {
         // WG_IMG) forms it too, with no other reader of dy (dy_out == NULL)
         const bool img = C1 == 0 && C0 == 8 && !p->db && !p->src[0].scale && p->Cout == 64 &&
                          p->Cin_real > 0 && p->Cin_real <= WGI_NCI && !p->dy && !p->dy_bf16 &&
-                         !wgrad_b16(p) && l->da && l->y && l->mean && l->invstd && l->scale &&
+                         !wgrad_b16(p) && l->da && !l->y != !l->y_bf16 && l->mean && l->invstd && l->scale &&
                          l->shift && l->coef && !l->dy_out && !l->route_src && !l->route_argmax;
         if (img) return UGPG_OK;
         if (p->dy || p->dy_bf16 || p->math != UGPG_WFMT_X6 || p->db || C0 % 64 || C1 % 64 ||
             wgrad_b16(p) || p->Cout % 64 || p->Cin_real > C0 + C1 ||
-            (!l->da && !l->route_src) || !l->route_src != !l->route_argmax || !l->y ||
+            (!l->da && !l->route_src) || !l->route_src != !l->route_argmax || !l->y || l->y_bf16 ||
             !l->mean || !l->invstd || !l->scale || !l->shift || !l->coef ||
             (l->dy_out && (l->dy_out == l->da || l->dy_out == l->y))) {
             set_error("conv3x3_wgrad: dy_bn needs the split-bf16 arithmetic, fp32 sources of "
@@ -1175,6 +1215,7 @@ extern "C" int ugpg_conv3x3_wgrad(const ugpg_wgrad_t* p, void* ws, size_t ws_byt
     a.bn_dy_out = bl ? bl->dy_out : nullptr;
     a.bn_rsrc = bl ? bl->route_src : nullptr;
     a.bn_ram = bl ? bl->route_argmax : nullptr;
+    a.bn_y16 = bl ? static_cast<const __bf16*>(bl->y_bf16) : nullptr;
     a.Cout = p->Cout;
     a.Cin = Cin;
     a.part = static_cast<float*>(ws);
@@ -1192,7 +1233,9 @@ extern "C" int ugpg_conv3x3_wgrad(const ugpg_wgrad_t* p, void* ws, size_t ws_byt
         launch_wgrad_x6(a, p->math == UGPG_WFMT_BF16 ? 1 : 3, st);
     } else if (kind == WG_IMG) {
         if (a.bn_y)
-            hipLaunchKernelGGL(conv3x3_wgrad_img_kernel<true>, dim3((unsigned)w.nsplit), dim3(256), 0, st, a);
+            hipLaunchKernelGGL((conv3x3_wgrad_img_kernel<true, float>), dim3((unsigned)w.nsplit), dim3(256), 0, st, a);
+        else if (a.bn_y16)
+            hipLaunchKernelGGL((conv3x3_wgrad_img_kernel<true, __bf16>), dim3((unsigned)w.nsplit), dim3(256), 0, st, a);
         else
             hipLaunchKernelGGL(conv3x3_wgrad_img_kernel<false>, dim3((unsigned)w.nsplit), dim3(256), 0, st, a);
     } else if (kind == WG_C8) {

@@ -181,6 +181,7 @@ struct WgradArgs {
     float* bn_dy_out;
     const float* bn_rsrc;    // MaxPool2d route of da (nullable): pooled gradient, argmax
     const uint8_t* bn_ram;
+    const __bf16* bn_y16;    // y stored in bf16 (bn_y == nullptr; the image layer's kernel only)
     int Cout, Cin;
     float* part;
     float* dbpart;

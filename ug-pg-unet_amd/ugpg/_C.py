@@ -50,7 +50,8 @@ class PackItem(C.Structure):
 class BnLazy(C.Structure):
     """ugpg_bn_lazy_t."""
     _fields_ = [("da", _p), ("y", _p), ("mean", _p), ("invstd", _p), ("scale", _p), ("shift", _p),
-                ("coef", _p), ("dy_out", _p), ("route_src", _p), ("route_argmax", _p)]
+                ("coef", _p), ("dy_out", _p), ("route_src", _p), ("route_argmax", _p),
+                ("y_bf16", _p)]
 
 
 class WgradDesc(C.Structure):

@@ -146,15 +146,17 @@ def _bn_relu_wgrad(conv, bn, y, st, in_srcs, da, grads, part=None, route=None, n
     # (a deferred max-pool backward is routed into da by the x6w loader too, -0.3 %,
     # profiles/r5o_ab_step_folded_apply_pool_route.txt; the head route keeps the apply pass)
     pool = route is not None and route[0][0] == "pool"
-    fold = (route is None or pool) and part is not None and dw is not None and co % 64 == 0 \
-        and ops.conv_math() == "x6" and y.dtype == torch.float32 and da.dtype == torch.float32
+    plain = part is not None and dw is not None and co % 64 == 0 and da.dtype == torch.float32
+    fold = (route is None or pool) and plain and ops.conv_math() == "x6" and y.dtype == torch.float32
     x6w = fold and all(s.C % 64 == 0 and s.y.dtype == torch.float32 for s in in_srcs)
-    # the image layer's weight gradient (conv3x3_wgrad_img_kernel) forms it as well; its dy
-    # has no other reader (in-process A/B -0.2 %, profiles/r5m_ab_step_folded_apply_img.txt)
+    # the image layer's weight gradient (conv3x3_wgrad_img_kernel) forms it as well, under
+    # either arithmetic (y fp32, or bf16 under the bf16 arithmetic); its dy has no other
+    # reader (in-process A/B -0.2 %, profiles/r5m_ab_step_folded_apply_img.txt)
     # (only up to 3 real input channels: conv.hip's image-layer form, WGI_NCI; a 4-8 channel
     # image padded to 8 takes the apply pass and the narrow-input weight gradient)
-    img = fold and not pool and not need_dy and co == 64 and len(in_srcs) == 1 and in_srcs[0].C == 8 and \
-        conv.weight.shape[1] <= 3 and in_srcs[0].scale is None and in_srcs[0].y.dtype == torch.float32
+    img = route is None and plain and not need_dy and co == 64 and len(in_srcs) == 1 and \
+        in_srcs[0].C == 8 and conv.weight.shape[1] <= 3 and in_srcs[0].scale is None and \
+        in_srcs[0].y.dtype == torch.float32
     if x6w or img:
         base = da if not pool or route[1] else None
         coef = ops.bn_relu_bwd(base, y, mean, invstd, scale, shift, None, grads.get(bn.weight),

@@ -324,8 +324,9 @@ def conv3x3_wgrad(srcs, dy, dw, db, cin_real, accumulate=0, flops=None):
     lazy = None
     if isinstance(dy, BnLazyDy):
         pool = dy.pool or (None, None)
-        lazy = BnLazy(ptr(dy.da), ptr(dy.y), ptr(dy.mean), ptr(dy.invstd), ptr(dy.scale),
-                      ptr(dy.shift), ptr(dy.coef), ptr(dy.dy_out), ptr(pool[0]), ptr(pool[1]))
+        y32, y16 = _yargs(dy.y)  # (a bf16 y: the image layer's kernel only)
+        lazy = BnLazy(ptr(dy.da), y32, ptr(dy.mean), ptr(dy.invstd), ptr(dy.scale),
+                      ptr(dy.shift), ptr(dy.coef), ptr(dy.dy_out), ptr(pool[0]), ptr(pool[1]), y16)
         d.dy_bn = C.pointer(lazy)
         dy = dy.y
     else:
