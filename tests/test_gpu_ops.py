@@ -1120,3 +1120,15 @@ def test_wgrad_lazy_bn_dy_pool_route_is_the_apply(dev, case, base):
             assert torch.equal(a_, b_), name
     finally:
         ops.set_conv_math(old)
+
+
+@pytest.mark.parametrize("B,C,H,W,cp", [(2, 3, 17, 19, 8), (16, 3, 64, 64, 8), (2, 1, 9, 7, 1),
+                                        (3, 5, 8, 8, 6), (2, 8, 16, 16, 8)])
+def test_nchw_to_nhwc_pads_and_copies(dev, B, C, H, W, cp):
+    """The image / gradient layout conversion: a pure copy with zero channel padding."""
+    from ugpg import ops
+    x = rnd((B, C, H, W), 310, "x").to(dev)
+    out = ops.nchw_to_nhwc(x, cp)
+    ref = torch.zeros(B, H, W, cp, device=dev)
+    ref[..., :C] = x.permute(0, 2, 3, 1)
+    assert torch.equal(out, ref)
