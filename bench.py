@@ -59,6 +59,9 @@ def parse():
                     help="seg: the Stage-4 UG segmentation step (BASELINE metric, default); "
                          "herlev: the Herlev Stage-4 classifier UG step (BASELINE configs[3])")
     ap.add_argument("--classes", type=int, default=7, help="Herlev classes (--workload herlev)")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the training step from a captured hipGraph (trainer.enable_graphs; "
+                         "single process; the sampled roofline steps still run eagerly)")
     return ap.parse_args()
 
 
@@ -239,11 +242,18 @@ def main():
     tr.current_model = tr.models[4]
     tr.setup_optimizer(4)  # (the trainer constructor already made the replicas equal)
     B, R = args.batch, args.res
+    # --res other than 256: the U map comes from Stage 3 at half the resolution, as in the
+    # reference's 128 -> 256 schedule
+    tr.stage_configs[4]["resolution"], tr.stage_configs[3]["resolution"] = R, R // 2
     g = torch.Generator().manual_seed(100 + rank)
     x = torch.randn(B, 3, R, R, generator=g).to(dev)
     t = (torch.rand(B, 1, R, R, generator=g) < 0.5).float().to(dev)
     tr.current_model.train()
     tr.models[3].eval()
+    if args.graph:
+        if world > 1:
+            raise SystemExit("--graph: single process only")
+        tr.enable_graphs()
 
     def run(n, timer=None):
         # the trainer's epoch loop: step k's metrics are read back (pinned copy +
@@ -328,6 +338,8 @@ def main():
                    "per_gpu_batch": B, "global_batch": B * world, "resolution": R,
                    "parallelism": f"dp{world}",
                    "batchnorm": "sync (global batch)" if sync_batchnorm_enabled() else "local (per rank)",
+                   "execution": ("hipGraph replay of the whole step (eager on the sampled roofline steps)"
+                                 if args.graph else "eager launches"),
                    "baseline_config": ("BASELINE.json configs[2] arithmetic (bf16 conv operands, "
                                        "fp32 accumulation, bf16 activation storage)" if args.conv_math == "bf16"
                                        else "BASELINE.json configs[1]")},

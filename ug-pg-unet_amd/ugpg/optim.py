@@ -75,6 +75,15 @@ class RMSprop(Optimizer):
             ops.weights_written(params)  # the kernels wrote through raw pointers
         return loss
 
+    def replayed_step(self):
+        """The host-side part of a step whose kernels ran as a graph replay
+        (ugpg.graphs): step counts and the parameters' version counters."""
+        for group in self.param_groups:
+            params = [p for p in group["params"] if p.grad is not None]
+            for p in params:
+                self.state[p]["step"] += 1
+            ops.weights_written(params)
+
 
 class Adam(Optimizer):
     """torch.optim.Adam rule on libugpg (Herlev trainer, train_herlev.py:178-194);

@@ -11,7 +11,9 @@ host once per batch instead of the reference's six ``.item()``/``.cpu()`` calls.
 from __future__ import annotations
 
 import json
+import os
 import time
+from collections import OrderedDict
 from pathlib import Path
 
 import numpy as np
@@ -21,7 +23,8 @@ import torch.nn as nn
 from . import ops
 from .dist import (allreduce_gradients, allreduce_metrics, broadcast_buffers,
                    broadcast_parameters, overlapped_allreduce, shard_batch,
-                   sync_batchnorm_from_env, world)
+                   sync_batchnorm_enabled, sync_batchnorm_from_env, world)
+from .graphs import StepGraph
 from .loss import UncertaintyGuidedLoss, weighted_loss_tensors
 from .optim import RMSprop
 from .unet import PGUNet1, PGUNet2, PGUNet3, PGUNet4, ProgressiveUNet
@@ -81,7 +84,21 @@ class UncertaintyGuidedProgressiveTrainer:
                                         "uncertainty_weights_mean", "uncertainty_weights_std",
                                         "base_loss", "stage_transitions")}
         sync_batchnorm_from_env()
+        self.use_graphs = os.environ.get("UGPG_GRAPHS", "0") == "1"
+        self._graphs, self._graph_warm, self.last_step_graph = OrderedDict(), [], None
         self.sync_replicas()
+
+    def enable_graphs(self, on=True):
+        """Opt-in (or UGPG_GRAPHS=1): run ``train_step`` as a replay of a captured hipGraph of
+        the whole step (ugpg.graphs; bit-identical to the eager step; 1.5x the eager rate at
+        bs2 x 64^2 and bs4 x 128^2, where the host's launch issue bounds the step, and equal at
+        bs16 x 256^2: profiles/r6l_graph_probe.txt).  Single process only.  The first
+        step of a key (shapes, stage, optimizer and its hyperparameters, the modules, the
+        frozen previous stage's weights) runs eagerly, the second captures and replays,
+        the rest replay; steps with the live kernel timer (bench.py's sampled roofline
+        steps) run eagerly."""
+        self.use_graphs = bool(on)
+        self._graphs, self._graph_warm, self.last_step_graph = OrderedDict(), [], None
 
     # ------------------------------------------------------------ data parallel
     def sync_replicas(self, stages=None, buffers_only=False):
@@ -168,6 +185,64 @@ class UncertaintyGuidedProgressiveTrainer:
     def train_step(self, data, target, stage):
         """One uncertainty-guided training step on device tensors already at the
         stage resolution.  Returns the 8-float device metrics buffer (unsynced)."""
+        if (self.use_graphs and data.is_cuda and world()[1] == 1 and not sync_batchnorm_enabled()
+                and ops.TIMER is None):
+            return self._train_step_graphed(data, target, stage)
+        self.last_step_graph = None
+        return self._train_step_eager(data, target, stage)
+
+    def _graph_key(self, data, target, stage):
+        """Everything a captured step bakes in besides the buffers it rewrites."""
+        prev = self.models[stage - 1] if stage > 1 else None
+        frozen = () if prev is None else tuple(
+            (t.data_ptr(), t._version) for t in (*prev.parameters(), *prev.buffers()))
+        groups = tuple((g["lr"], g["alpha"], g["eps"], g["weight_decay"])
+                       for g in self.optimizer.param_groups)
+        pw = getattr(self.base_criterion, "pos_weight", None)
+        res = tuple(self.stage_configs[s]["resolution"] for s in (stage - 1, stage) if s >= 1)
+        return (stage, tuple(data.shape), tuple(target.shape), data.dtype, target.dtype,
+                str(data.device), ops.conv_math(), id(self.optimizer), groups,
+                id(self.current_model), self.current_model.training,
+                tuple(p.data_ptr() for p in self.current_model.parameters()),
+                None if prev is None else (id(prev), prev.training), frozen,
+                self.uncertainty_alpha, id(self.base_criterion),
+                None if pw is None else (pw.data_ptr(), pw._version), res)
+
+    GRAPH_SLOTS = 2  # captured steps kept (an epoch's full batches and its last, shorter one)
+
+    def _train_step_graphed(self, data, target, stage):
+        key = self._graph_key(data, target, stage)
+        g = self._graphs.get(key)
+        if g is None:
+            if key not in self._graph_warm:
+                # the first step of a key runs eagerly: lazily built state (the frozen
+                # stage's cached weight packs, the optimizer's buffers, the parameters'
+                # flat layout) is then outside the capture instead of re-run by every
+                # replay; the key is taken again after it
+                out = self._train_step_eager(data, target, stage)
+                self._graph_warm = (self._graph_warm + [self._graph_key(data, target, stage)])[-4:]
+                self.last_step_graph = None
+                return out
+            while len(self._graphs) >= self.GRAPH_SLOTS:  # (releases a capture's pool first)
+                self._graphs.pop(next(iter(self._graphs)))
+            g = StepGraph(key, lambda x, t: self._train_step_eager(x, t, stage), (data, target))
+            # capturing ran the step's Python side once (RMSprop's step counts, the
+            # weights' version counters, the .grad tensors): the first replay is that step
+            g.grads = [(p, p.grad) for grp in self.optimizer.param_groups for p in grp["params"]]
+            self._graphs[key] = g
+            fresh = True
+        else:
+            self._graphs.move_to_end(key)
+            fresh = False
+        out = g.replay((data, target))
+        if not fresh:
+            for p, gr in g.grads:  # the replay wrote these; an eager step may have swapped .grad
+                p.grad = gr
+            self.optimizer.replayed_step()
+        self.last_step_graph = g
+        return out.clone()
+
+    def _train_step_eager(self, data, target, stage):
         mbuf = torch.zeros(8, dtype=torch.float32, device=data.device)
         self.optimizer.zero_grad()
         output, umap, final, _ = self._forward_device(data, target, stage, mbuf)
