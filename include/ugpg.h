@@ -374,7 +374,7 @@ int ugpg_head_fwd(ugpg_src_t src, int64_t npix, const float* w, const float* b, 
  * (hres[i] x hres[i]) with nc channels; resolution HxW == finest. */
 int ugpg_heads_combine(const float* const* h, const int* hres, int n, int B, int H, int W,
                        int nc, float* logits, void* stream);
-/* dh_i = upsample_i^T(dlogits) for every head (NHWC nc channels). */
+/* dh_i = upsample_i^T(dlogits) for every head (NHWC nc channels; n <= 4, one launch). */
 int ugpg_heads_split_bwd(const float* dlogits, int B, int H, int W, int nc, float* const* dh,
                          const int* hres, int n, void* stream);
 size_t ugpg_head_bwd_workspace(int64_t npix, int C, int nc);

@@ -70,6 +70,8 @@ def main():
     dl = torch.randn(B, 1, 256, 256, device=dev, generator=g)
     for R in (32, 64, 128):
         cases[f"split_bwd 256->{R}"] = (lambda R=R: ops.heads_split_bwd(dl, [R]), dl.numel() * 4)
+    cases["split_bwd 256->32,64,128,256 (the Stage-4 heads)"] = (
+        lambda: ops.heads_split_bwd(dl, [32, 64, 128, 256]), 4 * dl.numel() * 4)
     img = torch.randn(B, 3, 256, 256, device=dev, generator=g)
     cases["nchw_to_nhwc 3->8 256^2"] = (lambda: ops.nchw_to_nhwc(img, 8), img.numel() * 4 * (1 + 8 / 3))
     libs = [p for p in a.libs.split(",") if p] or [None]

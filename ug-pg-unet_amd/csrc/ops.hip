@@ -928,10 +928,18 @@ __global__ void heads_combine1_kernel(HeadSet hs, int B, int H, int W, int nc, f
 // rows that feed the input row into 256/R interleaved parts, reduced through LDS, so
 // the 32-wide head (x8: ~15x15 contributing pixels per input pixel) runs on B*R
 // blocks rather than B*R*R/256 (64 blocks at bs16: 70 us -> a few us).
-__global__ void __launch_bounds__(256) head_split_bwd_kernel(const float* dl, int B, int H,
-                                                             int W, int nc, float* dh, int R) {
+// All heads in one launch (blocks [0, B*R0) for head 0, then B*R1 for head 1, ...): one
+// launch instead of one per head (each a few us of latency-bound work); per block the same
+// arithmetic, so dh is unchanged.
+struct SplitSet {
+    float* dh[4];
+    int res[4];
+    int n;
+};
+__device__ __forceinline__ void head_split_bwd_block(const float* dl, int H, int W, int nc,
+                                                     float* dh, int R, int blk) {
     __shared__ float red[256];
-    const int b = blockIdx.x / R, iy = blockIdx.x % R, tid = threadIdx.x;
+    const int b = blk / R, iy = blk % R, tid = threadIdx.x;
     const int parts = R < 256 ? 256 / R : 1;
     const int part = R < 256 ? tid / R : 0, lane = R < 256 ? tid % R : tid;
     int ylo, yhi;
@@ -969,6 +977,20 @@ __global__ void __launch_bounds__(256) head_split_bwd_kernel(const float* dl, in
             }
             if (part == 0 && ix < R) dh[(((size_t)b * R + iy) * R + ix) * nc + k] = s;
         }
+    }
+}
+__global__ void __launch_bounds__(256) head_split_bwd_kernel(const float* dl, int B, int H,
+                                                             int W, int nc, SplitSet hs) {
+    int blk = blockIdx.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (j >= hs.n) break;
+        const int nb = B * hs.res[j];
+        if (blk < nb) {
+            head_split_bwd_block(dl, H, W, nc, hs.dh[j], hs.res[j], blk);
+            return;
+        }
+        blk -= nb;
     }
 }
 
@@ -1857,13 +1879,19 @@ extern "C" int ugpg_heads_combine(const float* const* h, const int* hres, int n,
 extern "C" int ugpg_heads_split_bwd(const float* dl, int B, int H, int W, int nc, float* const* dh,
                                     const int* hres, int n, void* stream) {
     UGPG_REQUIRE(dl && dh && hres && n >= 1 && H == W, "heads_split_bwd");
+    UGPG_REQUIRE(n <= 4, "heads_split_bwd: at most 4 heads");
+    SplitSet hs{};
+    hs.n = n;
+    int64_t blocks = 0;
     for (int i = 0; i < n; ++i) {
-        UGPG_REQUIRE(hres[i] >= 1 && hres[i] <= H, "heads_split_bwd: head resolution");
-        hipLaunchKernelGGL(head_split_bwd_kernel, dim3((unsigned)(B * hres[i])), dim3(256), 0,
-                           as_stream(stream), dl, B, H, W, nc, dh[i], hres[i]);
-        if (int e = check_launch("heads_split_bwd")) return e;
+        UGPG_REQUIRE(hres[i] >= 1 && hres[i] <= H && dh[i], "heads_split_bwd: head resolution");
+        hs.dh[i] = dh[i];
+        hs.res[i] = hres[i];
+        blocks += (int64_t)B * hres[i];
     }
-    return UGPG_OK;
+    hipLaunchKernelGGL(head_split_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                       as_stream(stream), dl, B, H, W, nc, hs);
+    return check_launch("heads_split_bwd");
 }
 
 extern "C" size_t ugpg_head_bwd_workspace(int64_t npix, int C, int nc) {
