@@ -1624,8 +1624,14 @@ int loss_nblk(int64_t n) {
     if (b > 1024) b = 1024;
     return (int)(b < 1 ? 1 : b);
 }
+#ifndef HEAD_BWD_PPB_MIN
+#define HEAD_BWD_PPB_MIN 64
+#endif
+// blocks of the head backward: at least 64 pixels each (4 per slot) up to 1,024 blocks -- the
+// 32^2 and 64^2 heads of a bs16 step (16k / 65k pixels) then fill the chip (with 256 pixels
+// per block the 32^2 head ran on 64 blocks: 50 us for 12 MB)
 int head_nblk(int64_t npix, int64_t& ppb) {
-    int64_t b = cdiv(npix, 256);
+    int64_t b = cdiv(npix, HEAD_BWD_PPB_MIN);
     if (b > 1024) b = 1024;
     if (b < 1) b = 1;
     ppb = cdiv(npix, b);
