@@ -1619,8 +1619,10 @@ __global__ void mul_kernel(const float* x, const float* m, float* y, int64_t n) 
 }
 
 namespace {
+// (the reductions below: 4 elements per thread, up to 1,024 blocks -- at 16 per thread the
+// bs16 x 256^2 loss, metrics and U statistics ran on 256 blocks, latency-bound: 11-21 us)
 int loss_nblk(int64_t n) {
-    int64_t b = cdiv(n, 256 * 16);
+    int64_t b = cdiv(n, 256 * 4);
     if (b > 1024) b = 1024;
     return (int)(b < 1 ? 1 : b);
 }
@@ -1638,11 +1640,11 @@ int head_nblk(int64_t npix, int64_t& ppb) {
     return (int)cdiv(npix, ppb);
 }
 int metrics_nbps(int HW) {
-    int n = (int)cdiv(HW, 4096);
+    int n = (int)cdiv(HW, 1024);
     return n < 1 ? 1 : (n > 64 ? 64 : n);
 }
 int ms_nblk(int64_t n, int64_t& per) {
-    int64_t b = cdiv(n, 4096);
+    int64_t b = cdiv(n, 1024);
     if (b > 1024) b = 1024;
     if (b < 1) b = 1;
     per = cdiv(n, b);
