@@ -1304,9 +1304,13 @@ __global__ void __launch_bounds__(256) seg_metrics_finalize_kernel(const float* 
     __shared__ float cnt[1024];
     for (int e = threadIdx.x; e < B * 4; e += 256) {
         const int b = e >> 2, q = e & 3;
-        float s = 0.f;
-        for (int k = 0; k < nbps; ++k) s += part[((size_t)b * nbps + k) * 4 + q];
-        cnt[e] = s;
+        // eight independent chains (integer-valued partials below 2^24: exact in any order)
+        float s8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int k0 = 0; k0 < nbps; k0 += 8)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (k0 + j < nbps) s8[j] += part[((size_t)b * nbps + k0 + j) * 4 + q];
+        cnt[e] = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
     }
     __syncthreads();
     if (threadIdx.x == 0) {
