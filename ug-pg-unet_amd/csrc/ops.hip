@@ -1144,34 +1144,33 @@ __device__ __forceinline__ double block_tree_sum(double v) {
     return r;
 }
 
-// one block per output element (nc*(C+1) of them)
-// Block = 64 consecutive outputs x 16 partial-groups (coalesced along the
-// outputs); thread (g, l) sums partial blocks g, g+16, ... then a fixed 16-way
-// combine.
+// Block = 16 consecutive outputs x 64 partial-groups: thread (g, l) sums partial blocks
+// g, g+64, ... (up to 16 for the 1,024-block head backward of a 256^2 head; 16 groups of 64
+// serial loads each held it at 7 us) then a fixed 64-way combine in order.
 __global__ void __launch_bounds__(1024) head_bwd_finalize_kernel(const float* part, int nblk, int nc,
                                                                  int C, float* dw, float* db) {
-    __shared__ double red[16][64];
+    __shared__ double red[64][16];
     const int total = nc * (C + 1);
-    const int l = threadIdx.x & 63, g = threadIdx.x >> 6;
-    const int e = blockIdx.x * 64 + l;
+    const int l = threadIdx.x & 15, g = threadIdx.x >> 4;
+    const int e = blockIdx.x * 16 + l;
     double s = 0;
     if (e < total) {
         int i = g;
-        for (; i + 48 < nblk; i += 64) {
-            const float a0 = part[(size_t)i * total + e], a1 = part[(size_t)(i + 16) * total + e];
-            const float a2 = part[(size_t)(i + 32) * total + e];
-            const float a3 = part[(size_t)(i + 48) * total + e];
+        for (; i + 192 < nblk; i += 256) {
+            const float a0 = part[(size_t)i * total + e], a1 = part[(size_t)(i + 64) * total + e];
+            const float a2 = part[(size_t)(i + 128) * total + e];
+            const float a3 = part[(size_t)(i + 192) * total + e];
             s += a0;
             s += a1;
             s += a2;
             s += a3;
         }
-        for (; i < nblk; i += 16) s += part[(size_t)i * total + e];
+        for (; i < nblk; i += 64) s += part[(size_t)i * total + e];
     }
     red[g][l] = s;
     __syncthreads();
     if (g == 0 && e < total) {
-        for (int q = 1; q < 16; ++q) s += red[q][l];
+        for (int q = 1; q < 64; ++q) s += red[q][l];
         const int k = e / (C + 1), c = e % (C + 1);
         if (c < C) dw[(size_t)k * C + c] = (float)s;
         else if (db) db[k] = (float)s;
@@ -1985,7 +1984,7 @@ static int head_bwd_common(ugpg_src_t s, int64_t npix, const float* w, int nc, c
                        yref(s), s.scale, s.shift, npix, s.C, w, nc, dh, da, acc_da, ppb,
                        static_cast<float*>(ws), nblk, bnb);
     if (int e = check_launch("head_bwd")) return e;
-    hipLaunchKernelGGL(head_bwd_finalize_kernel, dim3((unsigned)cdiv(nc * (s.C + 1), 64)), dim3(1024), 0,
+    hipLaunchKernelGGL(head_bwd_finalize_kernel, dim3((unsigned)cdiv(nc * (s.C + 1), 16)), dim3(1024), 0,
                        st, static_cast<const float*>(ws), nblk, nc, s.C, dw, db);
     return check_launch("head_bwd_finalize");
 }
