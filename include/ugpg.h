@@ -244,12 +244,15 @@ int ugpg_bn_relu_bwd_reduce(const float* da, const float* y_f32, const void* y_b
                             const float* scale, const float* shift, float* part, int nslots,
                             void* stream);
 /* Synchronised BatchNorm backward: ugpg_bn_bwd_partials_pack sums the slots per channel
- * in fp64, out[3][C] = (sum g, sum g*xhat, sum xhat); after a SUM all-reduce,
- * ugpg_bn_bwd_partials_unpack writes sums*scale (scale = 1/nranks) into slot 0 and zeroes
- * the others, so the finalize above sees the global means (torch SyncBatchNorm's backward)
- * and dgamma / dbeta / dconv_bias average to the global-batch gradient. */
-int ugpg_bn_bwd_partials_pack(const float* part, int nslots, int C, double* out, void* stream);
-int ugpg_bn_bwd_partials_unpack(const double* sums, double scale, float* part, int nslots,
+ * in fp64, out[3][C] = (sum g, sum g*xhat, sum xhat), and out[3C] = npix (this rank's
+ * pixel count); after a SUM all-reduce of the 3C+1 values, ugpg_bn_bwd_partials_unpack
+ * writes sums * npix / N_global (N_global = the all-reduced out[3C]) into slot 0 and zeroes
+ * the others, so the finalize above (which divides by the local npix) sees the global means
+ * (torch SyncBatchNorm's backward) for any shard sizes, and dgamma / dbeta / dconv_bias
+ * average over ranks to the global-batch gradient. */
+int ugpg_bn_bwd_partials_pack(const float* part, int nslots, int C, int64_t npix, double* out,
+                              void* stream);
+int ugpg_bn_bwd_partials_unpack(const double* sums, int64_t npix, float* part, int nslots,
                                 int C, void* stream);
 /* BatchNorm-backward partials folded into the kernel that last writes da (the pooling,
  * upsampling and head backward entries *_bnb): same partial layout, nslots from

@@ -31,15 +31,22 @@ def test_library_is_built_from_these_sources():
     b = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(b)
     assert _C.lib.ugpg_build_id().decode() == b.source_id() == b.lib_id(_C.LIB_PATH)
+    assert b.source_id().split("-")[0] == b.content_id()
 
-    class Fn:  # a ctypes function stand-in returning another id
-        def __call__(self):
-            return b"0" * 32
+    def fake(ident):
+        class Fn:  # a ctypes function stand-in returning `ident`
+            def __call__(self):
+                return ident.encode()
 
-    class Stale:
-        ugpg_build_id = Fn()
+        class Lib:
+            ugpg_build_id = Fn()
+        return Lib()
+
     with pytest.raises(ImportError, match="stale"):
-        _C._check_fresh(Stale())
+        _C._check_fresh(fake("0" * 32 + "-" + b.source_id().split("-")[1]))
+    # the same sources built with another configuration (UGPG_ARCH, defines) are
+    # not stale -- only the content part is compared, not this process's environment
+    _C._check_fresh(fake(b.content_id() + "-" + "f" * 32))
 
 
 def test_every_declared_symbol_is_exported_and_bound():

@@ -392,3 +392,185 @@ def test_sync_batchnorm_step_equals_global_batch():
     # and local BatchNorm does NOT equal it (the test can tell the two policies apart)
     la, _, _, _, _ = oracle_run(1, state, x[:B_PER], t[:B_PER])
     assert (la - logits32[:B_PER]).abs().max().item() > 1e-3
+
+
+def test_sync_batchnorm_native_exchange_has_its_own_communicator(monkeypatch):
+    """VERDICT r5 weak #5 / ADVICE r5: under UGPG_COMM=native the synchronised-BatchNorm
+    exchange runs on a libugpg Communicator of its own, never on the process-wide one that
+    carries the overlapped gradient buckets (one RCCL communicator serialises its
+    operations); on the torch path it uses its own process group.  Routing only (no GPU):
+    the communicator and the collectives are stand-ins that record their calls."""
+    from ugpg import dist as D
+    made = []
+
+    class FakeComm:
+        def __init__(self):
+            self.calls = []
+            made.append(self)
+
+        def all_reduce(self, t):
+            self.calls.append(t)
+            return t
+
+    class CudaLike:  # the exchange picks the native path for device tensors only
+        is_cuda = True
+
+    monkeypatch.setattr(D, "Communicator", FakeComm)
+    monkeypatch.setattr(D, "world", lambda: (1, 2))
+    monkeypatch.setattr(D, "_COMM", None)
+    monkeypatch.setattr(D.dist, "new_group", lambda ranks: ("bn-group", tuple(ranks)))
+    monkeypatch.setenv("UGPG_COMM", "native")
+    sb = D._SyncBN()
+    buckets = D.native_comm()  # the gradient buckets' communicator
+    t = CudaLike()
+    sb.all_reduce(t)
+    sb.all_reduce(t)
+    assert len(made) == 2 and sb._comm is not None and sb._comm is not buckets
+    assert sb._comm.calls == [t, t] and buckets.calls == []
+    assert sb.native() is sb._comm  # built once
+    # torch path: its own process group, never the default one
+    monkeypatch.setenv("UGPG_COMM", "torch")
+    seen = []
+    monkeypatch.setattr(D.dist, "all_reduce", lambda x, group=None, **kw: seen.append(group))
+    sb2 = D._SyncBN()
+    sb2.all_reduce(t)
+    assert seen == [("bn-group", (0, 1))] and sb2._comm is None
+    assert len(made) == 2
+
+
+WS8 = 8
+
+
+def _batch8():
+    from oracle import detgen as G
+    return G.randn(1, (WS8, 3, 32, 32), "x"), G.bernoulli(2, (WS8, 1, 32, 32), 0.5, "t")
+
+
+def _ws8_worker(rank, port, outdir):
+    """One of eight gloo ranks: PGUNet1 at bs8 x 32^2, one image per
+    rank.  (1) local BatchNorm: this shard's oracle gradients through allreduce_gradients;
+    (2) synchronised BatchNorm through ugpg.dist's exchange (the 8-row rank-order merge);
+    (3) the OverlapReducer fed block by block at eight ranks."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "ug-pg-unet_amd")]
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WS8)
+    torch.set_num_threads(1)
+    from oracle import ref_cpu as O
+    from tests._parity import det_state, oracle_run, param_keys
+    from ugpg import ops
+    from ugpg.dist import (OverlapReducer, allreduce_gradients, enable_sync_batchnorm,
+                           overlap_reducer, overlapped_allreduce, shard)
+    state = det_state(1, 3, 1)
+    keys = param_keys(state)
+    x, t = _batch8()
+    xs, ts = shard(x, rank, WS8), shard(t, rank, WS8)
+    out = {}
+
+    def averaged(g):
+        params = [nn.Parameter(torch.zeros_like(g[k])) for k in keys]
+        buf = torch.cat([g[k].reshape(-1) for k in keys])  # the flat layout
+        off = 0
+        for p, k in zip(params, keys):
+            p.grad = buf[off:off + g[k].numel()].view_as(g[k])
+            off += g[k].numel()
+        scale = allreduce_gradients(params, bucket_bytes=1 << 16)
+        return {k: p.grad * scale for k, p in zip(keys, params)}
+
+    _, _, _, g, _ = oracle_run(1, state, xs, ts)
+    out["local"] = averaged(g)
+    enable_sync_batchnorm(True)
+    O.BN_SYNC = ops._BN_SYNC
+    assert (O.BN_SYNC.rank, O.BN_SYNC.nranks) == (rank, WS8)
+    logits, _, _, g, P = oracle_run(1, state, xs, ts)
+    out["sync"] = averaged(g)
+    out["logits"] = logits
+    out["bufs"] = {k: v for k, v in P.items() if k.endswith(("running_mean", "running_var"))}
+    O.BN_SYNC = None
+    enable_sync_batchnorm(False)
+    # the reducer: uneven sizes, several buckets, completed back to front
+    sizes = [7, 300, 1, 4096, 33, 5000, 12, 900, 2]
+    flat = torch.randn(sum(sizes), generator=torch.Generator().manual_seed(30 + rank))
+    want = flat.clone()
+    dist.all_reduce(want)
+    views, off = [], 0
+    for n in sizes:
+        views.append(flat[off:off + n])
+        off += n
+    with overlapped_allreduce():
+        red = overlap_reducer()
+        assert isinstance(red, OverlapReducer)
+        red.bucket = 700
+        red.begin(flat, views)
+        for blk in ([8, 7], [6], [5, 4, 3], [2, 1], [0]):
+            red.done([views[i] for i in blk])
+        red.flush()
+    params = [nn.Parameter(torch.zeros(n)) for n in sizes]
+    for p, v in zip(params, views):
+        p.grad = v
+    assert allreduce_gradients(params) == 1.0 / WS8
+    out["reducer"] = (flat, want)
+    torch.save(out, os.path.join(outdir, f"r{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_data_parallel_world_size_8():
+    """data parallelism above world size 2, on CPU (gloo, 8 ranks, one
+    bs1 shard each of a bs8 PGUNet1 batch at 32^2):
+    * local BatchNorm: the averaged gradient equals the mean of the 8 per-shard gradients
+      computed in one process (G8's semantics at N = 8), identical on every rank;
+    * synchronised BatchNorm: the averaged step equals the reference's single-process bs8
+      step (the oracle, bit-identical to it): logits 1e-4, every gradient by the §8d rule
+      with the perturbation-aware floor, BN running statistics 1e-5 -- so the 8-row
+      rank-order merge and the backward sums are exact at 8 ranks;
+    * the OverlapReducer at 8 ranks sums like one all-reduce."""
+    from tests._parity import det_state, grad_check, noise_floor, oracle_run, param_keys
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_ws8_worker, args=(_free_port(), d), nprocs=WS8, join=True)
+        r = [torch.load(os.path.join(d, f"r{i}.pt"), weights_only=True) for i in range(WS8)]
+    nt = torch.get_num_threads()
+    state = det_state(1, 3, 1)
+    keys = param_keys(state)
+    x, t = _batch8()
+    # (1) local BatchNorm = mean of per-shard gradients (one thread, as the ranks: the
+    # pre-BN conv biases' gradients are pure rounding noise, which the thread count moves)
+    torch.set_num_threads(1)
+    try:
+        per = [oracle_run(1, state, x[i:i + 1], t[i:i + 1])[3] for i in range(WS8)]
+    finally:
+        torch.set_num_threads(nt)
+    for k in keys:
+        mean = torch.stack([p[k].double() for p in per]).mean(0)
+        scale = max(p[k].abs().max().item() for p in per)
+        got = r[0]["local"][k].double()
+        assert torch.allclose(got, mean, rtol=1e-6, atol=1e-6 * scale + 1e-12), k
+        for i in range(1, WS8):
+            assert torch.equal(r[i]["local"][k], r[0]["local"][k]), ("replicas diverged", k)
+    # (2) synchronised BatchNorm = the global bs8 step
+    logits32, _, _, g32, P32 = oracle_run(1, state, x, t)
+    _, _, _, g64, _ = oracle_run(1, state, x, t, dtype=torch.float64)
+    floor = noise_floor(1, state, x, t, g32, g64)
+    lg = torch.cat([ri["logits"] for ri in r])
+    assert (lg - logits32).abs().max().item() <= 1e-4
+    bad = []
+    for k in keys:
+        for i in range(1, WS8):
+            assert torch.equal(r[i]["sync"][k], r[0]["sync"][k]), ("replicas diverged", k)
+        ok, err, bound = grad_check(k, r[0]["sync"][k], g32[k], g64[k], floor[k])
+        if not ok:
+            bad.append(f"{k}: {err:.3e} > {bound:.3e}")
+    assert not bad, "synced gradients differ from the bs8 step:\n" + "\n".join(bad)
+    for k, v in r[0]["bufs"].items():
+        assert (v - P32[k]).abs().max().item() <= 1e-5 * max(1.0, P32[k].abs().max().item()), k
+        for i in range(1, WS8):
+            assert torch.equal(v, r[i]["bufs"][k]), k
+    # ... which local BatchNorm is not
+    assert (r[0]["logits"] - logits32[:1]).abs().max().item() <= 1e-4
+    la = oracle_run(1, state, x[:1], t[:1])[0]
+    assert (la - logits32[:1]).abs().max().item() > 1e-3
+    # (3) the reducer
+    for i in range(WS8):
+        got, want = r[i]["reducer"]
+        assert torch.allclose(got, want, rtol=1e-5, atol=1e-5)

@@ -54,6 +54,13 @@ def _hip_step(dev, state, prev, x, t):
     return m, out.detach().cpu(), u.cpu(), final.item(), base, grads
 
 
+# Gradients of config 2 that miss SURVEY §8d's literal rule (2x the reference's UNPERTURBED
+# fp32 error + 1e-6 of scale), each one where the reference's own fp32 runs under ulp-level
+# weight perturbations (G4b floor_pert) exceed that literal bound too -- checked per tensor
+# below and listed with the numbers in DESIGN §4.
+LITERAL_RULE_EXCEPTIONS = ()
+
+
 def test_config2_bs16_step_parity(dev):
     fx = np.load("tests/golden/g4b_pgunet4_bs16.npz")
     state, prev, x, t = _inputs()
@@ -85,9 +92,9 @@ def test_config2_bs16_step_parity(dev):
     assert torch.equal((torch.sigmoid(logits.double()) > 0.5)[sure], (torch.sigmoid(logits64) > 0.5)[sure])
     print(f"tie band: {int((~sure).sum())} of {sure.numel()} pixels")
     assert abs(final - final64.item()) <= 1e-5 * abs(final64.item())
-    bad, ratios = [], []
+    bad, ratios, literal, lit_bad, lit_exc = [], [], [], [], []
     for k in param_keys(state):
-        g32_max_err, g64_max = fx[f"floor/{k}"]
+        g32_max_err, g64_max = (float(v) for v in fx[f"floor/{k}"])
         floor = float(fx[f"floor_pert/{k}"])
         gb = grads[k].double()
         err = (gb - g64[k]).abs().max().item()
@@ -95,10 +102,34 @@ def test_config2_bs16_step_parity(dev):
         ratios.append((err / bound, k))
         if err > bound:
             bad.append(f"{k}: {err:.3e} > {bound:.3e}")
+        if is_prebn_bias(k):
+            continue  # (true gradient 0: absolute 1e-5 in the survey's rule too)
+        # SURVEY §8d's literal rule: max|g - g64| <= 2 max|g32 - g64| + 1e-6 max|g64|, with the
+        # reference's own UNPERTURBED fp32 error g32_max_err
+        lbound = 2.0 * g32_max_err + 1e-6 * g64_max
+        literal.append((err / lbound, k))
+        if err > lbound:
+            # the reference itself: its fp32 runs with ulp-level weight perturbations err by
+            # floor_pert; where that already breaks the literal bound, so may any other
+            # equally valid fp32 evaluation order
+            (lit_exc if floor > lbound else lit_bad).append(
+                f"{k}: {err:.3e} > {lbound:.3e} (reference perturbed-run error {floor:.3e} = "
+                f"{floor / lbound:.2f}x the literal bound)")
     ratios.sort(reverse=True)
+    literal.sort(reverse=True)
     print("bs16 gradient headroom err/bound: worst", [(round(r, 3), k) for r, k in ratios[:5]],
           "median", round(float(np.median([r for r, _ in ratios])), 4))
+    npass = sum(r <= 1.0 for r, _ in literal)
+    print(f"SURVEY §8d literal rule (2x unperturbed floor): {npass} of {len(literal)} tensors pass; "
+          f"median err/bound {float(np.median([r for r, _ in literal])):.4f}")
+    for line in lit_exc:
+        print("  literal-rule exception (reference fails it against itself):", line)
+    for line in lit_bad:
+        print("  LITERAL-RULE FAILURE:", line)
     assert not bad, "gradient parity failures:\n" + "\n".join(bad[:20])
+    assert sorted(l.split(":")[0] for l in lit_exc) == sorted(LITERAL_RULE_EXCEPTIONS), \
+        ("the literal-rule exceptions changed", [l.split(":")[0] for l in lit_exc])
+    assert not lit_bad, "literal §8d rule failures where the reference itself passes:\n" + "\n".join(lit_bad)
     # post-RMSprop parameters: exactly torch's RMSprop rule on the HIP gradients, and the
     # reference's post-step checksums up to the first step's sign flips (RMSprop's first
     # update is ~10 lr * sign(g) whatever |g|, so a noise-level gradient element whose

@@ -106,3 +106,72 @@ def test_graphed_train_step_equals_eager(dev, math):
     finally:
         ops.TIMER = None
         ops.set_conv_math(old)
+
+
+def test_graphed_step_after_optimizer_state_reload(dev):
+    """a captured step writes RMSprop's square_avg through the pointers it
+    was captured with.  ``optimizer.load_state_dict`` (resuming from the trainer's own
+    checkpoint dict) replaces those tensors: the key (which holds the optimizer and the
+    square_avg storages) must not match the old capture, so the next step runs eagerly and
+    captures again -- and the state stays equal to the eager trainer's."""
+    import copy
+    res, B = 64, 2
+    A, G = _make(dev, res), _make(dev, res)
+    G.enable_graphs()
+    gen = torch.Generator().manual_seed(11)
+    batches = [(torch.randn(B, 3, res, res, generator=gen).to(dev),
+                (torch.rand(B, 1, res, res, generator=gen) < 0.5).float().to(dev))
+               for _ in range(7)]
+
+    def step(k):
+        x, t = batches[k]
+        ma, mg = A.train_step(x, t, 4).tolist(), G.train_step(x, t, 4).tolist()
+        assert ma == mg, (k, ma, mg)
+
+    for k in range(3):
+        step(k)
+    old = G.last_step_graph
+    assert old is not None and old.replays == 2
+    for tr in (A, G):  # a resume: the saved optimizer state, loaded back (new tensors)
+        tr.optimizer.load_state_dict(copy.deepcopy(tr.optimizer.state_dict()))
+    step(3)
+    assert G.last_step_graph is None  # the old capture is not replayed
+    step(4)
+    step(5)
+    assert G.last_step_graph is not None and G.last_step_graph is not old
+    _equal(A, G)
+    # a new optimizer for the same stage (setup_optimizer) drops every capture
+    for tr in (A, G):
+        tr.setup_optimizer(4)
+    assert len(G._graphs) == 0 and G.last_step_graph is None
+    step(6)
+    _equal(A, G)
+
+
+def test_graphed_progressive_epochs_equal_eager(dev, tmp_path):
+    """the real epoch loop under UGPG_GRAPHS -- train_progressive over two
+    stages (transfer_weights + setup_optimizer between them), each epoch's training steps
+    replayed, eval-mode validation passes between epochs (eager, no_grad), the stage-end
+    BatchNorm buffers -- gives the eager run's weights, BatchNorm buffers and history."""
+    import ugpg
+    from torch.utils.data import DataLoader, TensorDataset
+    gen = torch.Generator().manual_seed(5)
+    x = torch.randn(8, 3, 64, 64, generator=gen)
+    t = (torch.rand(8, 1, 64, 64, generator=gen) < 0.3).float()
+    runs = []
+    for graphs in (False, True):
+        torch.manual_seed(99)
+        tr = ugpg.UncertaintyGuidedProgressiveTrainer(3, 1, device=dev, uncertainty_alpha=1.0)
+        for s in tr.stage_configs:
+            tr.stage_configs[s]["epochs_per_stage"] = 2
+        tr.enable_graphs(graphs)
+        loader = DataLoader(TensorDataset(x, t), batch_size=2, shuffle=False)
+        tr.train_progressive(loader, loader, max_stages=2, save_dir=str(tmp_path / f"g{int(graphs)}"))
+        if graphs:
+            assert any(g.replays > 0 for g in tr._graphs.values()), "no step was replayed"
+        runs.append(tr)
+    e, g = runs
+    assert e.history == g.history
+    for s in (1, 2):
+        for (k, a), (_, b) in zip(e.models[s].state_dict().items(), g.models[s].state_dict().items()):
+            assert torch.equal(a, b), (s, k)

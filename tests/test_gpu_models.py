@@ -486,6 +486,13 @@ def test_ug_training_trajectory_dice_parity(dev):
     lref = max(abs(a[0] - o[0]) / abs(o[0]) for a, o in zip(o32[1:], o64[1:]))
     assert lhip <= 2 * lref + 1e-3, (lhip, lref)
     print(f"max |Dice - fp64 oracle| over steps 2-10: HIP {dev_hip:.4f}, reference fp32 {dev_ref:.4f}")
+    # and the survey's literal k = 10 contract: Dice after ten steps
+    # within +-0.001 of the reference fp32 run's -- it holds here although the trajectories
+    # drift in between (the reference's own fp32/fp64 runs differ by 0.014 at step 5)
+    d10 = abs(rows[9][1] - o32[9][1])
+    print(f"k = 10: |Dice_HIP - Dice_ref32| = {d10:.6f} (contract 0.001); "
+          f"Dice {rows[9][1]:.6f} / {o32[9][1]:.6f} / fp64 {o64[9][1]:.6f}")
+    assert d10 <= 1e-3, (rows[9][1], o32[9][1])
 
 
 def test_weight_pack_cache_reuse_and_invalidation(dev):

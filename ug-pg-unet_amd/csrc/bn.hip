@@ -301,7 +301,7 @@ __global__ void bn_bwd_finalize_kernel(const float* part, int nblk, int C, int64
 // the global means, as torch's SyncBatchNorm backward -- while dgamma, dbeta and the conv
 // bias gradient become the global sums / nranks, whose average over ranks (the gradient
 // all-reduce) is the global-batch gradient of the local-loss average.
-__global__ void bn_bwd_pack_kernel(const float* part, int nblk, int C, double* out) {
+__global__ void bn_bwd_pack_kernel(const float* part, int nblk, int C, int64_t npix, double* out) {
     const int c = blockIdx.x;
     double A, Bs, X;
     bn_bwd_sum_slots(part, nblk, C, c, A, Bs, X);
@@ -309,11 +309,16 @@ __global__ void bn_bwd_pack_kernel(const float* part, int nblk, int C, double* o
         out[c] = A;
         out[C + c] = Bs;
         out[2 * C + c] = X;
+        if (c == 0) out[3 * C] = (double)npix;  // summed over ranks: the global pixel count
     }
 }
 
-__global__ void bn_bwd_unpack_kernel(const double* __restrict__ sums, double scale, float* part,
+// slot 0 = sum_all * npix_local / N_global: the finalize divides by npix_local, so its means
+// are the global ones whatever the ranks' shard sizes (a 1/nranks scale assumed
+// equal counts)
+__global__ void bn_bwd_unpack_kernel(const double* __restrict__ sums, int64_t npix, float* part,
                                      int nblk, int C) {
+    const double scale = (double)npix / sums[3 * C];
     const int64_t n = (int64_t)3 * C * nblk;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
@@ -707,26 +712,26 @@ extern "C" int ugpg_bn_relu_bwd_reduce(const float* da, const float* y_f32, cons
     return check_launch("bn_bwd_reduce");
 }
 
-extern "C" int ugpg_bn_bwd_partials_pack(const float* part, int nslots, int C, double* out,
-                                         void* stream) {
-    if (!part || !out || nslots <= 0 || C <= 0) {
+extern "C" int ugpg_bn_bwd_partials_pack(const float* part, int nslots, int C, int64_t npix,
+                                         double* out, void* stream) {
+    if (!part || !out || nslots <= 0 || C <= 0 || npix <= 0) {
         set_error("bn_bwd_partials_pack: bad arguments");
         return UGPG_ERR_INVALID;
     }
     hipLaunchKernelGGL(bn_bwd_pack_kernel, dim3(C), dim3(bwd_fin_threads(nslots)), 0,
-                       as_stream(stream), part, nslots, C, out);
+                       as_stream(stream), part, nslots, C, npix, out);
     return check_launch("bn_bwd_partials_pack");
 }
 
-extern "C" int ugpg_bn_bwd_partials_unpack(const double* sums, double scale, float* part,
+extern "C" int ugpg_bn_bwd_partials_unpack(const double* sums, int64_t npix, float* part,
                                            int nslots, int C, void* stream) {
-    if (!sums || !part || nslots <= 0 || C <= 0) {
+    if (!sums || !part || nslots <= 0 || C <= 0 || npix <= 0) {
         set_error("bn_bwd_partials_unpack: bad arguments");
         return UGPG_ERR_INVALID;
     }
     const int64_t n = (int64_t)3 * C * nslots;
     hipLaunchKernelGGL(bn_bwd_unpack_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 1024)),
-                       dim3(256), 0, as_stream(stream), sums, scale, part, nslots, C);
+                       dim3(256), 0, as_stream(stream), sums, npix, part, nslots, C);
     return check_launch("bn_bwd_partials_unpack");
 }
 

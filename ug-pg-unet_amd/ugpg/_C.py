@@ -77,8 +77,8 @@ SIGNATURES = {
     "ugpg_bn_stats_pack": (_i, [_p, _i, _i, _p, _p]),
     "ugpg_bn_finalize_merged": (_i, [_p, _i, _i, _p, _p, _p, _p, _p, _f, _f, _p, _p, _p, _p, _p]),
     "ugpg_bn_relu_bwd_reduce": (_i, [_p, _p, _p, _i64, _i, _p, _p, _p, _p, _p, _i, _p]),
-    "ugpg_bn_bwd_partials_pack": (_i, [_p, _i, _i, _p, _p]),
-    "ugpg_bn_bwd_partials_unpack": (_i, [_p, C.c_double, _p, _i, _i, _p]),
+    "ugpg_bn_bwd_partials_pack": (_i, [_p, _i, _i, _i64, _p, _p]),
+    "ugpg_bn_bwd_partials_unpack": (_i, [_p, _i64, _p, _i, _i, _p]),
     "ugpg_bn_eval_params": (_i, [_p, _p, _p, _p, _f, _i, _p, _p, _p]),
     "ugpg_bn_relu_bwd_workspace": (_sz, [_i64, _i]),
     "ugpg_bn_relu_bwd": (_i, [_p, _p, _p, _i64, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _p,
@@ -153,9 +153,11 @@ SIGNATURES = {
 
 def _check_fresh(lib) -> None:
     """Refuse an in-tree libugpg.so built from other sources than the ones beside it (a
-    stale prebuilt library travelling with the tree): its embedded
-    ugpg_build_id() must equal build.source_id() of csrc/ + include/.  Skipped for an
-    explicit UGPG_LIB (A/B variants are built from other defines on purpose)."""
+    stale prebuilt library travelling with the tree): the content part
+    of its embedded ugpg_build_id() must equal build.content_id() of csrc/ + include/.  The
+    compile configuration (flags, UGPG_ARCH, defines) is not compared: it is the builder's,
+    not this process's environment.  Skipped for an explicit UGPG_LIB (A/B
+    variants are built from other defines on purpose)."""
     if "UGPG_LIB" in os.environ:
         return
     bpy = Path(__file__).resolve().parent.parent / "build.py"
@@ -165,12 +167,12 @@ def _check_fresh(lib) -> None:
     spec = importlib.util.spec_from_file_location("_ugpg_build", bpy)
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
-    want = mod.source_id()
+    want = mod.content_id()
     fn = getattr(lib, "ugpg_build_id", None)
     got = None
     if fn is not None:
         fn.restype, fn.argtypes = C.c_char_p, []
-        got = fn().decode()
+        got = fn().decode().split("-")[0]
     if got != want:
         raise ImportError(
             f"ugpg: {LIB_PATH} is stale (built from sources {got}, tree has {want}) -- "

@@ -413,14 +413,15 @@ def bn_relu_bwd(da, y, mean, invstd, scale, shift, dy, dgamma, dbeta, dconv_bias
             check(lib.ugpg_bn_relu_bwd_reduce(ptr(da), *_yargs(y), npix, c, ptr(mean), ptr(invstd),
                                               ptr(scale), ptr(shift), ptr(part),
                                               part.numel() // (3 * c), stream()), "bn_relu_bwd_reduce")
-        # (sum g, sum g*xhat, sum xhat) summed over ranks, written back as one slot / nranks
-        sums = empty(3 * c, like=y, dtype=torch.float64)
+        # (sum g, sum g*xhat, sum xhat) and the pixel count summed over ranks, written back
+        # as one slot scaled by npix / N_global (any shard sizes: ADVICE r5)
+        sums = empty(3 * c + 1, like=y, dtype=torch.float64)
         nslots = part.numel() // (3 * c)
-        check(lib.ugpg_bn_bwd_partials_pack(ptr(part), nslots, c, ptr(sums), stream()),
+        check(lib.ugpg_bn_bwd_partials_pack(ptr(part), nslots, c, npix, ptr(sums), stream()),
               "bn_bwd_partials_pack")
         sync.all_reduce(sums)
-        check(lib.ugpg_bn_bwd_partials_unpack(ptr(sums), 1.0 / sync.nranks, ptr(part), nslots, c,
-                                              stream()), "bn_bwd_partials_unpack")
+        check(lib.ugpg_bn_bwd_partials_unpack(ptr(sums), npix, ptr(part), nslots, c, stream()),
+              "bn_bwd_partials_unpack")
     if route is not None:
         if route[0] == "pool":
             _, dout, am, H, W = route

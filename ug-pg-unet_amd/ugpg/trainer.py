@@ -118,6 +118,14 @@ class UncertaintyGuidedProgressiveTrainer:
     def setup_optimizer(self, stage):
         self.optimizer = RMSprop(self.current_model.parameters(),
                                  lr=self.stage_configs[stage]["lr"], weight_decay=1e-4)
+        # captured steps wrote through the old optimizer's state: never replay them
+        self._drop_graphs()
+
+    def _drop_graphs(self):
+        if hasattr(self, "_graphs"):
+            self._graphs.clear()
+            self._graph_warm = []
+            self.last_step_graph = None
 
     def dice_coefficient(self, pred, target, smooth=1):
         """Mean per-sample Dice (uncertainty_guided_trainer.py:90-107).  Host-side helper
@@ -192,20 +200,28 @@ class UncertaintyGuidedProgressiveTrainer:
         return self._train_step_eager(data, target, stage)
 
     def _graph_key(self, data, target, stage):
-        """Everything a captured step bakes in besides the buffers it rewrites."""
+        """Everything a captured step bakes in besides the buffers it rewrites.  Objects
+        (optimizer, modules, criterion) are held by the key itself and compare by identity,
+        so a freed object's id can never match a new one; the optimizer state the
+        replay writes through raw pointers (each square_avg) is keyed by storage, so
+        ``optimizer.load_state_dict`` -- new state tensors -- captures again."""
         prev = self.models[stage - 1] if stage > 1 else None
         frozen = () if prev is None else tuple(
             (t.data_ptr(), t._version) for t in (*prev.parameters(), *prev.buffers()))
         groups = tuple((g["lr"], g["alpha"], g["eps"], g["weight_decay"])
                        for g in self.optimizer.param_groups)
+        opt_state = tuple(
+            (p.data_ptr(), st["square_avg"].data_ptr() if "square_avg" in st else None)
+            for grp in self.optimizer.param_groups for p in grp["params"]
+            for st in (self.optimizer.state.get(p, {}),))
         pw = getattr(self.base_criterion, "pos_weight", None)
         res = tuple(self.stage_configs[s]["resolution"] for s in (stage - 1, stage) if s >= 1)
         return (stage, tuple(data.shape), tuple(target.shape), data.dtype, target.dtype,
-                str(data.device), ops.conv_math(), id(self.optimizer), groups,
-                id(self.current_model), self.current_model.training,
+                str(data.device), ops.conv_math(), self.optimizer, groups, opt_state,
+                self.current_model, self.current_model.training,
                 tuple(p.data_ptr() for p in self.current_model.parameters()),
-                None if prev is None else (id(prev), prev.training), frozen,
-                self.uncertainty_alpha, id(self.base_criterion),
+                None if prev is None else (prev, prev.training), frozen,
+                self.uncertainty_alpha, self.base_criterion,
                 None if pw is None else (pw.data_ptr(), pw._version), res)
 
     GRAPH_SLOTS = 2  # captured steps kept (an epoch's full batches and its last, shorter one)
@@ -239,6 +255,9 @@ class UncertaintyGuidedProgressiveTrainer:
             for p, gr in g.grads:  # the replay wrote these; an eager step may have swapped .grad
                 p.grad = gr
             self.optimizer.replayed_step()
+            # the replayed BatchNorm finalizes updated the running statistics in place (the
+            # eager bn_finalize bumps their versions: eval-mode parameter caches key on them)
+            ops.weights_written([b for b in self.current_model.buffers() if b.is_floating_point()])
         self.last_step_graph = g
         return out.clone()
 
