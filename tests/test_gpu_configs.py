@@ -58,7 +58,11 @@ def _hip_step(dev, state, prev, x, t):
 # fp32 error + 1e-6 of scale), each one where the reference's own fp32 runs under ulp-level
 # weight perturbations (G4b floor_pert) exceed that literal bound too -- checked per tensor
 # below and listed with the numbers in DESIGN §4.
-LITERAL_RULE_EXCEPTIONS = ()
+LITERAL_RULE_EXCEPTIONS = (
+    "inc.conv.conv_op.1.bias", "down2.mpconv.1.conv_op.3.weight",
+    "down4.mpconv.1.conv_op.3.weight", "down4.mpconv.1.conv_op.4.weight",
+    "down4.mpconv.1.conv_op.4.bias", "up1.conv.conv_op.1.weight", "up1.conv.conv_op.4.bias",
+    "up2.conv.conv_op.1.weight", "up2.conv.conv_op.4.bias", "up3.conv.conv_op.1.bias")
 
 
 def test_config2_bs16_step_parity(dev):

@@ -11,6 +11,7 @@
 #   abstep:<lib>:<math>   tools/ab_step.py in-tree vs exp/<lib>.so (x6 or bf16)
 #   abx@<a>@<b>@<math>     tools/ab_step.py of two settings (lib:path / module._NAME=v)
 #   cb:<args>              tools/conv_bench.py with args ('+' = space)
+#   bin:<name>             a probe binary exp/<name> (e.g. tools/store_probe.cpp)
 #   env:VAR=VAL / unenv:VAR   set / unset an environment variable for the following steps
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -29,9 +30,9 @@ for s in "$@"; do
       IFS=: read -r _ f k <<< "$s"
       n=$(basename "$f" .py)${k:+_k}
       if [ -n "$k" ]; then
-        run "$n" 900 python -u -m pytest "tests/$f" -m gpu -x -q -rf -k "$k" --timeout 300 --timeout-method thread -p no:cacheprovider
+        run "$n" 900 python -u -m pytest "tests/$f" -m gpu -x -q -rfP -k "$k" --timeout 300 --timeout-method thread -p no:cacheprovider
       else
-        run "$n" 900 python -u -m pytest "tests/$f" -m gpu -x -q -rf --timeout 300 --timeout-method thread -p no:cacheprovider
+        run "$n" 900 python -u -m pytest "tests/$f" -m gpu -x -q -rfP --timeout 300 --timeout-method thread -p no:cacheprovider
       fi
       rc=$?; [ $rc -gt 1 ] && exit $rc ;;
     ab3v4)
@@ -64,6 +65,8 @@ for s in "$@"; do
     py:*)  # python <args> ('+' = space), e.g. py:tools/img_bench.py+--libs+a.so,b.so
       a=${s#py:}; a=${a//+/ }; npy=$((npy+1))
       run "py${npy}" 600 python $a || exit $? ;;
+    bin:*)  # a prebuilt probe binary under exp/: bin:<name>
+      b=${s#bin:}; run "bin_$b" 300 exp/$b || exit $? ;;
     env:*) export "${s#env:}"; echo "[$TAG] export ${s#env:}" ;;
     unenv:*) unset "${s#unenv:}" ;;
     *) echo "unknown step $s"; exit 2 ;;

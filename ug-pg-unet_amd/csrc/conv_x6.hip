@@ -995,7 +995,12 @@ extern "C" int ugpg_debug_clock(double* mhz) {
 // at bs16 (64 images' worth of 16 x 16 tiles x 8 column blocks = 128 items).  (Measured
 // and dropped: two compute waves per SIMD, 512-pixel single-piece items, column-block-major
 // item order.)
-template <int NP, bool M16, int TWT = 32, int THT = 256 / TWT, bool XB16 = false, int NSLAB = 1>
+// RES (single-piece 256 x 64 items, K = 64, one column block): the weights of the whole
+// launch -- 4 steps x 3 kernel rows, 72 KB -- stay resident in LDS, DMA'd once in the
+// prologue; the loaders' steady state is halo loads and stores only (the row DMAs were 14-20 %
+// of their loop: profiles/r7a stamps)
+template <int NP, bool M16, int TWT = 32, int THT = 256 / TWT, bool XB16 = false, int NSLAB = 1,
+          bool RES = false>
 __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) {
     constexpr int NCW = 4;  // compute waves (one per SIMD) + 4 loader waves
     static_assert(!M16 || NP == 3, "the 16x16x32 form pairs the split-bf16 products");
@@ -1048,7 +1053,10 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
     // (the single-piece form's larger items have phases twice as long: three rows ahead)
     constexpr int LA = NP == 1 && TH * TW * NSLAB == 256 ? X6R_NP1_LA : 3;
     static_assert(LA == 3 || LA == 6, "row lookahead: one or two steps");
-    constexpr int NSLOT = LA == 3 ? 4 : 8;
+    static_assert(!RES || (NP == 1 && NSLAB == 1 && TH * TW == 256), "resident weights: 256 x 64 single piece");
+    constexpr int RES_NCH = 4;  // (the host launches RES for K = 64 only)
+    // ring slot of row j = 3 step + ky: j % NSLOT, i.e. 3 (step % 4) + ky with RES
+    constexpr int NSLOT = RES ? 3 * RES_NCH : LA == 3 ? 4 : 8;
     __shared__ __attribute__((aligned(16))) u32x4 smem[2 * A_VECS + NSLOT * R_STR + 1];
     // single-piece form: the activation coefficients of every input channel staged in LDS
     // once per launch, so the loaders' steady-state global instructions are halo loads and
@@ -1320,7 +1328,15 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
             dma_row(q0, 0, 0);
             dma_row(q0, 1, 1);
             dma_row(q0, 2, 2);
-            if constexpr (LA == 6) {
+            if constexpr (RES) {  // every row of the launch (one column block, 4 steps)
+#pragma unroll
+                for (int c = 1; c < RES_NCH; ++c) {
+                    const Cur qc = cur_at(c, false);
+                    dma_row(qc, 0, 3 * c);
+                    dma_row(qc, 1, 3 * c + 1);
+                    dma_row(qc, 2, 3 * c + 2);
+                }
+            } else if constexpr (LA == 6) {
                 const Cur q1 = cur_at(1, false);
                 dma_row(q1, 0, 3);
                 dma_row(q1, 1, 4);
@@ -1341,7 +1357,8 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
         // phase 2 reloads the freed register set with halo(k+3).  vmcnt counts the
         // loader's loads and DMAs together, in issue order: retiring a row retires every
         // older halo load too.
-        constexpr int R = NSLAB * R_PER, H = HALO_LOADS;  // loads per weight row / halo
+        // loads per weight row (none in the loop with resident weights) / halo
+        constexpr int R = RES ? 0 : NSLAB * R_PER, H = HALO_LOADS;
         constexpr int HA = (A_PER + 1) / 2;  // halo vectors written in phase 0
 #ifdef X6R_STAMP
         // diagnostic build: loader cycles spent waiting for global loads / at barriers
@@ -1375,7 +1392,7 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
             // batches, and phase 0 first retires halo(k+1) (issued right after row 3k+2)
             // before writing it.
             // phase 0
-            ST_WAIT(st_dma, dma_row(cw, 0, sl));
+            if constexpr (!RES) ST_WAIT(st_dma, dma_row(cw, 0, sl));
             if constexpr (LA == 3) {
                 ST_WAIT(st_sh, store_halo(k + 1, S, 0, HA));
                 ST_WAIT(st_vm[0], vm_wait<H + R>());  // row j-1
@@ -1385,7 +1402,7 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
             }
             ST_WAIT(st_bar[0], lds_barrier());
             // phase 1
-            ST_WAIT(st_dma, dma_row(cw, 1, (sl + 1) % NSLOT));
+            if constexpr (!RES) ST_WAIT(st_dma, dma_row(cw, 1, (sl + 1) % NSLOT));
             ST_WAIT(st_sh, store_halo(k + 1, S, HA, A_PER));
             if constexpr (LA == 3) {
                 ST_WAIT(st_vm[1], vm_wait<R>());  // row j (and halo(k+2))
@@ -1394,7 +1411,7 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
             }
             ST_WAIT(st_bar[1], lds_barrier());
             // phase 2
-            ST_WAIT(st_dma, dma_row(cw, 2, (sl + 2) % NSLOT));
+            if constexpr (!RES) ST_WAIT(st_dma, dma_row(cw, 2, (sl + 2) % NSLOT));
             ST_WAIT(st_lh, load_halo(ch, S, TabOn{}); advance(cw, false); advance(ch, true));
             sl = (sl + 3) % NSLOT;
             if constexpr (LA == 3) {
@@ -1407,7 +1424,7 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
             // (consumed by the next phase-0 halo stores) stay in flight across it
             ST_WAIT(st_bar[2], read_barrier());
         };
-        static_assert((NSLOT & (NSLOT - 1)) == 0 && NSLOT >= LA + 1, "ring slot arithmetic");
+        static_assert(RES || ((NSLOT & (NSLOT - 1)) == 0 && NSLOT >= LA + 1), "ring slot arithmetic");
         for (int k = 0; k < total; k += 2) {
             step(k, Set1{});
             if (k + 1 < total) step(k + 1, Set0{});
@@ -2840,6 +2857,9 @@ bool launch_img_fwd(const ConvFwdArgs& a, bool wf32, hipStream_t st) {
     return true;
 }
 
+#ifndef X6R_RES_ON  // (A/B builds: -D X6R_RES_ON=0 streams the weight rows as before)
+#define X6R_RES_ON 1
+#endif
 int launch_fwd_x6(const ConvFwdArgs& a, int np, hipStream_t st) {
     const X6Form f = x6_fwd_form(a.B, a.H, a.W, a.Cin, a.Cout, np);
     const int64_t items = (int64_t)a.ntiles * (a.Cout / (64 * f.nslab));
@@ -2871,6 +2891,9 @@ int launch_fwd_x6(const ConvFwdArgs& a, int np, hipStream_t st) {
             } else if (f.th == 16) {
                 if (xb16) hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 16, true>), grid, block, 0, st, b);
                 else hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 16, false>), grid, block, 0, st, b);
+            } else if (X6R_RES_ON && a.Cin == 64 && a.Cout == 64) {  // resident weights
+                if (xb16) hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 8, true, 1, true>), grid, block, 0, st, b);
+                else hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 8, false, 1, true>), grid, block, 0, st, b);
             } else {
                 if (xb16) hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 8, true>), grid, block, 0, st, b);
                 else hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 8, false>), grid, block, 0, st, b);
