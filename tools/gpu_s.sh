@@ -53,6 +53,9 @@ for s in "$@"; do
     stamps:*)  # in-kernel loader/compute stamps of exp/lib_stamp.so (-D X6R_STAMP=1), math x6 or bf16
       m=${s#stamps:}; ns=$((ns+1))
       run "stamps${ns}_$m" 300 env UGPG_LIB=exp/lib_stamp.so python tools/clock_probe.py --stamps --seconds 1 --math $m $( [ "$m" = bf16 ] && echo --out16 ) --layers inc.3,down1.3,down2.3,down3.3,up4.0 || exit $? ;;
+    stampsl:*)  # stamps of another stamp build: stampsl:<exp lib name>:<math>
+      IFS=: read -r _ l m <<< "$s"; ns=$((ns+1))
+      run "stamps${ns}_${l}_$m" 300 env UGPG_LIB=exp/$l.so python tools/clock_probe.py --stamps --seconds 1 --math $m $( [ "$m" = bf16 ] && echo --out16 ) --layers inc.3,down1.3,down2.3,down3.3,up4.0 || exit $? ;;
     wstamps:*)  # weight-gradient loader stamps of exp/lib_wstamp.so (-D X6W_STAMP=1)
       m=${s#wstamps:}; ns=$((ns+1))
       run "wstamps${ns}_$m" 300 env UGPG_LIB=exp/lib_wstamp.so python tools/clock_probe.py --stamps --wgrad --seconds 1 --math $m $( [ "$m" = bf16 ] && echo --out16 ) --layers inc.3,down1.3,down2.3,down3.3,up4.0 || exit $? ;;

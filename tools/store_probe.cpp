@@ -115,6 +115,8 @@ __global__ void __launch_bounds__(256) conv_like_kernel(float* out, int items_pe
     if (x == 12345.f) out[0] = x;
 }
 
+constexpr int SPIN = 600;
+
 int main() {
     const int wgs = 256, items = 16;
     const size_t n = (size_t)wgs * items * 256 * 64;
@@ -126,6 +128,21 @@ int main() {
     const char* names[4] = {"A fragment (16 px x 64 B)", "B rows (8 px x 128 B)", "C = A non-temporal",
                             "D = B non-temporal"};
     // per-CU limit or chip-wide bandwidth: the same per-workgroup work on 256, 128, 64, 32 CUs
+    for (int ng : {32}) {  // pattern B (8 px x 128 B: whole lines, not contiguous) per CU
+        std::vector<float> ts;
+        for (int r = 0; r < 20; ++r) {
+            (void)hipEventRecord(e0);
+            hipLaunchKernelGGL(store_kernel<1>, dim3(ng), dim3(256), 0, 0, out, items, 1.f);
+            (void)hipEventRecord(e1);
+            (void)hipEventSynchronize(e1);
+            float ms = 0.f;
+            (void)hipEventElapsedTime(&ms, e0, e1);
+            ts.push_back(ms);
+        }
+        std::sort(ts.begin(), ts.end());
+        const double ms = ts[ts.size() / 2];
+        printf("B on %3d workgroups: %8.1f us  %7.0f ns per item per CU\n", ng, ms * 1e3, ms * 1e6 / items);
+    }
     for (int ng : {256, 128, 64, 32}) {
         std::vector<float> ts;
         for (int r = 0; r < 20; ++r) {
@@ -173,7 +190,7 @@ int main() {
             printf("%2d storing waves, %3d workgroups (whole 1-KiB runs): %7.1f us  %7.0f ns per item per CU\n",
                    1 << i, wgs2, t[i] * 1e3, t[i] * 1e6 / items);
     }
-    // conv-like: ~13 us of compute per item (spin tuned below), 16 items, all 256 CUs
+    // conv-like: ~10 us of compute per item (SPIN), 16 items, all 256 CUs
     for (int stagger : {0, 1}) {
         for (int pat = 0; pat < 3; ++pat) {
             double t[2];
@@ -181,9 +198,9 @@ int main() {
                 std::vector<float> ts;
                 for (int r = 0; r < 7; ++r) {
                     (void)hipEventRecord(e0);
-                    if (pat == 0) hipLaunchKernelGGL(conv_like_kernel<0>, dim3(wgs), dim3(256), 0, 0, out, items, 6000, stagger, ds);
-                    if (pat == 1) hipLaunchKernelGGL(conv_like_kernel<1>, dim3(wgs), dim3(256), 0, 0, out, items, 6000, stagger, ds);
-                    if (pat == 2) hipLaunchKernelGGL(conv_like_kernel<2>, dim3(wgs), dim3(256), 0, 0, out, items, 6000, stagger, ds);
+                    if (pat == 0) hipLaunchKernelGGL(conv_like_kernel<0>, dim3(wgs), dim3(256), 0, 0, out, items, SPIN, stagger, ds);
+                    if (pat == 1) hipLaunchKernelGGL(conv_like_kernel<1>, dim3(wgs), dim3(256), 0, 0, out, items, SPIN, stagger, ds);
+                    if (pat == 2) hipLaunchKernelGGL(conv_like_kernel<2>, dim3(wgs), dim3(256), 0, 0, out, items, SPIN, stagger, ds);
                     (void)hipEventRecord(e1);
                     (void)hipEventSynchronize(e1);
                     float ms = 0.f;

@@ -976,7 +976,7 @@ extern "C" int ugpg_conv3x3_fwd(const ugpg_conv_t* p, void* stream) {
     hipStream_t st = as_stream(stream);
     if (split) {
         const int np = p->wfmt == UGPG_WFMT_X6 ? 3 : 1;
-        if (np == 1 && p->W >= 32 && C0 + C1 > 2048) {  // X6R_CTAB_MAX (conv_x6.hip)
+        if (np == 1 && p->W >= 16 && C0 + C1 > 2048) {  // X6R_CTAB_MAX (conv_x6.hip)
             set_error("conv3x3_fwd: the bf16 persistent form takes at most 2048 input channels");
             return UGPG_ERR_INVALID;
         }
