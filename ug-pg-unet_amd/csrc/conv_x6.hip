@@ -469,12 +469,8 @@ __device__ __forceinline__ void x6_dma_bnb_y(const ConvFwdArgs& a, int b, int ty
 // path, and its registers, out of them).  FW: the tile is known to lie wholly inside the
 // image width (the caller's uniform branch), so no store or statistics term carries a
 // per-pixel column guard (each was an exec-mask branch per value)
-// PH (the 4 x 2-tile single-piece forms' paired store, round 6; the host launches those
-// kernels with PAIR only for a bf16-only output without BatchNorm-backward partials or
-// accumulate): 0 = the whole epilogue; 1 = the bias, rounding and statistics but no store --
-// the caller then stores both n-tiles together (x6_store16_pair)
-template <int TH, int TW, int MT, int WM = 2, bool Y32 = true, bool FW = false, int PH = 0>
-__device__ __forceinline__ bool x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&acc)[MT], int tile,
+template <int TH, int TW, int MT, int WM = 2, bool Y32 = true, bool FW = false>
+__device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&acc)[MT], int tile,
                                                  int b, int ty0, int tx0, int c0, int wm,
                                                  float* stg) {
     static_assert(TW == 32, "one image row per 32-pixel MFMA tile");
@@ -587,32 +583,11 @@ __device__ __forceinline__ bool x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
             asm volatile("" ::: "memory");  // the next m-tile's staging writes after these reads
         }
     };
-    // rounding (with bias) and the statistics sum of a joint store, without storing
-    auto round_rows = [&]() {
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-            if (wm * MT + mt >= vh) break;  // uniform
-#pragma unroll
-            for (int r = 0; r < 16; r += 2) {
-                float v0, v1;
-                pk_bf16(acc[mt][r] + bv, acc[mt][r + 1] + bv, v0, v1);
-                acc[mt][r] = v0;
-                acc[mt][r + 1] = v1;
-                const int p0 = (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (fullw || p0 < vw) psum += v0;
-                if (fullw || p0 + 1 < vw) psum += v1;
-            }
-        }
-    };
     const bool bnb = a.bnb_part != nullptr && !oacc;  // (the host refuses bnb + accumulate)
     EPI_T(et0);
-    if constexpr (PH == 1) {
-        round_rows();
-    } else {
-        if (oacc) store_rows(std::integral_constant<bool, true>{}, 0, MT);
-        else if (only16 && !bnb) store16_rows(std::false_type{});
-        else if (!bnb) store_rows(std::integral_constant<bool, false>{}, 0, MT);
-    }
+    if (oacc) store_rows(std::integral_constant<bool, true>{}, 0, MT);
+    else if (only16 && !bnb) store16_rows(std::false_type{});
+    else if (!bnb) store_rows(std::integral_constant<bool, false>{}, 0, MT);
     EPI_T(et1);
     if (bnb) {
         // BatchNorm-backward partials of the stored output (as x6q_epilogue_wave): this
@@ -705,11 +680,11 @@ __device__ __forceinline__ bool x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
             a.bnb_part[(1 * (size_t)a.Cout + n) * S + slot] = sgx;
             a.bnb_part[(2 * (size_t)a.Cout + n) * S + slot] = sx;
         }
-        return true;
+        return;
     }
-    if (a.stats == nullptr) return false;
+    if (a.stats == nullptr) return;
 #ifdef X6Q_NOSTATS
-    return false;
+    return;
 #endif
     constexpr int WROWS = MT * 32 / TW;  // image rows of one wave's pixels
     const int rows = min(max(vh - wm * WROWS, 0), WROWS);
@@ -737,69 +712,6 @@ __device__ __forceinline__ bool x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
         a.stats[(2 * (size_t)a.Cout + n) * S + slot] = q;
     }
     EPI_REC(et0, et1);
-    return false;
-}
-
-// The paired bf16 store of a 4 x 2-tile wave (x6_epilogue_wave<..., PH = 1> rounded both
-// n-tiles): per m-tile each n-tile goes through its own staging area as in store16_rows (lane
-// (q, k) reads pixel q + 16j, channels 8k..8k+7: half a 128-B line), then a DPP exchange between
-// lanes l and l ^ 4 (pixels q and q ^ 1) pairs the two halves of a line: X = even pixels, Y =
-// odd pixels, lane l holding channels 32 (q & 1) + 8k.. of its pixel -- 8 pixels x 128 B, whole
-// lines, per store instruction (a CU retires whole-line stores 2.5x as fast as half lines:
-// tools/store_probe.cpp).  Same values, same bytes, same number of store instructions.
-template <int TH, int TW, int MT>
-__device__ __forceinline__ void x6_store16_pair(const ConvFwdArgs& a, const f32x16 (&acc0)[MT],
-                                                const f32x16 (&acc1)[MT], int b, int ty0, int tx0,
-                                                int c0, int wm, float* stg0, float* stg1) {
-    static_assert(TW == 32, "one image row per 32-pixel MFMA tile");
-    const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
-    const int vh = min(TH, a.H - ty0), vw = min(TW, a.W - tx0);
-    const int ostride = a.Cout;  // (bf16-only output: one output, no split)
-    const int q = (lane >> 2) & 15, k = lane & 3;
-    auto pk = [](float x, float y) {  // exact bf16 values: the packed words are bit selections
-        return (__builtin_bit_cast(unsigned, x) >> 16) | (__builtin_bit_cast(unsigned, y) & 0xffff0000u);
-    };
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-        const int py = wm * MT + mt;
-        if (py >= vh) break;  // uniform
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int p = (r & 3) + 8 * (r >> 2) + 4 * h;
-            stg0[p * X6_STG_PITCH + l32] = acc0[mt][r];
-            stg1[p * X6_STG_PITCH + l32] = acc1[mt][r];
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        u32x4 w0[2], w1[2];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int p = (lane >> 2) + 16 * j;
-            const float* s0 = stg0 + p * X6_STG_PITCH + 8 * k;
-            const float* s1 = stg1 + p * X6_STG_PITCH + 8 * k;
-            const f32x4 a0 = *reinterpret_cast<const f32x4*>(s0), b0 = *reinterpret_cast<const f32x4*>(s0 + 4);
-            const f32x4 a1 = *reinterpret_cast<const f32x4*>(s1), b1 = *reinterpret_cast<const f32x4*>(s1 + 4);
-            w0[j] = u32x4{pk(a0.x, a0.y), pk(a0.z, a0.w), pk(b0.x, b0.y), pk(b0.z, b0.w)};
-            w1[j] = u32x4{pk(a1.x, a1.y), pk(a1.z, a1.w), pk(b1.x, b1.y), pk(b1.z, b1.w)};
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done: the next m-tile's writes
-        const size_t rowb = (size_t)((b * a.H + ty0 + py) * a.W + tx0) * ostride + c0 + 32 * (q & 1) + 8 * k;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            u32x4 x, y;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                // odd-pixel lanes (banks 1, 3 of each row) take lane l - 4's n-tile-1 half
-                // (row_ror:4), even-pixel lanes (banks 0, 2) lane l + 4's n-tile-0 half (row_ror:12)
-                x[i] = (unsigned)__builtin_amdgcn_update_dpp((int)w0[j][i], (int)w1[j][i], 0x124, 0xF, 0xA, false);
-                y[i] = (unsigned)__builtin_amdgcn_update_dpp((int)w1[j][i], (int)w0[j][i], 0x12C, 0xF, 0x5, false);
-            }
-            const int px = (q & ~1) + 16 * j, py1 = (q | 1) + 16 * j;
-            if (px < vw)
-                __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(a.out0_16 + rowb + (size_t)px * ostride));
-            if (py1 < vw)
-                __builtin_nontemporal_store(y, reinterpret_cast<u32x4*>(a.out0_16 + rowb + (size_t)py1 * ostride));
-        }
-    }
 }
 
 // Epilogue of the 16x16x32 form: acc[mt][nt] is D[oc][px] of m-tile mt (16 pixels:
@@ -855,61 +767,6 @@ __device__ __forceinline__ void x6q_epilogue_wave(const ConvFwdArgs& a,
             const int py = wm * WR + prow(mt), px = pcol(mt) + l16;
             if (py >= vh) break;  // uniform
             const bool ok = px < vw;
-#ifndef X6Q_WHOLELINE  // (pending its GPU A/B: -D X6Q_WHOLELINE=1 builds the whole-line stores)
-#define X6Q_WHOLELINE 0
-#endif
-#if X6Q_WHOLELINE
-            // Whole 128-B lines per store instruction (round 6): a fragment store writes 16 pixels
-            // x 64 B (half a line each, nt = 0 or 1), and one CU retires those at ~31 GB/s, whole
-            // lines at ~78 (tools/store_probe.cpp, profiles/r7a_store_probe.txt: 2.1 vs 0.84 us per
-            // 64 KB item).  A row_ror:8 DPP exchange of the two n-tile vectors between lanes l and
-            // l ^ 8 of each 16-lane row gives w[0] = pixels 0-7 and w[1] = pixels 8-15 of the
-            // m-tile, lane l holding pixel l & 7's channels 16 (l >> 3) + 4g..: 8 pixels x the
-            // wave's 32 channels (one 128-B line each) per instruction.  Same values, same bytes.
-            {
-                f32x4 v[2];
-#pragma unroll
-                for (int nt = 0; nt < 2; ++nt) {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) v[nt][i] = acc[mt][nt][i] + bv[nt][i];
-                    acc[mt][nt] = v[nt];
-                    if (ok) {
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) psum[nt][i] += v[nt][i];
-                    }
-                }
-                f32x4 w[2];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int b0 = __builtin_bit_cast(int, v[0][i]), b1 = __builtin_bit_cast(int, v[1][i]);
-                    // lanes 8-15 of each row (banks 2, 3) take lane l - 8's nt = 1 value, lanes 0-7
-                    // (banks 0, 1) lane l + 8's nt = 0 value
-                    w[0][i] = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(b0, b1, 0x128, 0xF, 0xC, false));
-                    w[1][i] = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(b1, b0, 0x128, 0xF, 0x3, false));
-                }
-                const int pl = l16 & 7;
-                float* pb = out + (size_t)((b * a.H + ty0 + py) * a.W + tx0 + pcol(mt) + pl) * ostride +
-                            ocol0 + c0 + 16 * (l16 >> 3);
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-#ifdef X6Q_NOSTORE  // diagnostic build: no output stores (results are wrong)
-                    if (pcol(mt) + 8 * j + pl < vw && w[j][0] == 12345.f) {
-#else
-                    if (pcol(mt) + 8 * j + pl < vw) {
-#endif
-                        f32x4* q = reinterpret_cast<f32x4*>(pb + (size_t)(8 * j) * ostride);
-                        f32x4 o = w[j];
-                        if constexpr (ACC) {
-                            const f32x4 e = *q;
-#pragma unroll
-                            for (int i = 0; i < 4; ++i) o[i] += e[i];
-                        }
-                        *q = o;
-                    }
-                }
-                continue;
-            }
-#endif
             float* p = out + (size_t)((b * a.H + ty0 + py) * a.W + tx0 + px) * ostride + ocol0 + c0;
 #pragma unroll
             for (int nt = 0; nt < 2; ++nt) {
@@ -1142,10 +999,8 @@ extern "C" int ugpg_debug_clock(double* mhz) {
 // launch -- 4 steps x 3 kernel rows, 72 KB -- stay resident in LDS, DMA'd once in the
 // prologue; the loaders' steady state is halo loads and stores only (the row DMAs were 14-20 %
 // of their loop: profiles/r7a stamps)
-// PAIR (4 x 2-tile single-piece forms, bf16-only output without BatchNorm-backward partials):
-// the two n-tiles of a wave leave together as whole 128-B lines (x6_store16_pair)
 template <int NP, bool M16, int TWT = 32, int THT = 256 / TWT, bool XB16 = false, int NSLAB = 1,
-          bool RES = false, bool PAIR = false>
+          bool RES = false>
 __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) {
     constexpr int NCW = 4;  // compute waves (one per SIMD) + 4 loader waves
     static_assert(!M16 || NP == 3, "the 16x16x32 form pairs the split-bf16 products");
@@ -1941,21 +1796,6 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
 #else
             if (cp.tx0 + TW <= a.W) {  // (uniform) the common case: a full-width tile
 #endif
-                if constexpr (NT > 1 && PAIR) {
-                    // both n-tiles rounded, then (bf16-only output, no partials) stored together
-                    // as whole lines; otherwise each call stored its own
-                    auto pair_epi = [&]() {
-                        const int n0 = cp.nb * BNI + wn * NT * 32;
-                        float* s0 = ostg + wave * NT * X6_STG_WAVE;
-                        float* s1 = ostg + (wave * NT + 1) * X6_STG_WAVE;
-                        x6_epilogue_wave<TH, TW, MT, WM, false, true, 1>(a, acc[0], cp.tile, cp.b, cp.ty0,
-                                                                         cp.tx0, n0, wm, s0);
-                        x6_epilogue_wave<TH, TW, MT, WM, false, true, 1>(a, acc[1], cp.tile, cp.b, cp.ty0,
-                                                                         cp.tx0, n0 + 32, wm, s1);
-                        x6_store16_pair<TH, TW, MT>(a, acc[0], acc[1], cp.b, cp.ty0, cp.tx0, n0, wm, s0, s1);
-                    };
-                    CS_WAIT(cs_epi, pair_epi());
-                } else {
                 CS_WAIT(cs_epi, (x6_epilogue_wave<TH, TW, MT, WM, NT == 1, true>(
                                     a, acc[0], cp.tile, cp.b, cp.ty0, cp.tx0, cp.nb * BNI + wn * NT * 32,
                                     wm, ostg + wave * NT * X6_STG_WAVE)));
@@ -1964,7 +1804,6 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
                                         a, acc[1], cp.tile, cp.b, cp.ty0, cp.tx0,
                                         cp.nb * BNI + (wn * NT + 1) * 32, wm,
                                         ostg + (wave * NT + 1) * X6_STG_WAVE)));
-                }
             } else {
                 CS_WAIT(cs_epi, (x6_epilogue_wave<TH, TW, MT, WM, NT == 1>(
                                     a, acc[0], cp.tile, cp.b, cp.ty0, cp.tx0, cp.nb * BNI + wn * NT * 32,
@@ -3083,22 +2922,13 @@ int launch_fwd_x6(const ConvFwdArgs& a, int np, hipStream_t st) {
             const bool wide = f.nslab == 2 || f.th == 16;
             const bool nofuse = wide && a.bnb_part && !a.bnb_y.h;
             if (nofuse) b.bnb_part = nullptr;
-#ifndef X6_PAIR_ON  // (pending its GPU A/B: -D X6_PAIR_ON=1 builds the paired stores)
-#define X6_PAIR_ON 0
-#endif
-            // the paired whole-line store: bf16 sources and a bf16-only output (the bf16
-            // arithmetic's forward), no partials, no accumulate
-            const bool pair = X6_PAIR_ON && xb16 && !b.out0 && b.out0_16 && !b.bnb_part && !b.acc0 &&
-                              b.split == b.Cout;
             if (f.tw == 16) {  // (16-wide sources are fp32: ugpg_conv3x3_fwd)
                 hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 16, 8, false>), grid, block, 0, st, b);
             } else if (f.nslab == 2) {
-                if (pair) hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 8, true, 2, false, true>), grid, block, 0, st, b);
-                else if (xb16) hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 8, true, 2>), grid, block, 0, st, b);
+                if (xb16) hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 8, true, 2>), grid, block, 0, st, b);
                 else hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 8, false, 2>), grid, block, 0, st, b);
             } else if (f.th == 16) {
-                if (pair) hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 16, true, 1, false, true>), grid, block, 0, st, b);
-                else if (xb16) hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 16, true>), grid, block, 0, st, b);
+                if (xb16) hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 16, true>), grid, block, 0, st, b);
                 else hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 16, false>), grid, block, 0, st, b);
             } else if (X6R_RES_ON && a.Cin == 64 && a.Cout == 64) {  // resident weights
                 if (xb16) hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 8, true, 1, true>), grid, block, 0, st, b);
