@@ -52,13 +52,13 @@ for s in "$@"; do
       nc=$((nc+1)); run "convbench${nc}" 600 python tools/conv_bench.py $a || exit $? ;;
     stamps:*)  # in-kernel loader/compute stamps of exp/lib_stamp.so (-D X6R_STAMP=1), math x6 or bf16
       m=${s#stamps:}; ns=$((ns+1))
-      run "stamps${ns}_$m" 300 env UGPG_LIB=exp/lib_stamp.so python tools/clock_probe.py --stamps --seconds 1 --math $m $( [ "$m" = bf16 ] && echo --out16 ) --layers inc.3,down1.3,down2.3,down3.3,up4.0 || exit $? ;;
+      run "stamps${ns}_$m" 300 env UGPG_LIB=exp/lib_stamp.so python tools/clock_probe.py --stamps --seconds 1 --math $m $( [ "$m" = bf16 ] && echo --out16 ) --layers ${STAMP_LAYERS:-inc.3,down1.3,down2.3,down3.3,up4.0} || exit $? ;;
     stampsl:*)  # stamps of another stamp build: stampsl:<exp lib name>:<math>
       IFS=: read -r _ l m <<< "$s"; ns=$((ns+1))
-      run "stamps${ns}_${l}_$m" 300 env UGPG_LIB=exp/$l.so python tools/clock_probe.py --stamps --seconds 1 --math $m $( [ "$m" = bf16 ] && echo --out16 ) --layers inc.3,down1.3,down2.3,down3.3,up4.0 || exit $? ;;
+      run "stamps${ns}_${l}_$m" 300 env UGPG_LIB=exp/$l.so python tools/clock_probe.py --stamps --seconds 1 --math $m $( [ "$m" = bf16 ] && echo --out16 ) --layers ${STAMP_LAYERS:-inc.3,down1.3,down2.3,down3.3,up4.0} || exit $? ;;
     wstamps:*)  # weight-gradient loader stamps of exp/lib_wstamp.so (-D X6W_STAMP=1)
       m=${s#wstamps:}; ns=$((ns+1))
-      run "wstamps${ns}_$m" 300 env UGPG_LIB=exp/lib_wstamp.so python tools/clock_probe.py --stamps --wgrad --seconds 1 --math $m $( [ "$m" = bf16 ] && echo --out16 ) --layers inc.3,down1.3,down2.3,down3.3,up4.0 || exit $? ;;
+      run "wstamps${ns}_$m" 300 env UGPG_LIB=exp/lib_wstamp.so python tools/clock_probe.py --stamps --wgrad --seconds 1 --math $m $( [ "$m" = bf16 ] && echo --out16 ) --layers ${STAMP_LAYERS:-inc.3,down1.3,down2.3,down3.3,up4.0} || exit $? ;;
     abstep:*)  # in-process whole-step A/B: in-tree library vs exp/<lib>.so, arithmetic m
       IFS=: read -r _ l m <<< "$s"; na=$((na+1))
       run "abstep${na}_${l}_$m" 600 python tools/ab_step.py --a lib:ug-pg-unet_amd/ugpg/libugpg.so --b lib:exp/$l.so --conv-math $m --rounds 6 || exit $? ;;

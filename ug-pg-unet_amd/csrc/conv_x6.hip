@@ -442,6 +442,9 @@ __device__ unsigned long long g_epi[512 * 4];
 #define EPI_T(v)
 #define EPI_REC(t0, t1)
 #endif
+#ifndef X6R_PAIR16  // (A/B build: X6R_PAIR16=0, each n-tile through x6_epilogue_wave)
+#define X6R_PAIR16 1
+#endif
 constexpr int X6_STG_PITCH = 40;
 constexpr int X6_STG_WAVE = 2048;  // floats: 32 x 40 fp32, or the bf16 y tile of 4 m-tiles
 // BatchNorm-backward partials with bf16 y: the item's y tile (MT m-tiles x 32 pixels x the
@@ -710,6 +713,96 @@ __device__ __forceinline__ void x6_epilogue_wave(const ConvFwdArgs& a, f32x16 (&
         a.stats[(0 * (size_t)a.Cout + n) * S + slot] = cnt;
         a.stats[(1 * (size_t)a.Cout + n) * S + slot] = s;
         a.stats[(2 * (size_t)a.Cout + n) * S + slot] = q;
+    }
+    EPI_REC(et0, et1);
+}
+
+// The 4 x 2-tile single-piece forms' common epilogue -- bf16-only output, no accumulate, no
+// BatchNorm-backward partials, a full-width tile: the wave's two n-tiles are one pixel's 64
+// channels, i.e. one whole 128-B line of the bf16 output, so each m-tile leaves as 4 store
+// instructions of 8 lanes x 16 B per line (x6_epilogue_wave per n-tile writes half lines:
+// a CU retires those at ~31 GB/s against ~78 GB/s for whole lines, tools/store_probe.cpp).
+// Staging pitch 32 floats and the second n-tile's area 4 dwords off: conflict-free for the
+// stores (ds_write_b32) and for the line reads (ds_read_b128 lane groups).  The
+// BatchNorm partials are taken in one pass as shifted sums (K = a value of the channel,
+// d = v - K: sum = n K + sum d, M2 = sum d^2 - (sum d)^2 / n), so each m-tile's
+// accumulators die once staged; the two-pass form held all of them to its second pass (the
+// round-6 paired store that rounded both tiles first spilled 480 B).
+template <int TH, int TW, int MT, int WM>
+__device__ __forceinline__ void x6_epilogue_pair16(const ConvFwdArgs& a, f32x16 (&acc0)[MT],
+                                                   f32x16 (&acc1)[MT], int tile, int b, int ty0,
+                                                   int tx0, int c0, int wm, float* stg) {
+    static_assert(TW == 32, "one image row per 32-pixel MFMA tile");
+    constexpr int P = 32;
+    const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
+    const int vh = min(TH, a.H - ty0);
+    float* const stg1 = stg + X6_STG_WAVE + 4;
+    const float bv0 = a.bias ? a.bias[c0 + l32] : 0.f, bv1 = a.bias ? a.bias[c0 + 32 + l32] : 0.f;
+    // the shift of channel c0 + l32 (+ 32): lane l32's first value, the same in both halves
+    const float k0 = __shfl(acc0[0][0] + bv0, l32, 64), k1 = __shfl(acc1[0][0] + bv1, l32, 64);
+    float s0 = 0.f, q0 = 0.f, s1 = 0.f, q1 = 0.f;
+    auto pk = [](float x, float y) {  // exact bf16 values: the packed words are bit selections
+        return (__builtin_bit_cast(unsigned, x) >> 16) | (__builtin_bit_cast(unsigned, y) & 0xffff0000u);
+    };
+    const int k = lane & 7;
+    const float* const sk = (k < 4 ? stg : stg1) + 8 * (k & 3);
+    EPI_T(et0);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        const int py = wm * MT + mt;
+        if (py >= vh) break;  // uniform
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+            const int p0 = (r & 3) + 8 * (r >> 2) + 4 * h;  // r + 1: pixel p0 + 1
+            float v0, v1, w0, w1;
+            pk_bf16(acc0[mt][r] + bv0, acc0[mt][r + 1] + bv0, v0, v1);
+            pk_bf16(acc1[mt][r] + bv1, acc1[mt][r + 1] + bv1, w0, w1);
+            float d = v0 - k0;
+            s0 += d;
+            q0 = fmaf(d, d, q0);
+            d = v1 - k0;
+            s0 += d;
+            q0 = fmaf(d, d, q0);
+            d = w0 - k1;
+            s1 += d;
+            q1 = fmaf(d, d, q1);
+            d = w1 - k1;
+            s1 += d;
+            q1 = fmaf(d, d, q1);
+            stg[p0 * P + l32] = v0;
+            stg[(p0 + 1) * P + l32] = v1;
+            stg1[p0 * P + l32] = w0;
+            stg1[(p0 + 1) * P + l32] = w1;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const size_t rowb = (size_t)((b * a.H + ty0 + py) * a.W + tx0) * a.Cout + c0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int p = (lane >> 3) + 8 * j;
+            const f32x4 lo = *reinterpret_cast<const f32x4*>(sk + p * P);
+            const f32x4 hi = *reinterpret_cast<const f32x4*>(sk + p * P + 4);
+            const u32x4 w = {pk(lo.x, lo.y), pk(lo.z, lo.w), pk(hi.x, hi.y), pk(hi.z, hi.w)};
+            __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(a.out0_16 + rowb + (size_t)p * a.Cout + 8 * k));
+        }
+        asm volatile("" ::: "memory");  // the next m-tile's staging writes after these reads
+    }
+    EPI_T(et1);
+    s0 += __shfl_xor(s0, 32, 64);
+    q0 += __shfl_xor(q0, 32, 64);
+    s1 += __shfl_xor(s1, 32, 64);
+    q1 += __shfl_xor(q1, 32, 64);
+    if (a.stats != nullptr && lane < 32) {
+        const int rows = min(max(vh - wm * MT, 0), MT);
+        const float cnt = (float)(rows * TW);
+        const size_t S = WM * (size_t)a.ntiles, slot = WM * (size_t)tile + wm;
+        auto put = [&](int n, float kk, float s, float q) {
+            const bool any = cnt > 0.f;
+            a.stats[(0 * (size_t)a.Cout + n) * S + slot] = cnt;
+            a.stats[(1 * (size_t)a.Cout + n) * S + slot] = any ? fmaf(cnt, kk, s) : 0.f;
+            a.stats[(2 * (size_t)a.Cout + n) * S + slot] = any ? fmaxf(q - s * (s / cnt), 0.f) : 0.f;
+        };
+        put(c0 + l32, k0, s0, q0);
+        put(c0 + 32 + l32, k1, s1, q1);
     }
     EPI_REC(et0, et1);
 }
@@ -1000,7 +1093,7 @@ extern "C" int ugpg_debug_clock(double* mhz) {
 // prologue; the loaders' steady state is halo loads and stores only (the row DMAs were 14-20 %
 // of their loop: profiles/r7a stamps)
 template <int NP, bool M16, int TWT = 32, int THT = 256 / TWT, bool XB16 = false, int NSLAB = 1,
-          bool RES = false>
+          bool RES = false, bool PAIR = false>
 __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) {
     constexpr int NCW = 4;  // compute waves (one per SIMD) + 4 loader waves
     static_assert(!M16 || NP == 3, "the 16x16x32 form pairs the split-bf16 products");
@@ -1028,11 +1121,21 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
     constexpr int WM = M16 || TH * TW < 256 ? 2 : TH * TW / 128, WN = NCW / WM, MR = 32 / TW,
                   MT = M16 ? TH / 2 : TH * TW / (32 * WM), NT = M16 ? 1 : BNI / (32 * WN);
     static_assert(M16 || (WM * WN == NCW && NT >= 1 && MT * WM * 32 == TH * TW), "wave grid");
-    constexpr int HWD = TW + 2, HS = HWD;
+    // halo row pitch HS in 16-B pixel slots.  The single-piece 16-wide form's A fragment
+    // is two image rows (lanes 0-15 / 16-31): a ds_read_b128 lane group {0-3,12-15,20-27}
+    // then holds pixels 0-3, 12-15 of one row and 4-11 of the next, conflict-free only
+    // when HS = 0 (mod 16) -- the dense pitch 18 made every A read 2-way in each group
+    // (2.18 conflict cycles per LDS instruction, profiles/r7b_bf16_summary.md)
+#ifndef X6R_W16_HS  // (A/B build: X6R_W16_HS=18, the dense pitch)
+#define X6R_W16_HS 32
+#endif
+    constexpr int HWD = TW + 2, HS = TW == 16 && !M16 ? X6R_W16_HS : HWD;
+    static_assert(HS >= HWD, "halo row pitch");
     constexpr int NHALO = (TH + 2) * HWD;                   // 340 / 324 halo pixels
-    // spare slot NHALO; plane pitch 348 = 4 (mod 8) for the 32x32 fragment pattern, 352
+    constexpr int NSPARE = (TH + 2) * HS;                   // the idle lanes' slot
+    // spare slot NSPARE; plane pitch 348 = 4 (mod 8) for the 32x32 fragment pattern, 352
     // = 0 (mod 16) for the 16x16 one (ds_read_b128 lane groups, MI355X_MICROARCH.md §LDS)
-    constexpr int NHP = M16 ? (NHALO + 1 + 15) / 16 * 16 : NHALO + 1 + (11 - NHALO % 8) % 8;
+    constexpr int NHP = M16 ? (NSPARE + 1 + 15) / 16 * 16 : NSPARE + 1 + (11 - NSPARE % 8) % 8;
     // (halo pixel, channel half) items: lane group i of 16 takes 16 consecutive pixels of
     // one half (i & 1), so each 8-lane group of a halo ds_write_b128 stores 128 contiguous
     // bytes of one plane -- conflict-free (the two halves of a pixel sit 352 vectors apart,
@@ -1236,7 +1339,7 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
                         u32x4 w = __builtin_bit_cast(u32x4, ra[st][v][0]);
 #pragma unroll
                         for (int i = 0; i < 4; ++i) w[i] = ok ? w[i] : 0u;
-                        const int hl = hp < NHALO ? (hp / HWD) * HS + hp % HWD : NHALO;
+                        const int hl = hp < NHALO ? (hp / HWD) * HS + hp % HWD : NSPARE;
                         As[hhl * NHP + hl] = w;
                     }
                     return;
@@ -1272,7 +1375,7 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
                                      ok ? hi4.z : 0.f, ok ? hi4.w : 0.f};
                     split_n<NP>(x, pc);
                 }
-                const int hl = hp < NHALO ? (hp / HWD) * HS + hp % HWD : NHALO;
+                const int hl = hp < NHALO ? (hp / HWD) * HS + hp % HWD : NSPARE;
 #pragma unroll
                 for (int q = 0; q < NP; ++q) As[(q * 2 + hh) * NHP + hl] = pc[q];
             }
@@ -1779,7 +1882,14 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
         if (++cc == nchunk) {
             // (explicit calls: a loop around the inlined epilogue cost the allocator ~240
             // spilled registers)
-            if constexpr (TW == 16) {
+            if constexpr (PAIR) {
+                // (host: bf16-only output, no accumulate, no BatchNorm-backward partials, W % 32
+                // == 0) both n-tiles as whole lines; only this epilogue is compiled in
+                static_assert(NP == 1 && NT == 2 && TW == 32, "the 4 x 2-tile single-piece forms");
+                CS_WAIT(cs_epi, (x6_epilogue_pair16<TH, TW, MT, WM>(
+                                    a, acc[0], acc[1], cp.tile, cp.b, cp.ty0, cp.tx0,
+                                    cp.nb * BNI + wn * NT * 32, wm, ostg + wave * NT * X6_STG_WAVE)));
+            } else if constexpr (TW == 16) {
                 // 16-wide image (host: W == 16, H even): a 32-pixel m-tile is two whole image
                 // rows, so the NHWC addresses are those of a 32-wide image of half the rows --
                 // the 32-wide epilogue on that view, every tile full width
@@ -2348,23 +2458,35 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
                 bf[q] = u32x4{lo.x, lo.y, hi.x, hi.y};
             }
         };
-        // 2 rows x 9 taps as one sequence: the next tap's fragments (and the next row's
-        // dy fragments) are read during the current tap's MFMAs
-        u32x4 afr[2][NP], bfr[2][NP];
-        lda(0, afr[0]);
-        ldb(0, 0, bfr[0]);
+        // TH rows x 9 taps as one sequence: the fragments of unit u + BD (a tap; and the
+        // dy fragments of the next row) are read during unit u's MFMAs
+#ifndef X6W_BDEPTH3  // (A/B builds: read depth in units, split-bf16 / single-piece forms)
+#define X6W_BDEPTH3 1
+#endif
+#ifndef X6W_BDEPTH1
+#define X6W_BDEPTH1 1
+#endif
+        constexpr int BD = NP == 3 ? X6W_BDEPTH3 : X6W_BDEPTH1, NU = 9 * TH;
+        static_assert(BD >= 1 && BD <= 8, "read depth");
+        u32x4 afr[2][NP], bfr[BD + 1][NP];
+#pragma unroll
+        for (int v = 0; v < BD; ++v) {
+            if (v % 9 == 0) lda(v / 9, afr[(v / 9) & 1]);
+            ldb(v / 9, v % 9, bfr[v]);
+        }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int u = 0; u < 9 * TH; ++u) {
-            const int ks = u / 9, t = u % 9;
-            if (u + 1 < 9 * TH) {
-                if ((u + 1) % 9 == 0) lda((u + 1) / 9, afr[((u + 1) / 9) & 1]);
-                ldb((u + 1) / 9, (u + 1) % 9, bfr[(u + 1) & 1]);
+        for (int u = 0; u < NU; ++u) {
+            const int ks = u / 9, t = u % 9, un = u + BD;
+            // (row un/9's dy fragments go to the buffer row un/9 - 2 used: done, BD <= 8)
+            if (un < NU) {
+                if (un % 9 == 0) lda(un / 9, afr[(un / 9) & 1]);
+                ldb(un / 9, un % 9, bfr[un % (BD + 1)]);
             }
-            acc[t] = mfma_xn<NP>(afr[ks & 1], bfr[u & 1], acc[t]);
+            acc[t] = mfma_xn<NP>(afr[ks & 1], bfr[u % (BD + 1)], acc[t]);
             // next fragments (2 reads per piece, twice that at a row change) spread over
-            // the first half of the tap's MFMA gaps, so they land before the next tap
-            const bool more = u + 1 < 9 * TH, row = (u + 1) % 9 == 0;
+            // the first half of the tap's MFMA gaps
+            const bool more = un < NU, row = un % 9 == 0;
             if constexpr (NP == 3) {
 #pragma unroll
                 for (int i = 0; i < 6; ++i) {
@@ -2924,12 +3046,21 @@ int launch_fwd_x6(const ConvFwdArgs& a, int np, hipStream_t st) {
             if (nofuse) b.bnb_part = nullptr;
             if (f.tw == 16) {  // (16-wide sources are fp32: ugpg_conv3x3_fwd)
                 hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 16, 8, false>), grid, block, 0, st, b);
-            } else if (f.nslab == 2) {
-                if (xb16) hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 8, true, 2>), grid, block, 0, st, b);
-                else hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 8, false, 2>), grid, block, 0, st, b);
-            } else if (f.th == 16) {
-                if (xb16) hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 16, true>), grid, block, 0, st, b);
-                else hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 16, false>), grid, block, 0, st, b);
+            } else if (f.nslab == 2 || f.th == 16) {
+                // the 4 x 2-tile forms: whole-line bf16 stores when the output allows them
+                const bool pair = X6R_PAIR16 && b.out0 == nullptr && b.out0_16 != nullptr &&
+                                  b.bnb_part == nullptr && !b.acc0 && b.split == b.Cout && b.W % 32 == 0;
+                if (f.nslab == 2) {
+                    if (pair && xb16) hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 8, true, 2, false, true>), grid, block, 0, st, b);
+                    else if (pair) hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 8, false, 2, false, true>), grid, block, 0, st, b);
+                    else if (xb16) hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 8, true, 2>), grid, block, 0, st, b);
+                    else hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 8, false, 2>), grid, block, 0, st, b);
+                } else {
+                    if (pair && xb16) hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 16, true, 1, false, true>), grid, block, 0, st, b);
+                    else if (pair) hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 16, false, 1, false, true>), grid, block, 0, st, b);
+                    else if (xb16) hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 16, true>), grid, block, 0, st, b);
+                    else hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 16, false>), grid, block, 0, st, b);
+                }
             } else if (X6R_RES_ON && a.Cin == 64 && a.Cout == 64) {  // resident weights
                 if (xb16) hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 8, true, 1, true>), grid, block, 0, st, b);
                 else hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 8, false, 1, true>), grid, block, 0, st, b);
