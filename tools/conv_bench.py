@@ -91,7 +91,11 @@ def main():
             ops.set_conv_math(m)
             wpk = ops.pack_conv3x3(w, ops.conv_pack_k(cin), 0)
             wpk1 = ops.pack_conv3x3(w, real_cin, 1) if real_cin % 64 == 0 else None
-            nt = ops.conv_ntiles(B, H, H, cin, Cout, wpk)
+            nt = 0  # (slot counts may differ between the compared builds: the largest)
+            for _, L in libs:
+                if L is not None:
+                    lib._lib = L
+                nt = max(nt, ops.conv_ntiles(B, H, H, cin, Cout, wpk))
             st = torch.empty(3 * Cout * nt, device=dev)
 
             st16 = m == "bf16" and H >= 32 and cin >= 16
