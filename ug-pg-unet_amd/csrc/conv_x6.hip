@@ -2036,7 +2036,17 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
     // BatchNorm-backward dy, the y loads plus the max-pool route's pooled-gradient and argmax
     // loads (2 * DY_PER, an upper bound: issued only on routed launches).  Only counted waits
     // of earlier register sets use it (NSET > 1), which BN excludes today (static_assert below)
-    constexpr int LOADS = DY_PER + X_PER + 2 + (BN ? 3 * DY_PER : 0);
+    // O8: bf16 dy and activations (XB == 3, the bf16 arithmetic's weight gradient): 16-byte
+    // loads of 8 channels, 8 lanes per pixel -- 2 + 4 loads per step for the 64-pixel tile and
+    // its halo instead of 4 + 7 of 4 channels (the loaders spend 41-57 % of this form's loop
+    // issuing loads: profiles/r7c_x6w_stamps.txt) -- and 16-byte LDS record stores
+#ifndef X6W_O8  // (A/B build: -D X6W_O8=0, 8-byte loads of 4 channels)
+#define X6W_O8 1
+#endif
+    constexpr bool O8 = X6W_O8 && NP == 1 && XB16 && DB16 && !BN;
+    constexpr int DY_PER8 = (P * 8 + 255) / 256, X_O8 = NHALO * 8, X_PER8 = (X_O8 + 255) / 256;
+    static_assert(P * 8 % 256 == 0, "whole dy rounds");
+    constexpr int LOADS = O8 ? DY_PER8 + X_PER8 + 4 : DY_PER + X_PER + 2 + (BN ? 3 * DY_PER : 0);
     __shared__ __attribute__((aligned(16))) char smem[(2 * RECS + 1) * REC];
     char* const dummy = smem + 2 * RECS * REC;    // record for idle lanes' writes
 
@@ -2155,7 +2165,89 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
             xof_in[1][v] = idx < X_Q ? o * a.C1 : 0;
             xin_all |= (idx < X_Q ? 1u : 0u) << v;
         }
+        // O8 state: 8 bf16 per vector, the lane's 8 channels' activation coefficients
+        f32x4 rdy8[O8 ? NSET : 1][O8 ? DY_PER8 : 1], rx8[O8 ? NSET : 1][O8 ? X_PER8 : 1];
+        Act4 xa8[O8 ? NSET : 1][2];
+        int dof8_in[O8 ? DY_PER8 : 1], xof8_in[2][O8 ? X_PER8 : 1];
+        unsigned xin8_all = 0;
+        if constexpr (O8) {
+#pragma unroll
+            for (int v = 0; v < DY_PER8; ++v) {
+                const int p = (lt + v * 256) >> 3;
+                dof8_in[v] = ((p / TW) * a.W + p % TW) * a.Cout;
+            }
+#pragma unroll
+            for (int v = 0; v < X_PER8; ++v) {
+                const int idx = lt + v * 256;
+                const int hp = idx < X_O8 ? idx >> 3 : 0;
+                const int o = (hp / HWD - 1) * a.W + hp % HWD - 1;
+                xof8_in[0][v] = idx < X_O8 ? o * a.C0 : 0;
+                xof8_in[1][v] = idx < X_O8 ? o * a.C1 : 0;
+                xin8_all |= (idx < X_O8 ? 1u : 0u) << v;
+            }
+        }
+        auto gload8 = [&](const LCur& c, auto S) {
+            constexpr int st = decltype(S)::value;
+            const int co0 = c.nb * 64, ci0 = c.cb * 64;
+            const bool second = ci0 >= a.C0;
+            const __bf16* xsrc16 = second ? a.src1_16 : a.src0_16;
+            const float* xsc = second ? a.sc1 : a.sc0;
+            const float* xsh = second ? a.sh1 : a.sh0;
+            const int Cs = second ? a.C1 : a.C0, cbase = second ? ci0 - a.C0 : ci0;
+            const bool xon = xsc != nullptr;
+            xlo[st] = xon ? 0.f : -INFINITY;
+            const int o8 = (lt & 7) * 8;
+            const float* scp = (xon ? xsc : g_act_ones) + cbase + o8;
+            const float* shp = (xon ? xsh : g_act_zeros) + cbase + o8;
+            xa8[st][0].s = gld16(scp);
+            xa8[st][0].h = gld16(shp);
+            xa8[st][1].s = gld16(scp + 4);
+            xa8[st][1].h = gld16(shp + 4);
+            const int b = c.b, ty0 = c.ty0, tx0 = c.tx0;
+            int dof[DY_PER8], xof[X_PER8];
+            if (ty0 >= 1 && tx0 >= 1 && ty0 + TH + 1 <= a.H && tx0 + TW + 1 <= a.W) {
+                // interior tile (uniform): every dy pixel and halo pixel is in the image
+#pragma unroll
+                for (int v = 0; v < DY_PER8; ++v) dof[v] = dof8_in[v];
+#pragma unroll
+                for (int v = 0; v < X_PER8; ++v) xof[v] = second ? xof8_in[1][v] : xof8_in[0][v];
+                dvalid[st] = (1u << DY_PER8) - 1;
+                xvalid[st] = xin8_all;
+            } else {
+                dvalid[st] = 0;
+#pragma unroll
+                for (int v = 0; v < DY_PER8; ++v) {
+                    const int p = (lt + v * 256) >> 3;
+                    const int gy = ty0 + p / TW, gx = tx0 + p % TW;
+                    const bool ok = gy < a.H && gx < a.W;
+                    const int cy = min(gy, a.H - 1), cx = min(gx, a.W - 1);
+                    dof[v] = ((cy - ty0) * a.W + (cx - tx0)) * a.Cout;
+                    dvalid[st] |= (ok ? 1u : 0u) << v;
+                }
+                xvalid[st] = 0;
+#pragma unroll
+                for (int v = 0; v < X_PER8; ++v) {
+                    const int idx = lt + v * 256;
+                    const int hp = idx < X_O8 ? idx >> 3 : 0;
+                    const int gy = ty0 + hp / HWD - 1, gx = tx0 + hp % HWD - 1;
+                    const bool ok = idx < X_O8 && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
+                    const int cy = min(max(gy, 0), a.H - 1), cx = min(max(gx, 0), a.W - 1);
+                    xof[v] = ((cy - ty0) * a.W + (cx - tx0)) * Cs;
+                    xvalid[st] |= (ok ? 1u : 0u) << v;
+                }
+            }
+            const size_t dyo0 = ((size_t)(b * a.H + ty0) * a.W + tx0) * a.Cout + co0 + o8;
+            const size_t xb = ((size_t)(b * a.H + ty0) * a.W + tx0) * Cs + cbase + o8;
+#pragma unroll
+            for (int v = 0; v < DY_PER8; ++v) rdy8[st][v] = gld16(a.dy16 + dyo0 + dof[v]);
+#pragma unroll
+            for (int v = 0; v < X_PER8; ++v) rx8[st][v] = gld16(xsrc16 + xb + xof[v]);
+        };
         auto gload = [&](const LCur& c, auto S) {
+            if constexpr (O8) {
+                gload8(c, S);
+                return;
+            }
             constexpr int st = decltype(S)::value;
             const int co0 = c.nb * 64, ci0 = c.cb * 64;
             const bool second = ci0 >= a.C0;
@@ -2283,7 +2375,53 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
 #pragma unroll
             for (int k = 0; k < NP; ++k) *reinterpret_cast<u32x2*>(r + 128 * k) = pc[k];
         };
+        auto lstore8 = [&](int buf, auto S) {
+            constexpr int st = decltype(S)::value;
+            char* dys = smem + buf * RECS * REC;
+            char* xs = dys + P * REC;
+            // record layout [64 ch] bf16: lane (pixel, o) writes channels 8o..8o+7 (16 B; an
+            // 8-lane store group covers one pixel's 128 contiguous bytes: conflict-free)
+#pragma unroll
+            for (int v = 0; v < DY_PER8; ++v) {
+                const int idx = lt + v * 256;
+                const bool ok = (dvalid[st] >> v) & 1u;
+                u32x4 w = __builtin_bit_cast(u32x4, rdy8[st][v]);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) w[i] = ok ? w[i] : 0u;
+                *reinterpret_cast<u32x4*>(dys + (idx >> 3) * REC + (idx & 7) * 16) = w;
+            }
+            const bool act = xlo[st] > -INFINITY;  // (uniform) else the bits as they are
+#pragma unroll
+            for (int v = 0; v < X_PER8; ++v) {
+                const int idx = lt + v * 256;
+                const bool ok = (xvalid[st] >> v) & 1u;
+                u32x4 w = __builtin_bit_cast(u32x4, rx8[st][v]);
+                if (act) {
+                    f32x4 lo4, hi4;  // 8 bf16 widened (exact), activated, rounded back
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        lo4[2 * i] = __uint_as_float(w[i] << 16);
+                        lo4[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+                        hi4[2 * i] = __uint_as_float(w[2 + i] << 16);
+                        hi4[2 * i + 1] = __uint_as_float(w[2 + i] & 0xffff0000u);
+                    }
+                    lo4 = act_floor4(lo4, xa8[st][0], xlo[st]);
+                    hi4 = act_floor4(hi4, xa8[st][1], xlo[st]);
+                    u32x2 pl[1], ph[1];
+                    split_n4<1>(lo4, pl);
+                    split_n4<1>(hi4, ph);
+                    w = u32x4{pl[0].x, pl[0].y, ph[0].x, ph[0].y};
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) w[i] = ok ? w[i] : 0u;
+                *reinterpret_cast<u32x4*>((idx < X_O8 ? xs + (idx >> 3) * REC : dummy) + (idx & 7) * 16) = w;
+            }
+        };
         auto lstore = [&](int buf, auto S) {
+            if constexpr (O8) {
+                lstore8(buf, S);
+                return;
+            }
             constexpr int st = decltype(S)::value;
             char* dys = smem + buf * RECS * REC;
             char* xs = dys + P * REC;
