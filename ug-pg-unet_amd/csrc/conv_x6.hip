@@ -2039,7 +2039,7 @@ __global__ void __launch_bounds__(512, 1) conv3x3_wgrad_x6w_kernel(WgradArgs a) 
     // O8: bf16 dy and activations (XB == 3, the bf16 arithmetic's weight gradient): 16-byte
     // loads of 8 channels, 8 lanes per pixel -- 2 + 4 loads per step for the 64-pixel tile and
     // its halo instead of 4 + 7 of 4 channels (the loaders spend 41-57 % of this form's loop
-    // issuing loads: profiles/r7c_x6w_stamps.txt) -- and 16-byte LDS record stores
+    // issuing loads: profiles/r7c_ab_x6w_o8.txt) -- and 16-byte LDS record stores
 #ifndef X6W_O8  // (A/B build: -D X6W_O8=0, 8-byte loads of 4 channels)
 #define X6W_O8 1
 #endif
