@@ -204,6 +204,10 @@ template <bool STORE>
 __global__ void __launch_bounds__(256)
     maxpool2_bwd_bnb_kernel(const float* dout, const uint8_t* am, int B, int H, int W, int C,
                             float* din, int acc, BnbArgs bnb) {
+    // U pixels' loads go out before the first is used, with 32-bit pixel coordinates (the
+    // host requires B*H*W < 2^31): the four 64-bit divisions per pixel and one pixel's loads
+    // in flight per thread held the pass at 4.75-5.07 TB/s.  Same sums in the same order.
+    constexpr int U = 4;
     const int Ho = H / 2, Wo = W / 2, c4n = C / 4, slots = 256 / c4n;
     const int tid = threadIdx.x, q = tid % c4n, slot = tid / c4n, c = 4 * q;
     const int64_t npix = (int64_t)B * H * W;
@@ -211,26 +215,38 @@ __global__ void __launch_bounds__(256)
     st.init(bnb, c);
     if (slot < slots) {
         const int64_t p0 = blockIdx.x * bnb.ppb, p1 = min(npix, p0 + bnb.ppb);
-        for (int64_t p = p0 + slot; p < p1; p += slots) {
-            const int x = (int)(p % W);
-            const int64_t r = p / W;
-            const int yy = (int)(r % H), b = (int)(r / H);
-            const int oy = yy >> 1, ox = x >> 1;
-            f32x4 g = {0.f, 0.f, 0.f, 0.f};
-            if (oy < Ho && ox < Wo) {
-                const int k = (yy & 1) * 2 + (x & 1);
-                const size_t o = ((size_t)(b * Ho + oy) * Wo + ox) * C + c;
-                const f32x4 d = *reinterpret_cast<const f32x4*>(dout + o);
-                const uchar4 m = *reinterpret_cast<const uchar4*>(am + o);
-                g[0] = m.x == k ? d[0] : 0.f;
-                g[1] = m.y == k ? d[1] : 0.f;
-                g[2] = m.z == k ? d[2] : 0.f;
-                g[3] = m.w == k ? d[3] : 0.f;
+        for (int64_t p = p0 + slot; p < p1; p += U * slots) {
+            f32x4 d[U], base[U], yv[U];
+            uchar4 m[U];
+            int k[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t pc = (uint32_t)min(p + u * slots, p1 - 1);  // (clamped: loads only)
+                const uint32_t x = pc % (uint32_t)W, r = pc / (uint32_t)W;
+                const uint32_t yy = r % (uint32_t)H, b = r / (uint32_t)H;
+                const uint32_t oy = yy >> 1, ox = x >> 1;
+                const bool in = oy < (uint32_t)Ho && ox < (uint32_t)Wo;
+                k[u] = in ? (int)((yy & 1) * 2 + (x & 1)) : -1;  // -1: outside the pooled area
+                const size_t o = in ? ((size_t)(b * Ho + oy) * Wo + ox) * C + c : (size_t)c;
+                d[u] = *reinterpret_cast<const f32x4*>(dout + o);
+                m[u] = *reinterpret_cast<const uchar4*>(am + o);
+                base[u] = acc ? *reinterpret_cast<const f32x4*>(din + (size_t)pc * C + c)
+                              : f32x4{0.f, 0.f, 0.f, 0.f};
+                yv[u] = bnb.y.ld4((size_t)pc * C + c);
             }
-            f32x4* dst = reinterpret_cast<f32x4*>(din + p * C + c);
-            if (acc) g += *dst;
-            if constexpr (STORE) *dst = g;
-            st.add(g, bnb.y.ld4(p * C + c));
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t pu = p + u * slots;
+                if (pu >= p1) break;
+                f32x4 g;
+                g[0] = m[u].x == k[u] ? d[u][0] : 0.f;
+                g[1] = m[u].y == k[u] ? d[u][1] : 0.f;
+                g[2] = m[u].z == k[u] ? d[u][2] : 0.f;
+                g[3] = m[u].w == k[u] ? d[u][3] : 0.f;
+                if (acc) g += base[u];
+                if constexpr (STORE) *reinterpret_cast<f32x4*>(din + pu * C + c) = g;
+                st.add(g, yv[u]);
+            }
         }
     }
     st.write(bnb, C);
@@ -525,15 +541,39 @@ __global__ void __launch_bounds__(256)
     float wy[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) wy[j] = ylo + j <= yhi ? ac_weight(ylo + j, iy, Hi, Ho) : 0.f;
+    // the column ranges and weights of the row's input columns, once per workgroup (C/4
+    // threads shared each column's, and evaluated it per element: ac_range_tight's loops and
+    // ac_weight's index arithmetic made this pass VALU-bound); the same values, so the same sums
+    constexpr int TAB = 256;
+    __shared__ int txlo[TAB], txhi[TAB];
+    __shared__ float twx[4][TAB];
+    const bool tab = Wi <= TAB;  // (uniform)
+    if (tab) {
+        for (int ix = threadIdx.x; ix < Wi; ix += blockDim.x) {
+            int xlo, xhi;
+            ac_range_tight(ix, Wi, Wo, xlo, xhi);
+            txlo[ix] = xlo;
+            txhi[ix] = xhi;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) twx[k][ix] = xlo + k <= xhi ? ac_weight(xlo + k, ix, Wi, Wo) : 0.f;
+        }
+        __syncthreads();
+    }
     for (int t = threadIdx.x; t < n; t += blockDim.x) {
         const int c = (t % C4) * 4, ix = t / C4;
         int xlo, xhi;
-        ac_range_tight(ix, Wi, Wo, xlo, xhi);
+        if (tab) {
+            xlo = txlo[ix];
+            xhi = txhi[ix];
+        } else {
+            ac_range_tight(ix, Wi, Wo, xlo, xhi);
+        }
         f32x4 s = {0.f, 0.f, 0.f, 0.f};
         if (yhi - ylo <= 3 && xhi - xlo <= 3) {
             float wx[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) wx[k] = xlo + k <= xhi ? ac_weight(xlo + k, ix, Wi, Wo) : 0.f;
+            for (int k = 0; k < 4; ++k)
+                wx[k] = tab ? twx[k][ix] : xlo + k <= xhi ? ac_weight(xlo + k, ix, Wi, Wo) : 0.f;
             f32x4 d[4][4];
 #pragma unroll
             for (int j = 0; j < 4; ++j)
@@ -1718,7 +1758,7 @@ extern "C" int ugpg_maxpool2_bwd_bnb(const float* dout, const uint8_t* am, int B
                                      void* stream) {
     BnbArgs b;
     UGPG_REQUIRE(dout && am && din && B > 0 && H > 0 && W > 0 &&
-                     bnb_args(bnb, (int64_t)B * H * W, C, b),
+                     (int64_t)B * H * W < (int64_t(1) << 31) && bnb_args(bnb, (int64_t)B * H * W, C, b),
                  "maxpool2_bwd_bnb");
     hipLaunchKernelGGL(maxpool2_bwd_bnb_kernel<true>, dim3(b.nblk), dim3(256), 0,
                        as_stream(stream), dout, am, B, H, W, C, din, acc, b);
@@ -1730,7 +1770,7 @@ extern "C" int ugpg_maxpool2_bwd_partials(const float* dout, const uint8_t* am, 
                                           const ugpg_bnb_t* bnb, void* stream) {
     BnbArgs b;
     UGPG_REQUIRE(dout && am && B > 0 && H > 0 && W > 0 &&
-                     bnb_args(bnb, (int64_t)B * H * W, C, b),
+                     (int64_t)B * H * W < (int64_t(1) << 31) && bnb_args(bnb, (int64_t)B * H * W, C, b),
                  "maxpool2_bwd_partials");
     hipLaunchKernelGGL(maxpool2_bwd_bnb_kernel<false>, dim3(b.nblk), dim3(256), 0,
                        as_stream(stream), dout, am, B, H, W, C, const_cast<float*>(din_base),
