@@ -18,21 +18,23 @@ CSRC = ROOT / "ug-pg-unet_amd" / "csrc"
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 X6R = "_ZN4ugpg22conv3x3_fwd_x6r_kernelIL{}EEEvNS_11ConvFwdArgsE"  # (last: PAIR)
 KERNELS = [
-    X6R.format("i3ELb1ELi32ELi8ELb0ELi1ELb0ELb0"),
-    X6R.format("i3ELb1ELi16ELi8ELb0ELi1ELb0ELb0"),
-    X6R.format("i1ELb0ELi32ELi8ELb0ELi1ELb0ELb0"),
-    X6R.format("i1ELb0ELi32ELi8ELb1ELi1ELb0ELb0"),
-    X6R.format("i1ELb0ELi32ELi8ELb0ELi2ELb0ELb0"),    # single-piece 256 x 128 items
-    X6R.format("i1ELb0ELi32ELi8ELb1ELi2ELb0ELb0"),
-    X6R.format("i1ELb0ELi32ELi16ELb0ELi1ELb0ELb0"),   # single-piece 512 x 64 items
-    X6R.format("i1ELb0ELi32ELi16ELb1ELi1ELb0ELb0"),
-    X6R.format("i1ELb0ELi32ELi8ELb0ELi1ELb1ELb0"),    # 256 x 64, K = 64: resident weights
-    X6R.format("i1ELb0ELi32ELi8ELb1ELi1ELb1ELb0"),
-    X6R.format("i1ELb0ELi16ELi8ELb0ELi1ELb0ELb0"),    # single-piece 8 x 16 items (16-wide images)
-    X6R.format("i1ELb0ELi32ELi8ELb0ELi2ELb0ELb1"),    # 4 x 2-tile forms, whole-line bf16 epilogue
-    X6R.format("i1ELb0ELi32ELi8ELb1ELi2ELb0ELb1"),
-    X6R.format("i1ELb0ELi32ELi16ELb0ELi1ELb0ELb1"),
-    X6R.format("i1ELb0ELi32ELi16ELb1ELi1ELb0ELb1"),
+    X6R.format("i3ELb1ELi32ELi8ELb0ELi1ELb0ELi0"),
+    X6R.format("i3ELb1ELi16ELi8ELb0ELi1ELb0ELi0"),
+    X6R.format("i1ELb0ELi32ELi8ELb0ELi1ELb0ELi0"),
+    X6R.format("i1ELb0ELi32ELi8ELb1ELi1ELb0ELi0"),
+    X6R.format("i1ELb0ELi32ELi8ELb0ELi2ELb0ELi0"),    # single-piece 256 x 128 items
+    X6R.format("i1ELb0ELi32ELi8ELb1ELi2ELb0ELi0"),
+    X6R.format("i1ELb0ELi32ELi16ELb0ELi1ELb0ELi0"),   # single-piece 512 x 64 items
+    X6R.format("i1ELb0ELi32ELi16ELb1ELi1ELb0ELi0"),
+    X6R.format("i1ELb0ELi32ELi8ELb0ELi1ELb1ELi0"),    # 256 x 64, K = 64: resident weights
+    X6R.format("i1ELb0ELi32ELi8ELb1ELi1ELb1ELi0"),
+    X6R.format("i1ELb0ELi16ELi8ELb0ELi1ELb0ELi0"),    # single-piece 8 x 16 items (16-wide images)
+    X6R.format("i1ELb0ELi32ELi8ELb0ELi2ELb0ELi1"),    # 4 x 2-tile forms, whole-line bf16 epilogue
+    X6R.format("i1ELb0ELi32ELi8ELb1ELi2ELb0ELi1"),
+    X6R.format("i1ELb0ELi32ELi16ELb0ELi1ELb0ELi1"),
+    X6R.format("i1ELb0ELi32ELi16ELb1ELi1ELb0ELi1"),
+    X6R.format("i1ELb0ELi32ELi8ELb1ELi2ELb0ELi2"),    # the same forms' data gradient with partials
+    X6R.format("i1ELb0ELi32ELi16ELb1ELi1ELb0ELi2"),
     "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi3ELi0ELb0EEEvNS_9WgradArgsE",
     "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi3ELi0ELb1EEEvNS_9WgradArgsE",  # lazy BN dy
     "_ZN4ugpg24conv3x3_wgrad_x6w_kernelILi4ELi16ELi1ELi0ELb0EEEvNS_9WgradArgsE",

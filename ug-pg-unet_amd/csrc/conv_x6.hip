@@ -445,6 +445,9 @@ __device__ unsigned long long g_epi[512 * 4];
 #ifndef X6R_PAIR16  // (A/B build: X6R_PAIR16=0, each n-tile through x6_epilogue_wave)
 #define X6R_PAIR16 1
 #endif
+#ifndef X6R_PAIR16_BNB  // (A/B build: X6R_PAIR16_BNB=0, data gradients with partials per n-tile)
+#define X6R_PAIR16_BNB 1
+#endif
 constexpr int X6_STG_PITCH = 40;
 constexpr int X6_STG_WAVE = 2048;  // floats: 32 x 40 fp32, or the bf16 y tile of 4 m-tiles
 // BatchNorm-backward partials with bf16 y: the item's y tile (MT m-tiles x 32 pixels x the
@@ -807,6 +810,103 @@ __device__ __forceinline__ void x6_epilogue_pair16(const ConvFwdArgs& a, f32x16 
     EPI_REC(et0, et1);
 }
 
+// The same forms' data-gradient epilogue with BatchNorm-backward partials (bf16-only da, bf16
+// y, no accumulate, full-width tile): pass 1 rounds both n-tiles and takes their partials
+// from the y tiles DMA'd into the two staging areas (x6_dma_bnb_y; each n-tile's values,
+// order and rounding exactly as x6_epilogue_wave's bnb path), pass 2 sends each m-tile out as
+// whole 128-B lines through the then free staging (as x6_epilogue_pair16)
+template <int TH, int TW, int MT, int WM>
+__device__ __forceinline__ void x6_epilogue_pair16_bnb(const ConvFwdArgs& a, f32x16 (&acc0)[MT],
+                                                       f32x16 (&acc1)[MT], int tile, int b, int ty0,
+                                                       int tx0, int c0, int wm, float* stg) {
+    static_assert(TW == 32, "one image row per 32-pixel MFMA tile");
+    constexpr int P = 32;
+    const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
+    const int vh = min(TH, a.H - ty0);
+    float* const stg1 = stg + X6_STG_WAVE + 4;
+    EPI_T(et0);
+    float sg[2] = {0.f, 0.f}, sgx[2] = {0.f, 0.f}, sx[2] = {0.f, 0.f};
+    vm_wait<0>();  // the staged y tiles have landed
+    auto pass1 = [&](f32x16 (&acc)[MT], int nt) {
+        const int n = c0 + 32 * nt + l32;
+        const float bv = a.bias ? a.bias[n] : 0.f;
+        const float mu = a.bnb_mean[n], is = a.bnb_invstd[n], sc = a.bnb_scale[n], sh = a.bnb_shift[n];
+        const __bf16* ys = reinterpret_cast<const __bf16*>(stg + nt * X6_STG_WAVE) + l32;
+        auto part = [&](float d, float y) {
+            const float gv = fmaf(y, sc, sh) > 0.f ? d : 0.f;
+            const float xh = (y - mu) * is;
+            sg[nt] += gv;
+            sgx[nt] = fmaf(gv, xh, sgx[nt]);
+            sx[nt] += xh;
+        };
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+            if (wm * MT + mt >= vh) break;  // uniform
+            const __bf16* t16 = ys + mt * 1024;
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) {
+                float v0 = acc[mt][r] + bv, v1 = acc[mt][r + 1] + bv;
+                pk_bf16(v0, v1, v0, v1);
+                acc[mt][r] = v0;
+                acc[mt][r + 1] = v1;
+                part(v0, (float)t16[((r & 3) + 8 * (r >> 2) + 4 * h) * 32]);
+                part(v1, (float)t16[(((r + 1) & 3) + 8 * ((r + 1) >> 2) + 4 * h) * 32]);
+            }
+            asm volatile("" ::: "memory");
+        }
+    };
+    pass1(acc0, 0);
+    pass1(acc1, 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // y reads done: the areas are free
+    auto pk = [](float x, float y) {
+        return (__builtin_bit_cast(unsigned, x) >> 16) | (__builtin_bit_cast(unsigned, y) & 0xffff0000u);
+    };
+    const int k = lane & 7;
+    const float* const sk = (k < 4 ? stg : stg1) + 8 * (k & 3);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        const int py = wm * MT + mt;
+        if (py >= vh) break;  // uniform
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+            const int p0 = (r & 3) + 8 * (r >> 2) + 4 * h;
+            stg[p0 * P + l32] = acc0[mt][r];
+            stg[(p0 + 1) * P + l32] = acc0[mt][r + 1];
+            stg1[p0 * P + l32] = acc1[mt][r];
+            stg1[(p0 + 1) * P + l32] = acc1[mt][r + 1];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const size_t rowb = (size_t)((b * a.H + ty0 + py) * a.W + tx0) * a.Cout + c0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int p = (lane >> 3) + 8 * j;
+            const f32x4 lo = *reinterpret_cast<const f32x4*>(sk + p * P);
+            const f32x4 hi = *reinterpret_cast<const f32x4*>(sk + p * P + 4);
+            const u32x4 w = {pk(lo.x, lo.y), pk(lo.z, lo.w), pk(hi.x, hi.y), pk(hi.z, hi.w)};
+            __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(a.out0_16 + rowb + (size_t)p * a.Cout + 8 * k));
+        }
+        asm volatile("" ::: "memory");
+    }
+    EPI_T(et1);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+        sg[nt] += __shfl_xor(sg[nt], 32, 64);
+        sgx[nt] += __shfl_xor(sgx[nt], 32, 64);
+        sx[nt] += __shfl_xor(sx[nt], 32, 64);
+    }
+    if (lane < 32) {
+        const size_t S = WM * (size_t)a.ntiles, slot = WM * (size_t)tile + wm;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+            const size_t n = c0 + 32 * nt + l32;
+            a.bnb_part[(0 * (size_t)a.Cout + n) * S + slot] = sg[nt];
+            a.bnb_part[(1 * (size_t)a.Cout + n) * S + slot] = sgx[nt];
+            a.bnb_part[(2 * (size_t)a.Cout + n) * S + slot] = sx[nt];
+        }
+    }
+    EPI_REC(et0, et1);
+}
+
 // Epilogue of the 16x16x32 form: acc[mt][nt] is D[oc][px] of m-tile mt (16 pixels:
 // image row wm*4 + mt/2, columns (mt&1)*16 + 0..15) and n-tile nt (16 channels); lane
 // (g, l) holds channels 4g..4g+3 of pixel l -> one 16-byte store per tile.  BatchNorm
@@ -1093,7 +1193,7 @@ extern "C" int ugpg_debug_clock(double* mhz) {
 // prologue; the loaders' steady state is halo loads and stores only (the row DMAs were 14-20 %
 // of their loop: profiles/r7a stamps)
 template <int NP, bool M16, int TWT = 32, int THT = 256 / TWT, bool XB16 = false, int NSLAB = 1,
-          bool RES = false, bool PAIR = false>
+          bool RES = false, int PAIR = 0>
 __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs a) {
     constexpr int NCW = 4;  // compute waves (one per SIMD) + 4 loader waves
     static_assert(!M16 || NP == 3, "the 16x16x32 form pairs the split-bf16 products");
@@ -1886,9 +1986,14 @@ __global__ void __launch_bounds__(8 * 64, 1) conv3x3_fwd_x6r_kernel(ConvFwdArgs 
                 // (host: bf16-only output, no accumulate, no BatchNorm-backward partials, W % 32
                 // == 0) both n-tiles as whole lines; only this epilogue is compiled in
                 static_assert(NP == 1 && NT == 2 && TW == 32, "the 4 x 2-tile single-piece forms");
-                CS_WAIT(cs_epi, (x6_epilogue_pair16<TH, TW, MT, WM>(
-                                    a, acc[0], acc[1], cp.tile, cp.b, cp.ty0, cp.tx0,
-                                    cp.nb * BNI + wn * NT * 32, wm, ostg + wave * NT * X6_STG_WAVE)));
+                if constexpr (PAIR == 2)  // (host: with BN-backward partials of a bf16 y)
+                    CS_WAIT(cs_epi, (x6_epilogue_pair16_bnb<TH, TW, MT, WM>(
+                                        a, acc[0], acc[1], cp.tile, cp.b, cp.ty0, cp.tx0,
+                                        cp.nb * BNI + wn * NT * 32, wm, ostg + wave * NT * X6_STG_WAVE)));
+                else
+                    CS_WAIT(cs_epi, (x6_epilogue_pair16<TH, TW, MT, WM>(
+                                        a, acc[0], acc[1], cp.tile, cp.b, cp.ty0, cp.tx0,
+                                        cp.nb * BNI + wn * NT * 32, wm, ostg + wave * NT * X6_STG_WAVE)));
             } else if constexpr (TW == 16) {
                 // 16-wide image (host: W == 16, H even): a 32-pixel m-tile is two whole image
                 // rows, so the NHWC addresses are those of a 32-wide image of half the rows --
@@ -3186,19 +3291,25 @@ int launch_fwd_x6(const ConvFwdArgs& a, int np, hipStream_t st) {
                 hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 16, 8, false>), grid, block, 0, st, b);
             } else if (f.nslab == 2 || f.th == 16) {
                 // the 4 x 2-tile forms: whole-line bf16 stores when the output allows them
+                // (with BN-backward partials: of a bf16 y, DMA'd into the staging areas)
                 const bool pair = X6R_PAIR16 && b.out0 == nullptr && b.out0_16 != nullptr &&
-                                  b.bnb_part == nullptr && !b.acc0 && b.split == b.Cout && b.W % 32 == 0;
+                                  (b.bnb_part == nullptr || (X6R_PAIR16_BNB && b.bnb_y.h)) && !b.acc0 &&
+                                  b.split == b.Cout && b.W % 32 == 0;
+                const int pr = !pair ? 0 : b.bnb_part ? 2 : 1;
+#define X6R_LW(TH_, XB_, NS_, PR_) \
+    hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, TH_, XB_, NS_, false, PR_>), grid, block, 0, st, b)
+#define X6R_LW3(TH_, XB_, NS_) \
+    do { if (pr == 2) X6R_LW(TH_, XB_, NS_, 2); else if (pr == 1) X6R_LW(TH_, XB_, NS_, 1); \
+         else X6R_LW(TH_, XB_, NS_, 0); } while (0)
                 if (f.nslab == 2) {
-                    if (pair && xb16) hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 8, true, 2, false, true>), grid, block, 0, st, b);
-                    else if (pair) hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 8, false, 2, false, true>), grid, block, 0, st, b);
-                    else if (xb16) hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 8, true, 2>), grid, block, 0, st, b);
-                    else hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 8, false, 2>), grid, block, 0, st, b);
+                    if (xb16) X6R_LW3(8, true, 2);
+                    else X6R_LW3(8, false, 2);
                 } else {
-                    if (pair && xb16) hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 16, true, 1, false, true>), grid, block, 0, st, b);
-                    else if (pair) hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 16, false, 1, false, true>), grid, block, 0, st, b);
-                    else if (xb16) hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 16, true>), grid, block, 0, st, b);
-                    else hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 16, false>), grid, block, 0, st, b);
+                    if (xb16) X6R_LW3(16, true, 1);
+                    else X6R_LW3(16, false, 1);
                 }
+#undef X6R_LW3
+#undef X6R_LW
             } else if (X6R_RES_ON && a.Cin == 64 && a.Cout == 64) {  // resident weights
                 if (xb16) hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 8, true, 1, true>), grid, block, 0, st, b);
                 else hipLaunchKernelGGL((conv3x3_fwd_x6r_kernel<1, false, 32, 8, false, 1, true>), grid, block, 0, st, b);
