@@ -698,37 +698,47 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* part, co
     }
 }
 
-// The same reduction for few splits (<= 16: the wide-channel layers, large slabs): a
-// thread owns 4 consecutive (co, ci) elements for all 9 taps and sums the splits in
-// order, so its 36 results are one contiguous OIHW run (wgrad_reduce_kernel's writes
-// there are 4 B at a 36-B stride, each line assembled by blocks on different XCDs).
-__global__ void __launch_bounds__(256) wgrad_reduce_few_kernel(const float* part, int nsplit,
+// The same reduction for few splits (<= 16: the wide-channel layers, large slabs), each
+// (element, tap) summed over the splits in order, written as contiguous OIHW runs
+// (wgrad_reduce_kernel's writes there are 4 B at a 36-B stride, each line assembled by
+// blocks on different XCDs).
+// Block = 64 consecutive element quads x the 9 taps (wave t = tap t: coalesced reads of one
+// tap plane); the quads' 9-tap sums meet in LDS and leave as the block's 2304 contiguous OIHW
+// floats (one f32x4 per thread).  (A thread per quad with all 9 taps -- 4 waves per CU at
+// 512 x 512 -- ran at 3.4 TB/s.)
+__global__ void __launch_bounds__(576) wgrad_reduce_few_kernel(const float* part, int nsplit,
                                                                int Cout, int Cin, float* dw,
                                                                int accumulate) {
-    const int64_t m4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // 4 (co, ci) elements
-    const int64_t nm = (int64_t)Cout * Cin, n4 = nm / 4;
-    if (m4 >= n4) return;
-    const f32x4* p = reinterpret_cast<const f32x4*>(part);
-    f32x4 s[9];
+    __shared__ f32x4 sm[64][9];
+    const int l = threadIdx.x & 63, t = threadIdx.x >> 6;
+    const int64_t n4 = (int64_t)Cout * Cin / 4, m4 = (int64_t)blockIdx.x * 64 + l;
+    if (m4 < n4) {
+        const f32x4* p = reinterpret_cast<const f32x4*>(part) + (size_t)t * n4 + m4;
+        // every split's load in flight, then the sum in split order (nsplit <= 16)
+        f32x4 v[16];
 #pragma unroll
-    for (int t = 0; t < 9; ++t) s[t] = p[(size_t)t * n4 + m4];
-    for (int k = 1; k < nsplit; ++k) {
-        const f32x4* q = p + (size_t)k * 9 * n4;
+        for (int k = 0; k < 16; ++k)
+            if (k < nsplit) v[k] = p[(size_t)k * 9 * n4];
+        f32x4 s = v[0];
 #pragma unroll
-        for (int t = 0; t < 9; ++t) s[t] += q[(size_t)t * n4 + m4];
+        for (int k = 1; k < 16; ++k)
+            if (k < nsplit) s += v[k];
+        sm[l][t] = s;
     }
-    // element e = 4*m4 + j, tap t -> dw[e*9 + t]: 36 consecutive floats
-    f32x4* o = reinterpret_cast<f32x4*>(dw + (size_t)m4 * 36);
-#pragma unroll
-    for (int v = 0; v < 9; ++v) {
+    __syncthreads();
+    // element e = 4*m4 + j, tap t -> dw[e*9 + t]: the block's 64 quads are 2304 floats
+    const int64_t f0 = (int64_t)blockIdx.x * 64 * 36, nf = n4 * 36;
+    const int i = threadIdx.x;  // f32x4 i of the block's run
+    if (f0 + 4 * i < nf) {
         f32x4 r;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int f = 4 * v + i, j = f / 9, t = f % 9;
-            r[i] = s[t][j];
+        for (int u = 0; u < 4; ++u) {
+            const int f = 4 * i + u, e = f / 9, tt = f % 9;
+            r[u] = sm[e >> 2][tt][e & 3];
         }
-        if (accumulate) r += o[v];
-        o[v] = r;
+        f32x4* o = reinterpret_cast<f32x4*>(dw + f0) + i;
+        if (accumulate) r += *o;
+        *o = r;
     }
 }
 
@@ -1251,7 +1261,7 @@ extern "C" int ugpg_conv3x3_wgrad(const ugpg_wgrad_t* p, void* ws, size_t ws_byt
     if (w.nsplit <= 16 && Cr == Cin && !p->db && ((int64_t)p->Cout * Cin) % 4 == 0 &&
         reinterpret_cast<uintptr_t>(p->dw) % 16 == 0) {  // (dw may be a view of a flat buffer)
         const int64_t n4 = (int64_t)p->Cout * Cin / 4;
-        hipLaunchKernelGGL(wgrad_reduce_few_kernel, dim3((unsigned)cdiv(n4, 256)), dim3(256), 0, st,
+        hipLaunchKernelGGL(wgrad_reduce_few_kernel, dim3((unsigned)cdiv(n4, 64)), dim3(576), 0, st,
                            a.part, w.nsplit, p->Cout, Cin, p->dw, p->accumulate);
         return check_launch("conv3x3_wgrad_reduce");
     }
